@@ -1,0 +1,222 @@
+/*
+ * surf_hip.h -- C-ABI of the MI355X-native wavefront path tracer.
+ *
+ * This is the drop-in boundary for the reference's GPU path
+ * (nemjit001/surf-path-tracer).  Each entry point names the reference
+ * interface it replaces (paths relative to the reference repository root):
+ *
+ *   surf_create / surf_destroy      WaveFrontRenderer ctor/dtor (headers/renderer.h:211, sources/renderer.cpp:604-937)
+ *   surf_upload_scene               GPUScene ctor: the 9 SSBOs + scene UBO (headers/scene.h:94-122, sources/scene.cpp:159-258)
+ *   surf_update_instances           GPUScene::update re-upload (sources/scene.cpp:267-282)
+ *   surf_set_camera                 CameraUBO upload (sources/renderer.cpp:971-979, headers/camera.h:12-19)
+ *   surf_render                     WaveFrontRenderer::render dispatch loop (sources/renderer.cpp:1029-1118)
+ *   surf_clear_accumulator          IRenderer::clearAccumulator (headers/renderer.h:91, sources/renderer.cpp:927-937)
+ *   surf_read_accumulator           accumulator SSBO readback (headers/renderer.h:344-350)
+ *   surf_finalize_rgba8             wavefront_finalize.comp:15-26 (+ RgbaToU32 rounding, sources/surf_math.cpp:13-29)
+ *   surf_get_stats                  FrameInstrumentationData + Lumen energy (headers/renderer.h:30-34, sources/renderer.cpp:955-969)
+ *   surf_trace_closest / _any       ray_extend.comp / ray_connect.comp traversal, exposed for hit-record tests
+ *   surf_scene_build_indoor ...     host scene build of main.cpp:161-346 (Mesh/BvhBLAS/Instance/GPUBatcher)
+ *
+ * Conventions: every function returns 0 (SURF_OK) or a negative surf_status;
+ * nothing aborts.  A context belongs to one HIP device and is driven from one
+ * host thread.  Input records are byte-identical to the reference host structs
+ * (sizes asserted below); the library re-lays them out internally (SoA queues,
+ * child-box BVH nodes, BVH-ordered triangles).  Host buffers passed in are
+ * copied; the caller keeps ownership.
+ */
+#ifndef SURF_HIP_H
+#define SURF_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SURF_ABI_VERSION 1
+
+typedef enum {
+    SURF_OK = 0,
+    SURF_ERR_INVALID = -1,      /* bad argument / inconsistent scene */
+    SURF_ERR_HIP = -2,          /* HIP runtime error (see surf_last_error) */
+    SURF_ERR_NO_DEVICE = -3,    /* no gfx950 device at that index */
+    SURF_ERR_NO_SCENE = -4,     /* render before upload */
+    SURF_ERR_OOM = -5,          /* device allocation failed */
+    SURF_ERR_IO = -6,           /* asset file unreadable */
+    SURF_ERR_LIMIT = -7         /* scene exceeds a compiled limit (stack depth) */
+} surf_status;
+
+/* ---- reference record layouts (byte-identical; offsets in comments) ---- */
+
+typedef struct { float x, y, z, _pad; } surf_float3_16;         /* ALIGN(16) Float3 slot */
+
+typedef struct {                                                /* Triangle, mesh.h:14-25 (64 B) */
+    surf_float3_16 v0, v1, v2, centroid;                        /* v0 = OBJ vertex 1, v1 = OBJ vertex 0 */
+} surf_triangle;
+
+typedef struct {                                                /* TriExtension, mesh.h:26-30 (80 B) */
+    surf_float3_16 n0, n1, n2;                                  /* @0 @16 @32 */
+    float uv0[2], uv1[2], uv2[2];                               /* @48 @56 @64 */
+    float _pad[2];
+} surf_tri_extension;
+
+typedef struct {                                                /* BvhNode, bvh.h:36-46 (48 B) */
+    uint32_t left_first, count, _pad[2];                        /* leaf iff count != 0 */
+    surf_float3_16 bb_min, bb_max;                              /* @16 @32 */
+} surf_bvh_node;
+
+typedef struct {                                                /* Material, material.h:6-19 (64 B) */
+    float emission_strength, reflectivity, refractivity, index_of_refraction;
+    surf_float3_16 emission_color, albedo, absorption;          /* @16 @32 @48 */
+} surf_material;
+
+typedef struct {                                                /* GPUInstance, bvh.h:93-102 (160 B) */
+    uint32_t tri_offset, bvh_idx_offset, bvh_node_offset, material_offset;
+    float area;                                                 /* @16 */
+    uint32_t _pad[3];
+    float transform[16];                                        /* @32, glm column major */
+    float inv_transform[16];                                    /* @96 */
+} surf_gpu_instance;
+
+typedef struct {                                                /* GPULightData, scene.h:67-71 (8 B) */
+    uint32_t light_instance_idx, primitive_count;
+} surf_light;
+
+typedef struct {                                                /* SceneBackground, scene.h:18-26 (64 B) */
+    uint32_t type;                                              /* 0 solid, 1 gradient */
+    uint32_t _pad[3];
+    surf_float3_16 color, gradient_a, gradient_b;               /* @16 @32 @48 */
+} surf_background;
+
+typedef struct {                                                /* CameraUBO, camera.h:12-19 (128 B) */
+    surf_float3_16 position, up, fwd, right;                    /* @0 @16 @32 @48 */
+    surf_float3_16 first_pixel, u_vector, v_vector;             /* @64 @80 @96 */
+    float resolution[2];                                        /* @112 */
+    float focal_length, defocus_angle;                          /* @120 @124 */
+} surf_camera_ubo;
+
+/* GPUScene's nine buffers + scene UBO (scene.h:113-122), host pointers. */
+typedef struct {
+    const surf_triangle* triangles;       uint32_t triangle_count;
+    const surf_tri_extension* tri_ext;    /* triangle_count records */
+    const uint32_t* blas_indices;         uint32_t blas_index_count;
+    const surf_bvh_node* blas_nodes;      uint32_t blas_node_count;
+    const surf_material* materials;       uint32_t material_count;
+    const surf_gpu_instance* instances;   uint32_t instance_count;
+    const uint32_t* tlas_indices;         /* instance_count records */
+    const surf_bvh_node* tlas_nodes;      uint32_t tlas_node_count;
+    const surf_light* lights;             uint32_t light_count;
+    const surf_background* background;
+} surf_scene_desc;
+
+typedef struct {
+    uint64_t samples;          /* camera samples finished (Mrays/s numerator, main.cpp:431) */
+    uint64_t n_ext;            /* extension rays traced */
+    uint64_t n_hit;            /* extension rays that hit geometry */
+    uint64_t n_cont;           /* continuation rays */
+    uint64_t n_shadow;         /* shadow rays traced */
+    uint64_t n_acc;            /* radiance contributions */
+    uint64_t n_unocc;          /* unoccluded shadow rays */
+    uint64_t iterations;       /* wavefront iterations (extend->shade->connect->regen) */
+    uint64_t tail_paths;       /* paths finished by the tail kernel */
+    double   ms_total;         /* device time of the last surf_render */
+    double   ms_extend, ms_shade, ms_connect, ms_regen, ms_tail, ms_accum;  /* per-kernel (surf_set_profiling) */
+    uint64_t launches_extend;  /* extend launches that did work (profiling mode) */
+    uint32_t stack_depth;      /* traversal stack entries reserved per ray */
+    uint32_t pool_capacity;    /* paths in flight */
+    float    energy;           /* sum of acc.rgb / samples over the shard ("Lumen", renderer.cpp:191-201) */
+    uint32_t _pad;
+} surf_stats;
+
+typedef struct surf_ctx surf_ctx;       /* one per HIP device */
+typedef struct surf_scene surf_scene;   /* host-side scene built by this library */
+
+/* ---- version / device ---- */
+int surf_abi_version(void);
+int surf_device_count(int* count);
+
+/* ---- context ----
+ * Renders rows [row_begin, row_end) of a width x height frame (one shard). */
+int surf_create(int hip_device, uint32_t width, uint32_t height,
+                uint32_t row_begin, uint32_t row_end, surf_ctx** out);
+/* Interleaved row blocks: block b = rows [b*row_block, (b+1)*row_block) goes to
+ * shard b % shard_count. row_block 0 = contiguous split. */
+int surf_create_sharded(int hip_device, uint32_t width, uint32_t height,
+                        uint32_t shard_index, uint32_t shard_count, uint32_t row_block,
+                        surf_ctx** out);
+void surf_destroy(surf_ctx* ctx);
+const char* surf_last_error(const surf_ctx* ctx);   /* ctx may be NULL: last global error */
+/* Rows of this shard in shard order (row_count from surf_shard_rows(ctx, NULL, &n)). */
+int surf_shard_rows(const surf_ctx* ctx, uint32_t* rows, uint32_t* row_count);
+
+/* Paths in flight (default: sized from the shard, >= 1M when possible). Must be
+ * called before the first render. */
+int surf_set_pool_capacity(surf_ctx* ctx, uint32_t paths);
+/* Frames rendered concurrently per internal batch (default 16). */
+int surf_set_frame_batch(surf_ctx* ctx, uint32_t frames);
+/* When enabled, per-kernel device times are measured with HIP events on the
+ * render stream (slower: disables the graph replay). */
+int surf_set_profiling(surf_ctx* ctx, int enabled);
+
+/* ---- scene / camera ---- */
+int surf_upload_scene(surf_ctx* ctx, const surf_scene_desc* desc);
+/* Replaces instances + TLAS (same BLASes/materials): the animation re-upload. */
+int surf_update_instances(surf_ctx* ctx, const surf_gpu_instance* instances, uint32_t instance_count,
+                          const uint32_t* tlas_indices, const surf_bvh_node* tlas_nodes, uint32_t tlas_node_count,
+                          const surf_light* lights, uint32_t light_count);
+int surf_set_camera(surf_ctx* ctx, const surf_camera_ubo* camera);
+
+/* ---- rendering ----
+ * Renders `frames` frames of one sample per pixel each; frame k is seeded
+ * initSeed(pixel + 1799 * (first_frame_index + k)) like the CPU renderer
+ * (renderer.cpp:169) and accumulates (rgb, 1) per sample in frame order.
+ * max_segments: 0 = unbounded + Russian roulette (reference semantics);
+ * N > 0 caps each path at N extension rays.  samples_per_frame must be 1
+ * (multi-sample frames are expressed as consecutive frames). */
+int surf_render(surf_ctx* ctx, uint32_t frames, uint32_t first_frame_index,
+                uint32_t max_segments, uint32_t samples_per_frame);
+int surf_clear_accumulator(surf_ctx* ctx);
+/* Float RGBA accumulator of this shard's rows, shard order, rows*width*4 floats. */
+int surf_read_accumulator(surf_ctx* ctx, float* rgba_rows);
+/* Device-to-device copy of the accumulator into dst (a device pointer on the
+ * same device, rows*width*16 bytes): feeds the RCCL gather. */
+int surf_copy_accumulator_device(surf_ctx* ctx, void* dst_device);
+/* RGBA8 of acc / total samples with RgbaToU32 rounding, rows*width words. */
+int surf_finalize_rgba8(surf_ctx* ctx, uint32_t* out_rgba8);
+int surf_get_stats(surf_ctx* ctx, surf_stats* out);
+int surf_synchronize(surf_ctx* ctx);
+
+/* ---- traversal entry points (kernel-level parity tests) ----
+ * n world-space rays, o/d 3 floats each.  closest: depth starts at 1e30;
+ * writes t,u,v (floats) and inst,prim (u32, ~0 on miss).  any: tmax per ray,
+ * occluded[i] = 1 when a hit is found. Host buffers. */
+int surf_trace_closest(surf_ctx* ctx, uint32_t n, const float* o, const float* d,
+                       float* out_t, float* out_u, float* out_v, uint32_t* out_inst, uint32_t* out_prim);
+int surf_trace_any(surf_ctx* ctx, uint32_t n, const float* o, const float* d, const float* tmax,
+                   uint8_t* occluded);
+
+/* ---- host scene build (the reference's main.cpp scene, OBJ assets) ----
+ * variant 0: bundled indoor scene; 1: C5 deep scene (+648 Suzannes in one mesh). */
+int surf_scene_build_indoor(const char* assets_dir, int variant, surf_scene** out);
+int surf_scene_desc_get(const surf_scene* scene, surf_scene_desc* out);
+/* Reference camera of main.cpp:141-149 for a width x height render. */
+int surf_scene_camera(const surf_scene* scene, uint32_t width, uint32_t height, surf_camera_ubo* out);
+/* Deepest root-to-leaf edge counts of the TLAS and of all BLASes. */
+int surf_scene_bvh_depths(const surf_scene* scene, uint32_t* tlas_depth, uint32_t* max_blas_depth);
+void surf_scene_destroy(surf_scene* scene);
+
+#ifdef __cplusplus
+}  /* extern "C" */
+
+static_assert(sizeof(surf_triangle) == 64, "Triangle is 64 B");
+static_assert(sizeof(surf_tri_extension) == 80, "TriExtension is 80 B");
+static_assert(sizeof(surf_bvh_node) == 48, "BvhNode is 48 B");
+static_assert(sizeof(surf_material) == 64, "Material is 64 B");
+static_assert(sizeof(surf_gpu_instance) == 160, "GPUInstance is 160 B");
+static_assert(sizeof(surf_light) == 8, "GPULightData is 8 B");
+static_assert(sizeof(surf_background) == 64, "SceneBackground is 64 B");
+static_assert(sizeof(surf_camera_ubo) == 128, "CameraUBO is 128 B");
+#endif
+
+#endif /* SURF_HIP_H */

@@ -1,0 +1,47 @@
+/*
+ * oracle/cpu_ref_bench.cpp -- CLI around the CPU oracle: the timed CPU baseline
+ * (bench.py cpu_baseline leg) and a PFM writer for eyeballing renders.
+ * TEST INFRASTRUCTURE ONLY (see cpu_ref.h).
+ *
+ * usage: cpu_ref_bench ASSETS W H FRAMES [ROW_BEGIN ROW_END [MAX_SEG [THREADS [OUT.pfm]]]]
+ * prints one JSON line: samples, seconds, mrays_per_s, threads, event counts.
+ */
+#include "cpu_ref.h"
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include <omp.h>
+
+int main(int argc, char** argv) {
+    if (argc < 5) { fprintf(stderr, "usage: %s ASSETS W H FRAMES [ROW_BEGIN ROW_END [MAX_SEG [THREADS [OUT.pfm]]]]\n", argv[0]); return 2; }
+    const char* assets = argv[1];
+    uint32_t W = (uint32_t)atoi(argv[2]), H = (uint32_t)atoi(argv[3]), F = (uint32_t)atoi(argv[4]);
+    uint32_t r0 = argc > 6 ? (uint32_t)atoi(argv[5]) : 0, r1 = argc > 6 ? (uint32_t)atoi(argv[6]) : H;
+    uint32_t maxSeg = argc > 7 ? (uint32_t)atoi(argv[7]) : 0;
+    int threads = argc > 8 ? atoi(argv[8]) : 0;
+    const char* out = argc > 9 ? argv[9] : nullptr;
+    if (r1 > H || r0 >= r1 || W == 0 || F == 0) { fprintf(stderr, "bad arguments\n"); return 2; }
+    orc_scene* s = orc_scene_create(assets, 0);
+    if (!s) return 1;
+    std::vector<float> acc((size_t)(r1 - r0) * W * 4, 0.0f);
+    orc_counters c;
+    double sec = orc_render(s, W, H, r0, r1, 0, F, maxSeg, threads, acc.data(), &c);
+    int used = threads > 0 ? threads : omp_get_max_threads();
+    printf("{\"samples\": %llu, \"seconds\": %.6f, \"mrays_per_s\": %.4f, \"threads\": %d, "
+           "\"n_ext\": %llu, \"n_hit\": %llu, \"n_cont\": %llu, \"n_shadow\": %llu, \"n_acc\": %llu, \"n_unocc\": %llu, \"max_segments\": %llu}\n",
+           (unsigned long long)c.samples, sec, (double)c.samples / sec / 1e6, used,
+           (unsigned long long)c.n_ext, (unsigned long long)c.n_hit, (unsigned long long)c.n_cont,
+           (unsigned long long)c.n_shadow, (unsigned long long)c.n_acc, (unsigned long long)c.n_unocc,
+           (unsigned long long)c.max_segments);
+    if (out) {
+        FILE* f = fopen(out, "wb");
+        if (f) {
+            fprintf(f, "PF\n%u %u\n-1.0\n", W, r1 - r0);
+            for (int64_t y = (int64_t)(r1 - r0) - 1; y >= 0; --y)
+                for (uint32_t x = 0; x < W; ++x) { const float* a = &acc[4 * ((size_t)y * W + x)]; float rgb[3] = {a[0] / F, a[1] / F, a[2] / F}; fwrite(rgb, 4, 3, f); }
+            fclose(f);
+        }
+    }
+    orc_scene_destroy(s);
+    return 0;
+}

@@ -1,0 +1,549 @@
+/*
+ * wavefront_kernels.h -- the hot path: HIP kernels for gfx950 (CDNA4, wave64).
+ *
+ * Pipeline per wavefront iteration ("phase", parity par = phase & 1; pool[par]
+ * is read, pool[par^1] is written):
+ *
+ *   k_extend   closest hit of every path in pool[par]        ray_extend.comp:26-185
+ *   k_shade    material eval, NEE shadow-ray emission, RR,   ray_shade.comp:44-191
+ *              compacted append of continuing paths           (CPU oracle: renderer.cpp:336-460)
+ *   k_connect  any-hit of the shadow queue + contribution    ray_connect.comp:34-212
+ *   k_regen    refill pool[par^1] with new camera samples    ray_generation.comp:32-80
+ *
+ * plus k_accumulate (frame-ordered per-pixel sum, renderer.cpp:180) and
+ * k_finalize (wavefront_finalize.comp:15-26 with RgbaToU32 rounding).
+ *
+ * Semantics follow the reference CPU renderer (the parity target), not the
+ * GLSL: one RNG stream per (pixel, frame) carried in the path record, GCC
+ * argument order for the jitter/disk draws, CPU cosine-frame constants, queues
+ * drained completely (no WF_RAY_DIFF_THRESHOLD early exit), no racy
+ * accumulator updates (per-sample radiance slots, each written by one lane).
+ *
+ * Memory layout (HBM, SoA, 16-B aligned float4 records, coalesced per lane):
+ *   path pool   o  : float4(origin.xyz, sample id bits)
+ *               d  : float4(dir.xyz,    flags bits: b0 inMedium, b1 lastSpecular, b2.. segments)
+ *               T  : float4(transmission.xyz, rng state bits)
+ *   hit         tuv: float4(t, u, v, prim bits), inst: u32
+ *   shadow q.   o  : float4(origin.xyz, tmax), d: float4(dir.xyz, sample id bits), c: float4(T*Ld, 0)
+ *   radiance    float4 per sample of the frame batch (energy of the path)
+ */
+#pragma once
+#include <hip/hip_runtime.h>
+#include "surf_math.h"
+
+namespace surfdev {
+
+constexpr uint32_t kUnset = 0xffffffffu;
+constexpr uint32_t kFlagMedium = 1u, kFlagSpecular = 2u;
+constexpr int kBlock = 256;
+
+struct DevInstance {          /* 160 B */
+    float Minv[16];
+    float M[16];
+    uint32_t triOffset, idxOffset, nodeOffset, material;
+    float area;
+    uint32_t _pad[3];
+};
+
+struct DevMaterial {          /* = Material (64 B) */
+    float emit, refl, refr, ior;
+    float ec[4], albedo[4], absorb[4];
+};
+
+struct DevScene {
+    const float4* nodes;      /* BLAS: 4 float4 per node (see upload) */
+    const float4* tris;       /* 3 float4 per BLAS index slot: (v0, prim), e1, e2 */
+    const float4* normals;    /* 3 float4 per global triangle: n0, n1, n2 */
+    const float4* verts;      /* reference Triangle records (v0, v1, v2, centroid) */
+    const float4* tlasNodes;  /* 4 float4 per TLAS node */
+    const uint32_t* tlasIdx;
+    const DevInstance* inst;
+    const DevMaterial* mats;
+    const uint2* lights;      /* (instance, primitive count) */
+    uint32_t nLights;
+    uint32_t bgType;
+    float bgColor[3], bgA[3], bgB[3];
+};
+
+struct DevCamera {
+    float pos[3], firstPixel[3], uVec[3], vVec[3], diskU[3], diskV[3];
+    float invW, invH;
+    uint32_t defocus;
+};
+
+struct Pool { float4* o; float4* d; float4* T; };
+struct ShadowQ { float4* o; float4* d; float4* c; };
+
+/* Device counters of one frame batch.  Double-buffered by phase parity so no
+ * kernel writes a word another block of the same launch still reads. */
+struct Counters {
+    uint32_t nIn[2];          /* paths in pool[p] when a phase reads it */
+    uint32_t nApp[2];         /* continuation append cursor into pool[p] */
+    uint32_t ns[2];           /* next sample to generate (per parity) */
+    uint32_t nSh[2];          /* shadow queue length of phase parity p */
+    uint32_t total;           /* samples in this batch */
+    uint32_t firstFrame;      /* frame index of batch sample 0 */
+    uint32_t maxSeg;          /* 0 = unbounded */
+    uint32_t _pad[5];
+    unsigned long long ev[8]; /* ext, hit, cont, shadow, acc, unocc, tail, spare */
+};
+
+SURF_HD V3 ld3(const float* p) { return mk3(p[0], p[1], p[2]); }
+SURF_HD V3 xyz(float4 v) { return mk3(v.x, v.y, v.z); }
+
+/* ------------------------------------------------------------------ traversal
+ * Stack in LDS: entry k of thread t at stk[k * stride] (stk = lds + t,
+ * stride = blockDim.x) -> consecutive lanes hit consecutive banks.
+ * BvhBLAS::intersect / intersectAny (bvh.cpp:129-253): near child first
+ * (left unless dist(left) > dist(right)), far child pushed when it hits,
+ * leaves in index order, LIFO pops.  Node record (64 B) of node n holds its
+ * own leftFirst/count and, if interior, both children's boxes:
+ *   q0 = (left.min.xyz,  leftFirst)   q1 = (left.max.xyz,  count)
+ *   q2 = (right.min.xyz, 0)           q3 = (right.max.xyz, 0)          */
+template <bool ANY>
+__device__ __forceinline__ bool blasTrace(const DevScene& S, const DevInstance& I, V3 o, V3 d, float& depth,
+                                          float& hu, float& hv, uint32_t& hprim,
+                                          uint32_t* stk, uint32_t stride, uint32_t base) {
+    const V3 rd = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    const uint32_t nodeOff = I.nodeOffset;
+    const float4* tri = S.tris + 3u * I.idxOffset;
+    uint32_t sp = base;
+    uint32_t node = nodeOff;
+    bool any = false;
+    for (;;) {
+        const float4* nd = S.nodes + 4u * node;
+        const float4 q0 = nd[0], q1 = nd[1];
+        const uint32_t lf = f2u(q0.w), cnt = f2u(q1.w);
+        if (cnt != 0u) {
+            for (uint32_t k = 0; k < cnt; ++k) {
+                const float4 a = tri[3u * (lf + k)], b = tri[3u * (lf + k) + 1u], c = tri[3u * (lf + k) + 2u];
+                float u, v;
+                if (triHit(xyz(a), xyz(b), xyz(c), o, d, depth, u, v)) {
+                    if (ANY) return true;
+                    any = true;
+                    hu = u; hv = v; hprim = f2u(a.w);
+                }
+            }
+            if (sp == base) break;
+            node = stk[(--sp) * stride];
+            continue;
+        }
+        const float4 q2 = nd[2], q3 = nd[3];
+        float dn = slab(q0.x, q0.y, q0.z, q1.x, q1.y, q1.z, o, rd, depth);
+        float df = slab(q2.x, q2.y, q2.z, q3.x, q3.y, q3.z, o, rd, depth);
+        uint32_t cn = nodeOff + lf, cf = cn + 1u;
+        if (dn > df) { const float t = dn; dn = df; df = t; const uint32_t c = cn; cn = cf; cf = c; }
+        if (dn == kFarAway) {
+            if (sp == base) break;
+            node = stk[(--sp) * stride];
+        } else {
+            node = cn;
+            if (df != kFarAway) stk[(sp++) * stride] = cf;
+        }
+    }
+    return any;
+}
+
+/* BvhTLAS::intersect / intersectAny (bvh.cpp:654-778) with the instance
+ * transform of Instance::intersect(Any) (bvh.cpp:481-513): origin
+ * (M^-1 (o,1)).xyz / w, direction (M^-1 (d,0)).xyz, not renormalized. */
+template <bool ANY>
+__device__ __forceinline__ bool traceScene(const DevScene& S, V3 o, V3 d, float& depth, float& hu, float& hv,
+                                           uint32_t& hinst, uint32_t& hprim, uint32_t* stk, uint32_t stride) {
+    const V3 rd = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    uint32_t sp = 0, node = 0;
+    bool any = false;
+    for (;;) {
+        const float4* nd = S.tlasNodes + 4u * node;
+        const float4 q0 = nd[0], q1 = nd[1];
+        const uint32_t lf = f2u(q0.w), cnt = f2u(q1.w);
+        if (cnt != 0u) {
+            for (uint32_t k = 0; k < cnt; ++k) {
+                const uint32_t ii = S.tlasIdx[lf + k];
+                const DevInstance& I = S.inst[ii];
+                const float* m = I.Minv;
+                const float w = mrow(m, 3, o.x, o.y, o.z, 1.0f);
+                const V3 oo = divs(mk3(mrow(m, 0, o.x, o.y, o.z, 1.0f), mrow(m, 1, o.x, o.y, o.z, 1.0f),
+                                       mrow(m, 2, o.x, o.y, o.z, 1.0f)), w);
+                const V3 dd = mk3(mrow(m, 0, d.x, d.y, d.z, 0.0f), mrow(m, 1, d.x, d.y, d.z, 0.0f),
+                                  mrow(m, 2, d.x, d.y, d.z, 0.0f));
+                if (blasTrace<ANY>(S, I, oo, dd, depth, hu, hv, hprim, stk, stride, sp)) {
+                    if (ANY) return true;
+                    any = true;
+                    hinst = ii;
+                }
+            }
+            if (sp == 0) break;
+            node = stk[(--sp) * stride];
+            continue;
+        }
+        const float4 q2 = nd[2], q3 = nd[3];
+        float dn = slab(q0.x, q0.y, q0.z, q1.x, q1.y, q1.z, o, rd, depth);
+        float df = slab(q2.x, q2.y, q2.z, q3.x, q3.y, q3.z, o, rd, depth);
+        uint32_t cn = lf, cf = lf + 1u;
+        if (dn > df) { const float t = dn; dn = df; df = t; const uint32_t c = cn; cn = cf; cf = c; }
+        if (dn == kFarAway) {
+            if (sp == 0) break;
+            node = stk[(--sp) * stride];
+        } else {
+            node = cn;
+            if (df != kFarAway) stk[(sp++) * stride] = cf;
+        }
+    }
+    return any;
+}
+
+/* --------------------------------------------------------------- wave helpers */
+__device__ __forceinline__ uint32_t laneId() { return __lane_id(); }
+__device__ __forceinline__ uint32_t rankBelow(unsigned long long mask) {
+    return (uint32_t)__popcll(mask & ((1ull << laneId()) - 1ull));
+}
+/* One atomic per wave reserves `popc(mask)` slots; returns this lane's slot. */
+__device__ __forceinline__ uint32_t waveAppend(uint32_t* counter, unsigned long long mask) {
+    uint32_t base = 0;
+    if (laneId() == 0 && mask) base = atomicAdd(counter, (uint32_t)__popcll(mask));
+    base = (uint32_t)__shfl((int)base, 0);
+    return base + rankBelow(mask);
+}
+__device__ __forceinline__ void waveCount(unsigned long long* ctr, unsigned long long v) {
+    if (laneId() == 0 && v) atomicAdd(ctr, v);
+}
+
+/* ------------------------------------------------------------------ kernels */
+__global__ __launch_bounds__(kBlock) void k_extend(DevScene S, Pool cur, float4* __restrict__ hitTUV,
+                                                   uint32_t* __restrict__ hitInst, const Counters* C, int par) {
+    extern __shared__ uint32_t lds[];
+    const uint32_t n = C->nIn[par];
+    const uint32_t stride = blockDim.x;
+    uint32_t* stk = lds + threadIdx.x;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const float4 o = cur.o[i], d = cur.d[i];
+        float depth = kFarAway, u = 0.0f, v = 0.0f;
+        uint32_t inst = kUnset, prim = kUnset;
+        const bool hit = traceScene<false>(S, xyz(o), xyz(d), depth, u, v, inst, prim, stk, stride);
+        hitTUV[i] = make_float4(depth, u, v, u2f(prim));
+        hitInst[i] = hit ? inst : kUnset;
+    }
+}
+
+/* randomOnHemisphereCosineWeighted, surf_math.cpp:116-134 (retry loop for R.N == 0) */
+__device__ __forceinline__ V3 cosineSample(uint32_t& seed, V3 n) {
+    for (;;) {
+        const float r0 = rndF(seed), r1 = rndF(seed);
+        const float r = sqrtf(r0);
+        const float theta = k2Pi * r1;
+        const V3 dir = mk3(r * gCosf(theta), r * gSinf(theta), sqrtf(1.0f - r0));
+        const float xMax = 1.0f - kEps;
+        const V3 tmp = (fabsf(n.x) > xMax) ? mk3(0.0f, 1.0f, 0.0f) : mk3(1.0f, 0.0f, 0.0f);
+        const V3 B = normalize(cross(n, tmp));
+        const V3 T = cross(B, n);
+        const V3 out = add(add(lscl(dir.x, T), lscl(dir.y, B)), lscl(dir.z, n));
+        if (!(dot(out, n) == 0.0f)) return out;
+    }
+}
+
+__device__ __forceinline__ void addRadiance(float4* rad, uint32_t sid, V3 c) {
+    float4 r = rad[sid];
+    r.x = r.x + c.x; r.y = r.y + c.y; r.z = r.z + c.z;
+    rad[sid] = r;
+}
+
+/* One bounce of Renderer::trace's loop body (renderer.cpp:338-460). */
+__global__ __launch_bounds__(kBlock) void k_shade(DevScene S, Pool cur, Pool nxt, const float4* __restrict__ hitTUV,
+                                                  const uint32_t* __restrict__ hitInst, ShadowQ Q,
+                                                  float4* __restrict__ rad, Counters* C, int par) {
+    const uint32_t n = C->nIn[par];
+    const uint32_t maxSeg = C->maxSeg;
+    const int nx = par ^ 1;
+    unsigned long long cHit = 0, cCont = 0, cSh = 0, cAcc = 0;
+    for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
+        const uint32_t i = base + threadIdx.x;
+        bool cont = false, shadow = false, hitGeom = false, accd = false;
+        float4 oOut = make_float4(0, 0, 0, 0), dOut = oOut, tOut = oOut;
+        float4 sO = oOut, sD = oOut, sC = oOut;
+        if (i < n) {
+            const float4 o4 = cur.o[i], d4 = cur.d[i], T4 = cur.T[i];
+            const float4 h4 = hitTUV[i];
+            const uint32_t inst = hitInst[i];
+            const uint32_t sid = f2u(o4.w);
+            uint32_t flags = f2u(d4.w);
+            uint32_t seed = f2u(T4.w);
+            const V3 o = xyz(o4), d = xyz(d4);
+            V3 T = xyz(T4);
+            bool lastSpecular = (flags & kFlagSpecular) != 0u;
+            const bool inMedium = (flags & kFlagMedium) != 0u;
+            const uint32_t seg = flags >> 2;
+            if (inst == kUnset) {
+                /* miss: energy += T * background (scene.cpp:35-51) */
+                V3 bg = mk3(0.0f, 0.0f, 0.0f);
+                if (S.bgType == 0u) bg = ld3(S.bgColor);
+                else if (S.bgType == 1u) {
+                    const float a = 0.5f * (1.0f + d.y);
+                    bg = add(lscl(a, ld3(S.bgB)), lscl(1.0f - a, ld3(S.bgA)));
+                }
+                addRadiance(rad, sid, mul(T, bg));
+                accd = true;
+            } else {
+                hitGeom = true;
+                const DevInstance& I = S.inst[inst];
+                const DevMaterial& m = S.mats[I.material];
+                const bool isLight = m.emit > 0.0f && (m.ec[0] > 0.0f || m.ec[1] > 0.0f || m.ec[2] > 0.0f);
+                if (isLight) {
+                    const V3 le = lscl(m.emit, ld3(m.ec));
+                    addRadiance(rad, sid, lastSpecular ? mul(T, le) : mk3(0.0f, 0.0f, 0.0f));
+                    accd = lastSpecular;
+                } else {
+                    const float t = h4.x, hu = h4.y, hv = h4.z;
+                    const uint32_t prim = f2u(h4.w);
+                    V3 medium = mk3(1.0f, 1.0f, 1.0f);
+                    if (inMedium) {
+                        const float nd = -t;
+                        medium = mk3(gExpf(m.absorb[0] * nd), gExpf(m.absorb[1] * nd), gExpf(m.absorb[2] * nd));
+                    }
+                    const V3 P = add(o, lscl(t, d));
+                    /* Instance::normal: M (u n0 + v n2 + w n1, 0), glm::normalize(vec4) */
+                    const float4* nr = S.normals + 3u * (I.triOffset + prim);
+                    const float4 n0 = nr[0], n1 = nr[1], n2 = nr[2];
+                    const float w = (1.0f - hu) - hv;
+                    const V3 no = add(add(lscl(hu, xyz(n0)), lscl(hv, xyz(n2))), lscl(w, xyz(n1)));
+                    const float* M = I.M;
+                    const float nx4 = mrow(M, 0, no.x, no.y, no.z, 0.0f), ny4 = mrow(M, 1, no.x, no.y, no.z, 0.0f);
+                    const float nz4 = mrow(M, 2, no.x, no.y, no.z, 0.0f), nw4 = mrow(M, 3, no.x, no.y, no.z, 0.0f);
+                    const float nn = (nx4 * nx4 + ny4 * ny4) + (nz4 * nz4 + nw4 * nw4);
+                    const float ninv = 1.0f / sqrtf(nn);
+                    V3 N = mk3(nx4 * ninv, ny4 * ninv, nz4 * ninv);
+                    const float rng = rndF(seed);
+                    V3 R = mk3(0.0f, 0.0f, 0.0f);
+                    bool nextMedium = inMedium;
+                    bool alive = true;
+                    if (dot(d, N) > 0.0f) N = scl(N, -1.0f);
+                    if (rng < m.refl) {
+                        R = sub(d, lscl(2.0f * dot(N, d), N));
+                        lastSpecular = true;
+                        T = mul(T, mul(ld3(m.albedo), medium));
+                    } else if (rng < (m.refl + m.refr)) {
+                        bool mustRefract = false;
+                        R = sub(d, lscl(2.0f * dot(N, d), N));
+                        const float n1f = inMedium ? m.ior : 1.0f, n2f = inMedium ? 1.0f : m.ior;
+                        const float ratio = n1f / n2f;
+                        const float cosI = -dot(d, N);
+                        const float cos2 = 1.0f - (ratio * ratio) * (1.0f - cosI * cosI);
+                        if (cos2 > 0.0f) {
+                            const float a = n1f - n2f, b = n1f + n2f;
+                            const float r0 = (a * a) / (b * b);
+                            const float c = 1.0f - cosI;
+                            const float fres = r0 + (1.0f - r0) * ((((c * c) * c) * c) * c);
+                            mustRefract = rndF(seed) > fres;
+                            if (mustRefract) R = add(lscl(ratio, d), lscl(ratio * cosI - sqrtf(fabsf(cos2)), N));
+                        }
+                        lastSpecular = true;
+                        T = mul(T, mul(ld3(m.albedo), medium));
+                        nextMedium = mustRefract ? !inMedium : inMedium;
+                    } else {
+                        R = cosineSample(seed, N);
+                        const float cosT = dot(N, R);
+                        const float pdf = cosT * kInvPi;
+                        const V3 brdf = scl(ld3(m.albedo), kInvPi);
+                        if (S.nLights > 0u) {
+                            /* Scene::sampleLights + Instance::samplePoint (scene.h:53, bvh.cpp:533-552) */
+                            const uint2 L = S.lights[rndRangeU(seed, 0u, S.nLights)];
+                            const DevInstance& LI = S.inst[L.x];
+                            const float lu = rndRange(seed, 0.0f, 1.0f);
+                            const float lv = rndRange(seed, 0.0f, 1.0f - lu);
+                            const uint32_t ti = rndRangeU(seed, 0u, L.y);
+                            const float4* tv = S.verts + 4u * (LI.triOffset + ti);
+                            const float4* tn = S.normals + 3u * (LI.triOffset + ti);
+                            const float lw = (1.0f - lu) - lv;
+                            const V3 lp = add(add(lscl(lu, xyz(tv[0])), lscl(lv, xyz(tv[2]))), lscl(lw, xyz(tv[1])));
+                            const V3 ln = add(add(lscl(lu, xyz(tn[0])), lscl(lv, xyz(tn[2]))), lscl(lw, xyz(tn[1])));
+                            const float* LM = LI.M;
+                            const float pw = mrow(LM, 3, lp.x, lp.y, lp.z, 1.0f);
+                            const V3 Pl = divs(mk3(mrow(LM, 0, lp.x, lp.y, lp.z, 1.0f), mrow(LM, 1, lp.x, lp.y, lp.z, 1.0f),
+                                                   mrow(LM, 2, lp.x, lp.y, lp.z, 1.0f)), pw);
+                            const V3 LN = normalize(mk3(mrow(LM, 0, ln.x, ln.y, ln.z, 0.0f), mrow(LM, 1, ln.x, ln.y, ln.z, 0.0f),
+                                                        mrow(LM, 2, ln.x, ln.y, ln.z, 0.0f)));
+                            const V3 IL = sub(Pl, P);
+                            const V3 Ld = normalize(IL);
+                            const V3 SO = add(P, lscl(kEps, Ld));
+                            const float srDepth = sqrtf(dot(IL, IL)) - 2.0f * kEps;
+                            const float falloff = 1.0f / dot(IL, IL);
+                            const float cosO = dot(N, Ld);
+                            const float cosL = dot(LN, lscl(-1.0f, Ld));
+                            if (cosO > 0.0f && cosL > 0.0f) {
+                                const float SA = (cosL * LI.area) * falloff;
+                                const float lightPdf = 1.0f / SA;
+                                const float invPdf = 1.0f / lightPdf;
+                                const DevMaterial& lm = S.mats[LI.material];
+                                const V3 le = lscl(lm.emit, ld3(lm.ec));
+                                const V3 Lc = scl(scl(mul(scl(le, invPdf), brdf), cosO), (float)S.nLights);
+                                const V3 contrib = mul(T, Lc);
+                                shadow = true;
+                                sO = make_float4(SO.x, SO.y, SO.z, srDepth);
+                                sD = make_float4(Ld.x, Ld.y, Ld.z, u2f(sid));
+                                sC = make_float4(contrib.x, contrib.y, contrib.z, 0.0f);
+                            }
+                        }
+                        const float pm = tmax(T.x, tmax(T.y, T.z));
+                        const float pr = pm < 0.0f ? 0.0f : (pm > 1.0f ? 1.0f : pm);
+                        if (pr < rndF(seed)) alive = false;
+                        else {
+                            const float rr = 1.0f / pr;
+                            const float invPdf = 1.0f / pdf;
+                            lastSpecular = false;
+                            T = mul(T, scl(mul(lscl(cosT * invPdf, brdf), medium), rr));
+                        }
+                    }
+                    if (alive && !(maxSeg != 0u && seg >= maxSeg)) {
+                        cont = true;
+                        const V3 O = add(P, lscl(kEps, R));
+                        flags = (nextMedium ? kFlagMedium : 0u) | (lastSpecular ? kFlagSpecular : 0u) | ((seg + 1u) << 2);
+                        oOut = make_float4(O.x, O.y, O.z, u2f(sid));
+                        dOut = make_float4(R.x, R.y, R.z, u2f(flags));
+                        tOut = make_float4(T.x, T.y, T.z, u2f(seed));
+                    }
+                }
+            }
+        }
+        const unsigned long long mCont = __ballot(cont), mSh = __ballot(shadow);
+        const uint32_t jc = waveAppend(&C->nApp[nx], mCont);
+        const uint32_t js = waveAppend(&C->nSh[par], mSh);
+        if (cont) { nxt.o[jc] = oOut; nxt.d[jc] = dOut; nxt.T[jc] = tOut; }
+        if (shadow) { Q.o[js] = sO; Q.d[js] = sD; Q.c[js] = sC; }
+        cHit += (unsigned long long)__popcll(__ballot(hitGeom));
+        cCont += (unsigned long long)__popcll(mCont);
+        cSh += (unsigned long long)__popcll(mSh);
+        cAcc += (unsigned long long)__popcll(__ballot(accd));
+    }
+    waveCount(&C->ev[1], cHit);
+    waveCount(&C->ev[2], cCont);
+    waveCount(&C->ev[3], cSh);
+    waveCount(&C->ev[4], cAcc);
+}
+
+__global__ __launch_bounds__(kBlock) void k_connect(DevScene S, ShadowQ Q, float4* __restrict__ rad, Counters* C, int par) {
+    extern __shared__ uint32_t lds[];
+    const uint32_t n = C->nSh[par];
+    const uint32_t stride = blockDim.x;
+    uint32_t* stk = lds + threadIdx.x;
+    unsigned long long cUn = 0;
+    for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
+        const uint32_t i = base + threadIdx.x;
+        bool unocc = false;
+        if (i < n) {
+            const float4 o = Q.o[i], d = Q.d[i];
+            float depth = o.w, u = 0.0f, v = 0.0f;
+            uint32_t inst = kUnset, prim = kUnset;
+            const bool occ = traceScene<true>(S, xyz(o), xyz(d), depth, u, v, inst, prim, stk, stride);
+            if (!occ) {
+                const float4 c = Q.c[i];
+                addRadiance(rad, f2u(d.w), xyz(c));
+                unocc = true;
+            }
+        }
+        cUn += (unsigned long long)__popcll(__ballot(unocc));
+    }
+    waveCount(&C->ev[5], cUn);
+    waveCount(&C->ev[4], cUn);
+}
+
+/* Camera::getPrimaryRay + sampleDefocusDisk (camera.h:59-87), jitter of
+ * renderer.cpp:173-177; draw order of g++ (last argument first). */
+__global__ __launch_bounds__(kBlock) void k_regen(DevCamera cam, Pool nxt, float4* __restrict__ rad, Counters* C, int par,
+                                                  uint32_t capacity, const uint32_t* __restrict__ rows,
+                                                  uint32_t width, uint32_t npx) {
+    const int nx = par ^ 1;
+    const uint32_t cont = C->nApp[nx];
+    const uint32_t ns = C->ns[par];
+    const uint32_t total = C->total;
+    const uint32_t frame0 = C->firstFrame;
+    const uint32_t room = capacity - cont, left = total - ns;
+    const uint32_t nnew = room < left ? room : left;
+    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+    for (uint32_t k = gid; k < nnew; k += gridDim.x * blockDim.x) {
+        const uint32_t s = ns + k;
+        const uint32_t f = s / npx, lp = s - f * npx;
+        const uint32_t row = rows[lp / width], x = lp - (lp / width) * width;
+        const uint32_t p = x + row * width;
+        uint32_t seed = initSeed(p + (frame0 + f) * 1799u);
+        const float jy = rndRange(seed, -0.5f, 0.5f);
+        const float jx = rndRange(seed, -0.5f, 0.5f);
+        const float u = ((float)x + jx) * cam.invW, v = ((float)row + jy) * cam.invH;
+        V3 origin = ld3(cam.pos);
+        if (cam.defocus) {
+            float sx, sy;
+            do {
+                sy = rndRange(seed, -1.0f, 1.0f);
+                sx = rndRange(seed, -1.0f, 1.0f);
+            } while (sx * sx + sy * sy > 1.0f);
+            origin = add(origin, add(lscl(sx, ld3(cam.diskU)), lscl(sy, ld3(cam.diskV))));
+        }
+        const V3 plane = add(add(ld3(cam.firstPixel), lscl(u, ld3(cam.uVec))), lscl(v, ld3(cam.vVec)));
+        const V3 dir = normalize(sub(plane, origin));
+        const uint32_t slot = cont + k;
+        nxt.o[slot] = make_float4(origin.x, origin.y, origin.z, u2f(s));
+        nxt.d[slot] = make_float4(dir.x, dir.y, dir.z, u2f(kFlagSpecular | (1u << 2)));
+        nxt.T[slot] = make_float4(1.0f, 1.0f, 1.0f, u2f(seed));
+        rad[s] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    }
+    if (gid == 0) {
+        C->nIn[nx] = cont + nnew;
+        C->ns[nx] = ns + nnew;
+        C->nApp[par] = 0;
+        C->nSh[nx] = 0;
+        C->ev[0] += cont + nnew;     /* extension rays of the next phase */
+    }
+}
+
+/* acc[p] += (radiance, 1) for each frame of the batch, in frame order. */
+__global__ __launch_bounds__(kBlock) void k_accumulate(const float4* __restrict__ rad, float4* __restrict__ acc,
+                                                       uint32_t npx, uint32_t frames) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= npx) return;
+    float4 a = acc[p];
+    for (uint32_t f = 0; f < frames; ++f) {
+        const float4 r = rad[(size_t)f * npx + p];
+        a.x = a.x + r.x; a.y = a.y + r.y; a.z = a.z + r.z; a.w = a.w + 1.0f;
+    }
+    acc[p] = a;
+}
+
+/* wavefront_finalize.comp + RgbaToU32 (cvtps2dq round-to-even, packus saturation) */
+__device__ __forceinline__ uint32_t packChannel(float v) {
+    if (!(v >= -2147483648.0f && v < 2147483648.0f)) return 0u;
+    const float r = rintf(v);
+    return r < 0.0f ? 0u : (r > 255.0f ? 255u : (uint32_t)r);
+}
+__global__ __launch_bounds__(kBlock) void k_finalize(const float4* __restrict__ acc, uint32_t* __restrict__ out,
+                                                     uint32_t npx, float inv) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= npx) return;
+    const float4 a = acc[p];
+    out[p] = packChannel((a.x * inv) * 255.0f) | (packChannel((a.y * inv) * 255.0f) << 8) |
+             (packChannel((a.z * inv) * 255.0f) << 16) | (packChannel((a.w * inv) * 255.0f) << 24);
+}
+
+/* Traversal entry points for kernel-level parity tests. */
+__global__ __launch_bounds__(kBlock) void k_trace_closest(DevScene S, const float* __restrict__ o, const float* __restrict__ d,
+                                                          uint32_t n, float4* __restrict__ tuv, uint2* __restrict__ ip) {
+    extern __shared__ uint32_t lds[];
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float depth = kFarAway, u = 0.0f, v = 0.0f;
+    uint32_t inst = kUnset, prim = kUnset;
+    const bool hit = traceScene<false>(S, mk3(o[3 * i], o[3 * i + 1], o[3 * i + 2]), mk3(d[3 * i], d[3 * i + 1], d[3 * i + 2]),
+                                       depth, u, v, inst, prim, lds + threadIdx.x, blockDim.x);
+    tuv[i] = make_float4(depth, hit ? u : 0.0f, hit ? v : 0.0f, 0.0f);
+    ip[i] = make_uint2(hit ? inst : kUnset, hit ? prim : kUnset);
+}
+__global__ __launch_bounds__(kBlock) void k_trace_any(DevScene S, const float* __restrict__ o, const float* __restrict__ d,
+                                                      const float* __restrict__ tmaxv, uint32_t n, uint8_t* __restrict__ occ) {
+    extern __shared__ uint32_t lds[];
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float depth = tmaxv[i], u = 0.0f, v = 0.0f;
+    uint32_t inst = kUnset, prim = kUnset;
+    occ[i] = traceScene<true>(S, mk3(o[3 * i], o[3 * i + 1], o[3 * i + 2]), mk3(d[3 * i], d[3 * i + 1], d[3 * i + 2]),
+                              depth, u, v, inst, prim, lds + threadIdx.x, blockDim.x) ? 1 : 0;
+}
+
+}  // namespace surfdev

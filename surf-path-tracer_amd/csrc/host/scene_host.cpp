@@ -1,0 +1,749 @@
+/*
+ * scene_host.cpp -- host half of the product: the reference's Renderer/Scene/BVH
+ * host API (surf/surf_host.hpp) and the C-ABI scene helpers of surf_hip.h.
+ *
+ * Everything here runs once per scene (OBJ parse, BLAS/TLAS binned-SAH build,
+ * instance setup, GPUBatcher flattening).  It must produce the exact node
+ * arrays the reference would, because BVH topology fixes traversal order and
+ * therefore which of two equal-depth hits wins.  Floating point is built with
+ * -ffp-contract=off (plain SSE arithmetic, like g++ on the reference).
+ */
+#include "surf/surf_host.hpp"
+
+#include <zlib.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <stdexcept>
+
+namespace surf {
+
+/* =================================================================== Mat4 */
+Mat4::Mat4(F32 diag) {
+    std::memset(c, 0, sizeof c);
+    for (int i = 0; i < 4; ++i) c[i][i] = diag;
+}
+
+/* glm operator*(mat4, vec4): pairwise column sums (m0 v0 + m1 v1) + (m2 v2 + m3 v3) */
+Float4 Mat4::operator*(const Float4& v) const {
+    F32 r[4];
+    for (int i = 0; i < 4; ++i) {
+        const F32 a = c[0][i] * v.x + c[1][i] * v.y;
+        const F32 b = c[2][i] * v.z + c[3][i] * v.w;
+        r[i] = a + b;
+    }
+    return Float4(r[0], r[1], r[2], r[3]);
+}
+
+Mat4 translate(const Mat4& m, const Float3& v) {
+    Mat4 r = m;
+    for (int i = 0; i < 4; ++i) {
+        F32 s = m.c[0][i] * v.x + m.c[1][i] * v.y;
+        s = s + m.c[2][i] * v.z;
+        r.c[3][i] = s + m.c[3][i];
+    }
+    return r;
+}
+
+Mat4 scale(const Mat4& m, const Float3& v) {
+    Mat4 r = m;
+    const F32 k[3] = {v.x, v.y, v.z};
+    for (int col = 0; col < 3; ++col)
+        for (int i = 0; i < 4; ++i) r.c[col][i] = m.c[col][i] * k[col];
+    return r;
+}
+
+Mat4 rotate(const Mat4& m, F32 angle, const Float3& axisIn) {
+    const F32 cs = cosf(angle), sn = sinf(angle);
+    const F32 len2 = (axisIn.x * axisIn.x + axisIn.y * axisIn.y) + axisIn.z * axisIn.z;
+    const F32 inv = 1.0f / sqrtf(len2);
+    const F32 a[3] = {axisIn.x * inv, axisIn.y * inv, axisIn.z * inv};
+    const F32 omc = 1.0f - cs;
+    const F32 t[3] = {omc * a[0], omc * a[1], omc * a[2]};
+    F32 rot[3][3];
+    rot[0][0] = cs + t[0] * a[0];
+    rot[0][1] = t[0] * a[1] + sn * a[2];
+    rot[0][2] = t[0] * a[2] - sn * a[1];
+    rot[1][0] = t[1] * a[0] - sn * a[2];
+    rot[1][1] = cs + t[1] * a[1];
+    rot[1][2] = t[1] * a[2] + sn * a[0];
+    rot[2][0] = t[2] * a[0] + sn * a[1];
+    rot[2][1] = t[2] * a[1] - sn * a[0];
+    rot[2][2] = cs + t[2] * a[2];
+    Mat4 r(0.0f);
+    for (int col = 0; col < 3; ++col)
+        for (int i = 0; i < 4; ++i) {
+            F32 s = m.c[0][i] * rot[col][0] + m.c[1][i] * rot[col][1];
+            r.c[col][i] = s + m.c[2][i] * rot[col][2];
+        }
+    for (int i = 0; i < 4; ++i) r.c[3][i] = m.c[3][i];
+    return r;
+}
+
+/* glm compute_inverse<4,4>: cofactors, sign pattern, det from row 0. */
+Mat4 inverse(const Mat4& m) {
+    const auto& a = m.c;
+    const F32 k00 = a[2][2] * a[3][3] - a[3][2] * a[2][3];
+    const F32 k02 = a[1][2] * a[3][3] - a[3][2] * a[1][3];
+    const F32 k03 = a[1][2] * a[2][3] - a[2][2] * a[1][3];
+    const F32 k04 = a[2][1] * a[3][3] - a[3][1] * a[2][3];
+    const F32 k06 = a[1][1] * a[3][3] - a[3][1] * a[1][3];
+    const F32 k07 = a[1][1] * a[2][3] - a[2][1] * a[1][3];
+    const F32 k08 = a[2][1] * a[3][2] - a[3][1] * a[2][2];
+    const F32 k10 = a[1][1] * a[3][2] - a[3][1] * a[1][2];
+    const F32 k11 = a[1][1] * a[2][2] - a[2][1] * a[1][2];
+    const F32 k12 = a[2][0] * a[3][3] - a[3][0] * a[2][3];
+    const F32 k14 = a[1][0] * a[3][3] - a[3][0] * a[1][3];
+    const F32 k15 = a[1][0] * a[2][3] - a[2][0] * a[1][3];
+    const F32 k16 = a[2][0] * a[3][2] - a[3][0] * a[2][2];
+    const F32 k18 = a[1][0] * a[3][2] - a[3][0] * a[1][2];
+    const F32 k19 = a[1][0] * a[2][2] - a[2][0] * a[1][2];
+    const F32 k20 = a[2][0] * a[3][1] - a[3][0] * a[2][1];
+    const F32 k22 = a[1][0] * a[3][1] - a[3][0] * a[1][1];
+    const F32 k23 = a[1][0] * a[2][1] - a[2][0] * a[1][1];
+    const F32 f0[4] = {k00, k00, k02, k03}, f1[4] = {k04, k04, k06, k07}, f2[4] = {k08, k08, k10, k11};
+    const F32 f3[4] = {k12, k12, k14, k15}, f4[4] = {k16, k16, k18, k19}, f5[4] = {k20, k20, k22, k23};
+    const F32 w0[4] = {a[1][0], a[0][0], a[0][0], a[0][0]};
+    const F32 w1[4] = {a[1][1], a[0][1], a[0][1], a[0][1]};
+    const F32 w2[4] = {a[1][2], a[0][2], a[0][2], a[0][2]};
+    const F32 w3[4] = {a[1][3], a[0][3], a[0][3], a[0][3]};
+    Mat4 inv(0.0f);
+    for (int i = 0; i < 4; ++i) {
+        const F32 sa = (i & 1) ? -1.0f : 1.0f, sb = -sa;
+        inv.c[0][i] = ((w1[i] * f0[i] - w2[i] * f1[i]) + w3[i] * f2[i]) * sa;
+        inv.c[1][i] = ((w0[i] * f0[i] - w2[i] * f3[i]) + w3[i] * f4[i]) * sb;
+        inv.c[2][i] = ((w0[i] * f1[i] - w1[i] * f3[i]) + w3[i] * f5[i]) * sa;
+        inv.c[3][i] = ((w0[i] * f2[i] - w1[i] * f4[i]) + w2[i] * f5[i]) * sb;
+    }
+    const F32 d01 = a[0][0] * inv.c[0][0] + a[0][1] * inv.c[1][0];
+    const F32 d23 = a[0][2] * inv.c[2][0] + a[0][3] * inv.c[3][0];
+    const F32 rdet = 1.0f / (d01 + d23);
+    for (int col = 0; col < 4; ++col)
+        for (int i = 0; i < 4; ++i) inv.c[col][i] = inv.c[col][i] * rdet;
+    return inv;
+}
+
+static inline Float3 dehomog(const Float4& v) { return Float3(v.x, v.y, v.z) / v.w; }
+
+/* =================================================================== Mesh */
+Triangle::Triangle(Float3 a, Float3 b, Float3 c) : v0(b), v1(a), v2(c), centroid(0.0f) {
+    centroid = (v0 + v1 + v2) * 0.333f;               /* mesh.cpp:20 */
+}
+
+namespace {
+
+std::string slurp(const std::string& path) {
+    gzFile f = gzopen(path.c_str(), "rb");
+    if (!f) throw std::runtime_error("cannot open " + path);
+    std::string out;
+    std::vector<char> buf(1 << 20);
+    for (;;) {
+        const int k = gzread(f, buf.data(), (unsigned)buf.size());
+        if (k <= 0) break;
+        out.append(buf.data(), (size_t)k);
+    }
+    gzclose(f);
+    return out;
+}
+
+/* Resolves a 1-based / negative OBJ index against `count` records. */
+inline long objIndex(long raw, size_t count) {
+    if (raw > 0) return raw - 1;
+    if (raw < 0) return (long)count + raw;
+    return -1;
+}
+
+struct Corner { long v = -1, t = -1, n = -1; };
+
+/* tinyobjloader-compatible reader (triangulate = true).  Floats parse through
+ * double then narrow to float, like tinyobj's real_t = float path. */
+void parseObj(const std::string& text, Mesh& mesh) {
+    std::vector<F32> pos, nrm, tex;
+    std::vector<Corner> corners;          /* three per triangle */
+    const char* p = text.data();
+    const char* end = p + text.size();
+    while (p < end) {
+        const char* eol = static_cast<const char*>(memchr(p, '\n', (size_t)(end - p)));
+        if (!eol) eol = end;
+        std::string line(p, eol);
+        p = eol + 1;
+        const char* s = line.c_str();
+        while (*s == ' ' || *s == '\t') ++s;
+        auto floats = [&](const char* q, int k, std::vector<F32>& dst) {
+            char* e = nullptr;
+            for (int i = 0; i < k; ++i) { dst.push_back((F32)strtod(q, &e)); q = e; }
+        };
+        if (s[0] == 'v' && (s[1] == ' ' || s[1] == '\t')) floats(s + 2, 3, pos);
+        else if (s[0] == 'v' && s[1] == 'n') floats(s + 2, 3, nrm);
+        else if (s[0] == 'v' && s[1] == 't') floats(s + 2, 2, tex);
+        else if (s[0] == 'f' && (s[1] == ' ' || s[1] == '\t')) {
+            std::vector<Corner> face;
+            const char* q = s + 1;
+            while (true) {
+                while (*q == ' ' || *q == '\t' || *q == '\r') ++q;
+                if (*q == '\0') break;
+                Corner c;
+                char* e = nullptr;
+                c.v = objIndex(strtol(q, &e, 10), pos.size() / 3);
+                q = e;
+                if (*q == '/') {
+                    ++q;
+                    if (*q != '/') { c.t = objIndex(strtol(q, &e, 10), tex.size() / 2); q = e; }
+                    if (*q == '/') { ++q; c.n = objIndex(strtol(q, &e, 10), nrm.size() / 3); q = e; }
+                }
+                face.push_back(c);
+                while (*q && *q != ' ' && *q != '\t') ++q;
+            }
+            const size_t n = face.size();
+            if (n < 3) continue;
+            if (n == 4) {
+                /* quad: split on the shorter diagonal; ties -> (0,1,3),(1,2,3) */
+                auto P = [&](int k) { const long v = face[k].v; return Float3(pos[3 * v], pos[3 * v + 1], pos[3 * v + 2]); };
+                const Float3 d02 = P(2) - P(0), d13 = P(3) - P(1);
+                const F32 l02 = d02.x * d02.x + d02.y * d02.y + d02.z * d02.z;
+                const F32 l13 = d13.x * d13.x + d13.y * d13.y + d13.z * d13.z;
+                static const int kA[6] = {0, 1, 2, 0, 2, 3}, kB[6] = {0, 1, 3, 1, 2, 3};
+                const int* k = (l02 < l13) ? kA : kB;
+                for (int j = 0; j < 6; ++j) corners.push_back(face[k[j]]);
+            } else {
+                for (size_t j = 1; j + 1 < n; ++j) { corners.push_back(face[0]); corners.push_back(face[j]); corners.push_back(face[j + 1]); }
+            }
+        }
+    }
+    auto vtx = [&](const Corner& c) {
+        if (c.v < 0 || (size_t)(3 * c.v + 2) >= pos.size()) throw std::runtime_error("OBJ vertex index out of range");
+        return Float3(pos[3 * c.v], pos[3 * c.v + 1], pos[3 * c.v + 2]);
+    };
+    auto nor = [&](const Corner& c) {
+        if (c.n < 0 || (size_t)(3 * c.n + 2) >= nrm.size()) return Float3(0.0f);
+        return Float3(nrm[3 * c.n], nrm[3 * c.n + 1], nrm[3 * c.n + 2]);
+    };
+    auto uv = [&](const Corner& c) {
+        if (c.t < 0 || (size_t)(2 * c.t + 1) >= tex.size()) return Float2(0.0f, 0.0f);
+        return Float2(tex[2 * c.t], tex[2 * c.t + 1]);
+    };
+    const size_t nt = corners.size() / 3;
+    mesh.triangles.reserve(nt);
+    mesh.triExtensions.reserve(nt);
+    for (size_t t = 0; t < nt; ++t) {
+        const Corner* c = &corners[3 * t];
+        mesh.triangles.emplace_back(vtx(c[0]), vtx(c[1]), vtx(c[2]));
+        TriExtension x;
+        x.n0 = nor(c[0]); x.n1 = nor(c[1]); x.n2 = nor(c[2]);
+        x.uv0 = uv(c[0]); x.uv1 = uv(c[1]); x.uv2 = uv(c[2]);
+        mesh.triExtensions.push_back(x);
+    }
+}
+
+}  // namespace
+
+Mesh::Mesh(const std::string& path) {
+    std::string text;
+    try { text = slurp(path); }
+    catch (const std::exception&) { text = slurp(path + ".gz"); }
+    parseObj(text, *this);
+}
+
+/* =================================================================== AABB */
+void AABB::grow(const Float3& p) { bbMin = min(bbMin, p); bbMax = max(bbMax, p); }
+void AABB::grow(const AABB& b) { bbMin = min(bbMin, b.bbMin); bbMax = max(bbMax, b.bbMax); }
+F32 AABB::area() const { const Float3 e = bbMax - bbMin; return e.x * e.y + e.y * e.z + e.z * e.x; }
+Float3 AABB::center() const { return 0.5f * (bbMax - bbMin); }
+
+/* ========================================================= binned SAH build
+ * One builder for both levels.  Prim access is a policy: key(p, axis) is the
+ * binning coordinate, addTo(box, p) grows a box by the primitive.  Build order
+ * reproduces the reference's recursive subdivide exactly (pre-order, children
+ * allocated in pairs at split time) with an explicit stack. */
+namespace {
+
+constexpr int kBins = 8;
+constexpr int kPlanes = kBins - 1;
+
+template <class Prims>
+struct SahBuilder {
+    const Prims& prims;
+    std::vector<U32>& idx;
+    std::vector<BvhNode>& nodes;
+    U32& used;
+
+    void bounds(U32 ni) {
+        BvhNode& n = nodes[ni];
+        for (U32 i = 0; i < n.count; ++i) prims.addTo(n.boundingBox, idx[n.leftFirst + i]);
+    }
+
+    /* returns split position; cost/axis out (bvh.cpp:294-377) */
+    F32 plane(const BvhNode& n, F32& bestCost, U32& bestAxis) const {
+        bestCost = INFINITY;
+        bestAxis = 0;
+        F32 bestSplit = 0.0f;
+        const U32 first = n.leftFirst, cnt = n.count;
+        for (U32 axis = 0; axis < 3; ++axis) {
+            F32 lo = 3.40282347e+38f, hi = 1.17549435e-38f;    /* F32_MAX / F32_MIN (sic) */
+            for (U32 i = 0; i < cnt; ++i) {
+                const F32 k = prims.key(idx[first + i], axis);
+                lo = lo < k ? lo : k;
+                hi = hi > k ? hi : k;
+            }
+            if (lo == hi) continue;
+            const F32 scaleK = (F32)kBins / (hi - lo);
+            U32 binCount[kBins] = {0};
+            AABB binBox[kBins];
+            for (U32 i = 0; i < cnt; ++i) {
+                const U32 pr = idx[first + i];
+                const size_t s = (size_t)((prims.key(pr, axis) - lo) * scaleK);
+                const size_t b = s < (size_t)(kBins - 1) ? s : (size_t)(kBins - 1);
+                binCount[b]++;
+                prims.addTo(binBox[b], pr);
+            }
+            F32 lArea[kPlanes], rArea[kPlanes];
+            U32 lCnt[kPlanes], rCnt[kPlanes];
+            AABB lBox, rBox;
+            U32 lSum = 0, rSum = 0;
+            for (int k = 0; k < kPlanes; ++k) {
+                lSum += binCount[k];
+                lCnt[k] = lSum;
+                lBox.grow(binBox[k]);
+                lArea[k] = lBox.area();
+                const int rb = kBins - 1 - k;
+                rSum += binCount[rb];
+                rCnt[rb - 1] = rSum;
+                rBox.grow(binBox[rb]);
+                rArea[rb - 1] = rBox.area();
+            }
+            const F32 extent = (hi - lo) / (F32)kBins;
+            for (int k = 0; k < kPlanes; ++k) {
+                const F32 c = (F32)lCnt[k] * lArea[k] + (F32)rCnt[k] * rArea[k];
+                if (c < bestCost) {
+                    bestCost = c;
+                    bestSplit = lo + extent * (F32)(k + 1);
+                    bestAxis = axis;
+                }
+            }
+        }
+        return bestSplit;
+    }
+
+    U32 split(const BvhNode& n, F32 pos, U32 axis) {
+        I32 i = (I32)n.leftFirst;
+        I32 j = (I32)(n.leftFirst + (n.count - 1));
+        while (i <= j) {
+            if (prims.key(idx[i], axis) < pos) ++i;
+            else { std::swap(idx[i], idx[j]); --j; }
+        }
+        return (U32)i;
+    }
+
+    void run(U32 count) {
+        idx.resize(count);
+        for (U32 i = 0; i < count; ++i) idx[i] = i;
+        BvhNode zero;                                /* MALLOC64 + memset(0): root box starts at the origin */
+        zero.leftFirst = 0;
+        zero.count = 0;
+        zero.boundingBox.bbMin = Float3(0.0f);
+        zero.boundingBox.bbMax = Float3(0.0f);
+        nodes.assign(2 * (size_t)count, zero);
+        used = 2;
+        nodes[0].leftFirst = 0;
+        nodes[0].count = count;
+        bounds(0);
+        std::vector<U32> todo{0};
+        while (!todo.empty()) {
+            const U32 ni = todo.back();
+            todo.pop_back();
+            F32 cost; U32 axis;
+            const F32 pos = plane(nodes[ni], cost, axis);
+            if (cost >= (F32)nodes[ni].count * nodes[ni].boundingBox.area()) continue;
+            const U32 pivot = split(nodes[ni], pos, axis);
+            const U32 nl = pivot - nodes[ni].leftFirst;
+            if (nl == 0 || nl == nodes[ni].count) continue;
+            const U32 l = used, r = used + 1;
+            used += 2;
+            nodes[l].leftFirst = nodes[ni].leftFirst; nodes[l].count = nl; nodes[l].boundingBox = AABB();
+            nodes[r].leftFirst = pivot; nodes[r].count = nodes[ni].count - nl; nodes[r].boundingBox = AABB();
+            nodes[ni].leftFirst = l;
+            nodes[ni].count = 0;
+            bounds(l);
+            bounds(r);
+            todo.push_back(r);                        /* left subtree first, like the recursion */
+            todo.push_back(l);
+        }
+    }
+};
+
+struct MeshPrims {
+    const Mesh* mesh;
+    F32 key(U32 p, U32 axis) const { return mesh->triangles[p].centroid[axis]; }
+    void addTo(AABB& b, U32 p) const {
+        const Triangle& t = mesh->triangles[p];
+        b.grow(t.v0); b.grow(t.v1); b.grow(t.v2);
+    }
+};
+
+struct InstancePrims {
+    const std::vector<Instance>* inst;
+    F32 key(U32 p, U32 axis) const { return (*inst)[p].bounds.center()[axis]; }
+    void addTo(AABB& b, U32 p) const { b.grow((*inst)[p].bounds); }
+};
+
+U32 depthOf(const std::vector<BvhNode>& nodes, U32 root) {
+    U32 best = 0;
+    std::vector<std::pair<U32, U32>> st{{root, 0}};
+    while (!st.empty()) {
+        auto [n, d] = st.back();
+        st.pop_back();
+        if (nodes[n].count != 0) { best = std::max(best, d); continue; }
+        st.push_back({nodes[n].leftFirst, d + 1});
+        st.push_back({nodes[n].leftFirst + 1, d + 1});
+    }
+    return best;
+}
+
+}  // namespace
+
+/* ================================================================= BvhBLAS */
+BvhBLAS::BvhBLAS(Mesh* mesh) : m_mesh(mesh) { build(); }
+
+void BvhBLAS::build() {
+    MeshPrims prims{m_mesh};
+    SahBuilder<MeshPrims> b{prims, m_indices, m_nodes, m_nodesUsed};
+    b.run((U32)m_mesh->triangles.size());
+}
+
+/* bvh.cpp:268-287 */
+void BvhBLAS::refit() {
+    MeshPrims prims{m_mesh};
+    for (int64_t i = (int64_t)m_nodesUsed - 1; i >= 0; --i) {
+        if (i == 1) continue;
+        BvhNode& n = m_nodes[(size_t)i];
+        if (n.isLeaf()) {
+            for (U32 k = 0; k < n.count; ++k) prims.addTo(n.boundingBox, m_indices[n.leftFirst + k]);
+            continue;
+        }
+        const BvhNode& l = m_nodes[n.leftFirst];
+        const BvhNode& r = m_nodes[n.leftFirst + 1];
+        n.boundingBox.bbMin = min(l.boundingBox.bbMin, r.boundingBox.bbMin);
+        n.boundingBox.bbMax = max(l.boundingBox.bbMax, r.boundingBox.bbMax);
+    }
+}
+
+U32 BvhBLAS::depth() const { return depthOf(m_nodes, 0); }
+
+/* ================================================================ Instance */
+Instance::Instance(BvhBLAS* blas, Material* mat, Mat4 transform)
+    : bvh(blas), material(mat), m_transform(transform), m_invTransform(1.0f) {
+    setTransform(transform);
+}
+
+void Instance::setTransform(const Mat4& transform) {            /* bvh.cpp:524-531 */
+    m_invTransform = inverse(transform);
+    m_transform = transform;
+    updateBounds();
+    calculateMeshArea();
+}
+
+void Instance::updateBounds() {                                  /* bvh.cpp:554-575 */
+    const AABB& lb = bvh->bounds();
+    bounds = AABB();
+    for (int k = 0; k < 8; ++k) {
+        /* corner order of the reference: x alternates fastest, max before min */
+        const Float3 corner((k & 1) ? lb.bbMin.x : lb.bbMax.x,
+                            (k & 2) ? lb.bbMin.y : lb.bbMax.y,
+                            (k & 4) ? lb.bbMin.z : lb.bbMax.z);
+        bounds.grow(dehomog(m_transform * Float4(corner, 1.0f)));
+    }
+}
+
+void Instance::calculateMeshArea() {                             /* bvh.cpp:577-594 */
+    area = 0.0f;
+    for (const Triangle& t : bvh->mesh()->triangles) {
+        const Float3 a = dehomog(m_transform * Float4(t.v0, 1.0f));
+        const Float3 b = dehomog(m_transform * Float4(t.v1, 1.0f));
+        const Float3 c = dehomog(m_transform * Float4(t.v2, 1.0f));
+        area = area + 0.5f * (b - a).cross(c - a).magnitude();
+    }
+}
+
+GPUInstance Instance::toGPUInstance() const {
+    GPUInstance g;
+    std::memset(&g, 0, sizeof g);
+    g.area = area;
+    std::memcpy(g.transform, m_transform.c, sizeof g.transform);
+    std::memcpy(g.inv_transform, m_invTransform.c, sizeof g.inv_transform);
+    return g;
+}
+
+/* ================================================================= BvhTLAS */
+BvhTLAS::BvhTLAS(std::vector<Instance> instances) : m_instances(std::move(instances)) { build(); }
+
+void BvhTLAS::build() {
+    InstancePrims prims{&m_instances};
+    SahBuilder<InstancePrims> b{prims, m_indices, m_nodes, m_nodesUsed};
+    b.run((U32)m_instances.size());
+}
+
+/* bvh.cpp:793-819 */
+void BvhTLAS::refit() {
+    InstancePrims prims{&m_instances};
+    for (int64_t i = (int64_t)m_nodesUsed - 1; i >= 0; --i) {
+        if (i == 1) continue;
+        BvhNode& n = m_nodes[(size_t)i];
+        if (n.isLeaf()) {
+            for (U32 k = 0; k < n.count; ++k) m_instances[m_indices[n.leftFirst + k]].updateInstanceData();
+            for (U32 k = 0; k < n.count; ++k) prims.addTo(n.boundingBox, m_indices[n.leftFirst + k]);
+            continue;
+        }
+        const BvhNode& l = m_nodes[n.leftFirst];
+        const BvhNode& r = m_nodes[n.leftFirst + 1];
+        n.boundingBox.bbMin = min(l.boundingBox.bbMin, r.boundingBox.bbMin);
+        n.boundingBox.bbMax = max(l.boundingBox.bbMax, r.boundingBox.bbMax);
+    }
+}
+
+U32 BvhTLAS::depth() const { return depthOf(m_nodes, 0); }
+
+/* ============================================================== GPUBatcher */
+GPUBatchInfo GPUBatcher::createBatchInfo(const std::vector<Instance>& instances) {
+    GPUBatchInfo out;
+    std::vector<const Mesh*> meshes;
+    std::vector<const BvhBLAS*> blases;
+    std::vector<const Material*> mats;
+    auto slot = [](auto& list, auto* key) {
+        for (size_t i = 0; i < list.size(); ++i) if (list[i] == key) return i;
+        list.push_back(key);
+        return list.size() - 1;
+    };
+    for (const Instance& in : instances) {
+        slot(meshes, in.bvh->mesh());
+        slot(blases, in.bvh);
+        slot(mats, in.material);
+    }
+    std::vector<U32> triBase, idxBase, nodeBase;
+    for (const Mesh* m : meshes) {
+        triBase.push_back((U32)out.triBuffer.size());
+        out.triBuffer.insert(out.triBuffer.end(), m->triangles.begin(), m->triangles.end());
+        out.triExtBuffer.insert(out.triExtBuffer.end(), m->triExtensions.begin(), m->triExtensions.end());
+    }
+    for (const BvhBLAS* b : blases) {
+        idxBase.push_back((U32)out.BLASIndices.size());
+        out.BLASIndices.insert(out.BLASIndices.end(), b->indices(), b->indices() + b->triCount());
+    }
+    for (const BvhBLAS* b : blases) {
+        nodeBase.push_back((U32)out.BLASNodes.size());
+        out.BLASNodes.insert(out.BLASNodes.end(), b->nodePool(), b->nodePool() + b->nodesUsed());
+    }
+    for (const Material* m : mats) out.materials.push_back(*m);
+    for (const Instance& in : instances) {
+        GPUInstance g = in.toGPUInstance();
+        const size_t mi = std::find(meshes.begin(), meshes.end(), in.bvh->mesh()) - meshes.begin();
+        const size_t bi = std::find(blases.begin(), blases.end(), in.bvh) - blases.begin();
+        g.tri_offset = triBase[mi];
+        g.bvh_idx_offset = idxBase[bi];
+        g.bvh_node_offset = nodeBase[bi];
+        g.material_offset = (U32)(std::find(mats.begin(), mats.end(), in.material) - mats.begin());
+        if (in.material->isLight())
+            out.lights.push_back(GPULightData{(U32)out.gpuInstances.size(), (U32)in.bvh->triCount()});
+        out.gpuInstances.push_back(g);
+    }
+    return out;
+}
+
+/* ================================================================ GPUScene */
+GPUScene::GPUScene(RenderContext* context, SceneBackground background, std::vector<Instance> instances)
+    : m_context(context), m_background(background), m_sceneTlas(instances),
+      m_batchInfo(GPUBatcher::createBatchInfo(instances)) {}
+
+void GPUScene::update(F32 deltaTime) {
+    Instance& in = m_sceneTlas.instance(3);
+    in.setTransform(rotate(in.transform(), 1.0f * deltaTime, WORLD_UP));
+    m_sceneTlas.refit();
+    m_batchInfo = GPUBatcher::createBatchInfo(m_sceneTlas.instances());
+    ++m_generation;
+}
+
+surf_scene_desc GPUScene::descriptor() const {
+    surf_scene_desc d;
+    std::memset(&d, 0, sizeof d);
+    d.triangles = reinterpret_cast<const surf_triangle*>(m_batchInfo.triBuffer.data());
+    d.triangle_count = (U32)m_batchInfo.triBuffer.size();
+    d.tri_ext = reinterpret_cast<const surf_tri_extension*>(m_batchInfo.triExtBuffer.data());
+    d.blas_indices = m_batchInfo.BLASIndices.data();
+    d.blas_index_count = (U32)m_batchInfo.BLASIndices.size();
+    d.blas_nodes = reinterpret_cast<const surf_bvh_node*>(m_batchInfo.BLASNodes.data());
+    d.blas_node_count = (U32)m_batchInfo.BLASNodes.size();
+    d.materials = reinterpret_cast<const surf_material*>(m_batchInfo.materials.data());
+    d.material_count = (U32)m_batchInfo.materials.size();
+    d.instances = m_batchInfo.gpuInstances.data();
+    d.instance_count = (U32)m_batchInfo.gpuInstances.size();
+    d.tlas_indices = m_sceneTlas.indices();
+    d.tlas_nodes = reinterpret_cast<const surf_bvh_node*>(m_sceneTlas.nodePool());
+    d.tlas_node_count = m_sceneTlas.nodesUsed();
+    d.lights = reinterpret_cast<const surf_light*>(m_batchInfo.lights.data());
+    d.light_count = (U32)m_batchInfo.lights.size();
+    d.background = reinterpret_cast<const surf_background*>(&m_background);
+    return d;
+}
+
+/* ================================================================== Camera */
+Camera::Camera(Float3 pos, Float3 target, U32 w, U32 h, F32 fov, F32 focal, F32 defocus)
+    : position(pos), forward(0.0f), up(0.0f), screenWidth((F32)w), screenHeight((F32)h),
+      fovY(fov), focalLength(focal), defocusAngle(defocus), viewPlane{} {
+    forward = (target - position).normalize();                   /* camera.cpp:21-23 */
+    const Float3 r = WORLD_UP.cross(forward).normalize();
+    up = forward.cross(r).normalize();
+    generateViewPlane();
+}
+
+void Camera::generateViewPlane() {                               /* camera.cpp:28-46 */
+    const F32 heightScale = tanf(radians(fovY) / 2.0f);
+    const F32 aspect = screenWidth / screenHeight;
+    const F32 vh = 2.0f * heightScale * focalLength;
+    const F32 vw = aspect * vh;
+    const Float3 u = right() * vw;
+    const Float3 v = (-1.0f * up) * vh;
+    const Float3 du = u / screenWidth, dv = v / screenHeight;
+    const Float3 topLeft = ((position + (forward * focalLength)) - (0.5f * u)) - (0.5f * v);
+    viewPlane.firstPixel = topLeft + 0.5f * (du + dv);
+    viewPlane.uVector = u;
+    viewPlane.vVector = v;
+}
+
+CameraUBO Camera::toUBO() const {
+    CameraUBO u;
+    std::memset(&u, 0, sizeof u);
+    auto put = [](surf_float3_16& d, const Float3& s) { d.x = s.x; d.y = s.y; d.z = s.z; d._pad = 0.0f; };
+    put(u.position, position); put(u.up, up); put(u.fwd, forward); put(u.right, right());
+    put(u.first_pixel, viewPlane.firstPixel); put(u.u_vector, viewPlane.uVector); put(u.v_vector, viewPlane.vVector);
+    u.resolution[0] = screenWidth; u.resolution[1] = screenHeight;
+    u.focal_length = focalLength; u.defocus_angle = defocusAngle;
+    return u;
+}
+
+}  // namespace surf
+
+/* ====================================================== C-ABI scene helpers */
+struct surf_scene {
+    std::vector<std::unique_ptr<surf::Mesh>> meshes;
+    std::vector<std::unique_ptr<surf::BvhBLAS>> blases;
+    std::vector<std::unique_ptr<surf::Material>> materials;
+    std::unique_ptr<surf::GPUScene> scene;
+    surf::RenderContext context;
+};
+
+namespace {
+
+/* The scene of the reference's main.cpp:161-346 (and the C5 deep variant). */
+void buildIndoor(surf_scene& S, const std::string& dir, int variant) {
+    using namespace surf;
+    for (const char* name : {"susanne", "cube", "lens", "plane"})
+        S.meshes.push_back(std::make_unique<Mesh>(dir + "/" + name + ".obj"));
+    Mesh* sus = S.meshes[0].get();
+    Mesh* cube = S.meshes[1].get();
+    Mesh* lens = S.meshes[2].get();
+    Mesh* plane = S.meshes[3].get();
+    Mesh* lattice = nullptr;
+    if (variant == 1) {
+        /* C5: 648 Suzannes, translate(-8+2i, -0.4+1.2j, -4+1.5k) * scale(0.5), one mesh */
+        auto m = std::make_unique<Mesh>();
+        m->triangles.reserve(648 * sus->triangles.size());
+        m->triExtensions.reserve(648 * sus->triangles.size());
+        for (int i = 0; i < 9; ++i)
+            for (int j = 0; j < 8; ++j)
+                for (int k = 0; k < 9; ++k) {
+                    const Mat4 X = scale(translate(Mat4(1.0f), Float3(-8.0f + 2.0f * (F32)i, -0.4f + 1.2f * (F32)j, -4.0f + 1.5f * (F32)k)), Float3(0.5f));
+                    for (size_t t = 0; t < sus->triangles.size(); ++t) {
+                        const Triangle& s = sus->triangles[t];
+                        /* OBJ order is (v1, v0, v2) of the stored triangle */
+                        m->triangles.emplace_back(dehomog(X * Float4(s.v1, 1.0f)), dehomog(X * Float4(s.v0, 1.0f)), dehomog(X * Float4(s.v2, 1.0f)));
+                        m->triExtensions.push_back(sus->triExtensions[t]);
+                    }
+                }
+        lattice = m.get();
+        S.meshes.push_back(std::move(m));
+    }
+    for (Mesh* m : {sus, cube, lens, plane}) S.blases.push_back(std::make_unique<BvhBLAS>(m));
+    if (lattice) S.blases.push_back(std::make_unique<BvhBLAS>(lattice));
+    BvhBLAS* susB = S.blases[0].get();
+    BvhBLAS* cubeB = S.blases[1].get();
+    BvhBLAS* lensB = S.blases[2].get();
+    BvhBLAS* planeB = S.blases[3].get();
+
+    auto mat = [&]() { S.materials.push_back(std::make_unique<Material>()); return S.materials.back().get(); };
+    Material* floorM = mat(); floorM->albedo = Float3(0.8f); floorM->reflectivity = 0.01f;
+    Material* wallRed = mat(); wallRed->albedo = Float3(1.0f, 0.0f, 0.0f);
+    Material* wallGreen = mat(); wallGreen->albedo = Float3(0.0f, 1.0f, 0.0f);
+    Material* diffuse = mat(); diffuse->albedo = Float3(1.0f, 0.0f, 0.0f);
+    Material* dielectric = mat(); dielectric->albedo = Float3(0.7f, 0.7f, 0.2f); dielectric->absorption = Float3(0.03f, 0.04f, 0.03f);
+    dielectric->refractivity = 1.0f; dielectric->indexOfRefraction = 1.42f;
+    Material* specular = mat(); specular->albedo = Float3(0.2f, 0.9f, 1.0f); specular->reflectivity = 0.8f;
+    Material* softLight = mat(); softLight->emissionColor = Float3(1.0f, 0.8f, 0.6f); softLight->emissionStrength = 5.0f;
+    Material* redLight = mat(); redLight->emissionColor = Float3(1.0f, 0.5f, 0.2f); redLight->emissionStrength = 5.0f;
+
+    const Mat4 I(1.0f);
+    std::vector<Instance> inst;
+    inst.emplace_back(planeB, floorM, scale(translate(I, Float3(0.0f, -1.0f, 0.0f)), Float3(10.0f, 10.0f, 10.0f)));
+    inst.emplace_back(cubeB, softLight, scale(translate(I, Float3(-8.0f, 7.0f, 5.0f)), Float3(0.5f, 0.5f, 0.5f)));
+    inst.emplace_back(cubeB, redLight, scale(translate(I, Float3(9.0f, 5.0f, -5.0f)), Float3(1.0f, 1.0f, 1.0f)));
+    inst.emplace_back(susB, diffuse, translate(I, Float3(0.0f, 0.0f, -1.0f)));
+    inst.emplace_back(susB, specular, translate(I, Float3(3.0f, 0.0f, -1.0f)));
+    inst.emplace_back(lensB, dielectric, translate(I, Float3(-3.0f, 0.0f, -1.0f)));
+    inst.emplace_back(planeB, wallRed, scale(rotate(translate(I, Float3(-10.0f, 4.0f, 0.0f)), radians(90.0f), WORLD_FORWARD), Float3(5.0f, 10.0f, 10.0f)));
+    inst.emplace_back(planeB, wallGreen, scale(rotate(translate(I, Float3(10.0f, 4.0f, 0.0f)), radians(90.0f), WORLD_FORWARD), Float3(5.0f, 10.0f, 10.0f)));
+    inst.emplace_back(planeB, floorM, scale(translate(I, Float3(0.0f, 9.0f, 0.0f)), Float3(10.0f, 10.0f, 10.0f)));
+    inst.emplace_back(planeB, floorM, scale(rotate(translate(I, Float3(0.0f, 4.0f, -10.0f)), radians(90.0f), WORLD_RIGHT), Float3(10.0f, 10.0f, 5.0f)));
+    inst.emplace_back(planeB, floorM, scale(rotate(translate(I, Float3(0.0f, 4.0f, 10.0f)), radians(90.0f), WORLD_RIGHT), Float3(10.0f, 10.0f, 5.0f)));
+    if (lattice) inst.emplace_back(S.blases[4].get(), diffuse, I);
+
+    SceneBackground bg;
+    bg.type = BackgroundType::ColorGradient;
+    bg.gradient.colorA = Float3(0.8f, 0.8f, 0.8f);
+    bg.gradient.colorB = Float3(0.1f, 0.4f, 0.6f);
+    S.scene = std::make_unique<GPUScene>(&S.context, bg, std::move(inst));
+}
+
+}  // namespace
+
+extern "C" {
+
+int surf_scene_build_indoor(const char* assets_dir, int variant, surf_scene** out) {
+    if (!out || (variant != 0 && variant != 1)) return SURF_ERR_INVALID;
+    *out = nullptr;
+    auto s = std::make_unique<surf_scene>();
+    try {
+        buildIndoor(*s, assets_dir ? assets_dir : ".", variant);
+    } catch (const std::exception& e) {
+        fprintf(stderr, "surf_scene_build_indoor: %s\n", e.what());
+        return SURF_ERR_IO;
+    }
+    *out = s.release();
+    return SURF_OK;
+}
+
+int surf_scene_desc_get(const surf_scene* scene, surf_scene_desc* out) {
+    if (!scene || !out) return SURF_ERR_INVALID;
+    *out = scene->scene->descriptor();
+    return SURF_OK;
+}
+
+int surf_scene_camera(const surf_scene* scene, uint32_t width, uint32_t height, surf_camera_ubo* out) {
+    if (!scene || !out || width == 0 || height == 0) return SURF_ERR_INVALID;
+    /* main.cpp:141-149 */
+    surf::Camera cam(surf::Float3(0.0f, 0.0f, -7.0f), surf::Float3(0.0f, 0.0f, 0.0f), width, height, 70.0f, 7.0f, 0.5f);
+    *out = cam.toUBO();
+    return SURF_OK;
+}
+
+int surf_scene_bvh_depths(const surf_scene* scene, uint32_t* tlas_depth, uint32_t* max_blas_depth) {
+    if (!scene || !tlas_depth || !max_blas_depth) return SURF_ERR_INVALID;
+    *tlas_depth = scene->scene->tlas().depth();
+    uint32_t m = 0;
+    for (const auto& b : scene->blases) m = std::max(m, b->depth());
+    *max_blas_depth = m;
+    return SURF_OK;
+}
+
+void surf_scene_destroy(surf_scene* scene) { delete scene; }
+
+}  // extern "C"

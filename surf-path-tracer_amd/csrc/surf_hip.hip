@@ -1,0 +1,723 @@
+/*
+ * surf_hip.hip -- C-ABI implementation (include/surf_hip.h): device context,
+ * scene upload + re-layout, the wavefront render loop (hipGraph-captured
+ * phases), readback.  Replaces WaveFrontRenderer's Vulkan orchestration
+ * (renderer.cpp:604-1454) -- without its per-bounce host round trip: the
+ * host only polls a pinned counter block once per replayed graph of
+ * kPhasesPerGraph phases.
+ */
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "surf_hip.h"
+#include "device/wavefront_kernels.h"
+
+using namespace surfdev;
+
+namespace {
+
+constexpr int kPhasesPerGraph = 8;          /* even: parity returns to 0 after a replay */
+constexpr uint32_t kMaxStack = 120;          /* LDS stack entries per ray (block 256 -> 120 KiB max) */
+constexpr uint64_t kMaxIterations = 1ull << 22;  /* safety net: a path longer than this is a bug */
+
+std::mutex gErrMutex;
+std::string gLastError;
+
+void setGlobalError(const std::string& e) { std::lock_guard<std::mutex> l(gErrMutex); gLastError = e; }
+
+template <class T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    void release() { if (p) (void)hipFree(p); p = nullptr; n = 0; }
+};
+
+}  // namespace
+
+struct surf_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    uint32_t width = 0, height = 0;
+    std::vector<uint32_t> rows;
+    uint32_t npx = 0;
+    uint32_t capacity = 0;
+    uint32_t frameBatch = 16;
+    bool profiling = false;
+    std::string err;
+
+    /* scene */
+    bool hasScene = false;
+    DevScene S{};
+    std::vector<void*> sceneAllocs;
+    uint32_t stackDepth = 0;
+    uint32_t nInstances = 0, nTriangles = 0;
+    /* camera */
+    bool hasCamera = false;
+    DevCamera cam{};
+
+    /* wavefront state */
+    bool allocated = false;
+    Pool pool[2]{};
+    float4* hitTUV = nullptr;
+    uint32_t* hitInst = nullptr;
+    ShadowQ Q{};
+    float4* rad = nullptr;
+    size_t radCap = 0;
+    float4* acc = nullptr;
+    uint32_t* dRows = nullptr;
+    Counters* ctr = nullptr;
+    Counters* hctr = nullptr;      /* pinned */
+    uint32_t* dOutRGBA = nullptr;
+    std::vector<void*> wfAllocs;
+    uint64_t totalSamples = 0;
+
+    /* graph */
+    hipGraphExec_t graphExec = nullptr;
+    hipGraph_t graph = nullptr;
+    uint32_t gridWork = 0, gridRegen = 0;
+
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    surf_stats stats{};
+};
+
+#define SURF_CHECK(ctx, call)                                                             \
+    do {                                                                                  \
+        hipError_t e_ = (call);                                                           \
+        if (e_ != hipSuccess) {                                                           \
+            (ctx)->err = std::string(#call) + ": " + hipGetErrorString(e_);               \
+            setGlobalError((ctx)->err);                                                   \
+            return SURF_ERR_HIP;                                                          \
+        }                                                                                 \
+    } while (0)
+
+namespace {
+
+int fail(surf_ctx* c, int code, const std::string& msg) {
+    if (c) c->err = msg;
+    setGlobalError(msg);
+    return code;
+}
+
+template <class T>
+int devAlloc(surf_ctx* c, std::vector<void*>& list, T** out, size_t count) {
+    *out = nullptr;
+    if (count == 0) count = 1;
+    void* p = nullptr;
+    if (hipMalloc(&p, count * sizeof(T)) != hipSuccess || !p) {
+        return fail(c, SURF_ERR_OOM, "hipMalloc of " + std::to_string(count * sizeof(T)) + " bytes failed");
+    }
+    list.push_back(p);
+    *out = static_cast<T*>(p);
+    return SURF_OK;
+}
+
+void freeList(std::vector<void*>& list) {
+    for (void* p : list) (void)hipFree(p);
+    list.clear();
+}
+
+void destroyGraph(surf_ctx* c) {
+    if (c->graphExec) (void)hipGraphExecDestroy(c->graphExec);
+    if (c->graph) (void)hipGraphDestroy(c->graph);
+    c->graphExec = nullptr;
+    c->graph = nullptr;
+}
+
+size_t stackBytes(const surf_ctx* c) { return (size_t)c->stackDepth * kBlock * sizeof(uint32_t); }
+
+/* ----------------------------------------------------------- scene upload
+ * Walks every BLAS/TLAS from its root: validates indices (no kernel can
+ * fault on a malformed scene), measures depth, and emits the device node
+ * record that carries the children's boxes. */
+struct TreeWalk {
+    uint32_t depth = 0;
+    bool ok = true;
+    std::string why;
+};
+
+TreeWalk walkTree(const surf_bvh_node* nodes, uint32_t nodeCount, uint32_t offset, uint32_t idxCount, uint32_t idxOffset,
+                  std::vector<float4>& out, std::vector<uint8_t>& leafSeen) {
+    TreeWalk w;
+    std::vector<std::pair<uint32_t, uint32_t>> st{{0u, 0u}};
+    size_t visits = 0;
+    while (!st.empty()) {
+        auto [local, dep] = st.back();
+        st.pop_back();
+        if (++visits > (size_t)nodeCount + 1 || dep > 4096) { w.ok = false; w.why = "BVH has a cycle"; return w; }
+        const uint64_t g = (uint64_t)offset + local;
+        if (g >= nodeCount) { w.ok = false; w.why = "BVH node index out of range"; return w; }
+        const surf_bvh_node& n = nodes[g];
+        float4* rec = &out[4 * g];
+        rec[0].w = u2f(n.left_first);
+        rec[1].w = u2f(n.count);
+        if (n.count != 0) {
+            if ((uint64_t)idxOffset + n.left_first + n.count > idxCount) { w.ok = false; w.why = "BVH leaf range out of range"; return w; }
+            for (uint32_t k = 0; k < n.count; ++k) leafSeen[idxOffset + n.left_first + k] = 1;
+            w.depth = std::max(w.depth, dep);
+            continue;
+        }
+        const uint64_t l = (uint64_t)offset + n.left_first;
+        if (l + 1 >= nodeCount) { w.ok = false; w.why = "BVH child index out of range"; return w; }
+        const surf_bvh_node& L = nodes[l];
+        const surf_bvh_node& R = nodes[l + 1];
+        rec[0] = make_float4(L.bb_min.x, L.bb_min.y, L.bb_min.z, rec[0].w);
+        rec[1] = make_float4(L.bb_max.x, L.bb_max.y, L.bb_max.z, rec[1].w);
+        rec[2] = make_float4(R.bb_min.x, R.bb_min.y, R.bb_min.z, 0.0f);
+        rec[3] = make_float4(R.bb_max.x, R.bb_max.y, R.bb_max.z, 0.0f);
+        st.push_back({n.left_first + 1, dep + 1});
+        st.push_back({n.left_first, dep + 1});
+    }
+    return w;
+}
+
+template <class T>
+int upload(surf_ctx* c, const std::vector<T>& host, const T** devOut) {
+    T* d = nullptr;
+    int rc = devAlloc(c, c->sceneAllocs, &d, host.size());
+    if (rc) return rc;
+    if (!host.empty()) SURF_CHECK(c, hipMemcpy(d, host.data(), host.size() * sizeof(T), hipMemcpyHostToDevice));
+    *devOut = d;
+    return SURF_OK;
+}
+
+int allocWavefront(surf_ctx* c) {
+    if (c->allocated) return SURF_OK;
+    if (c->capacity == 0) {
+        /* default: enough paths to keep the chip busy through the RR tail */
+        const uint64_t want = (uint64_t)c->npx * std::max<uint32_t>(1u, std::min<uint32_t>(c->frameBatch, 4u));
+        c->capacity = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(want, 65536), 1u << 22);
+    }
+    const size_t cap = c->capacity;
+    int rc;
+    for (int p = 0; p < 2; ++p) {
+        if ((rc = devAlloc(c, c->wfAllocs, &c->pool[p].o, cap))) return rc;
+        if ((rc = devAlloc(c, c->wfAllocs, &c->pool[p].d, cap))) return rc;
+        if ((rc = devAlloc(c, c->wfAllocs, &c->pool[p].T, cap))) return rc;
+    }
+    if ((rc = devAlloc(c, c->wfAllocs, &c->hitTUV, cap))) return rc;
+    if ((rc = devAlloc(c, c->wfAllocs, &c->hitInst, cap))) return rc;
+    if ((rc = devAlloc(c, c->wfAllocs, &c->Q.o, cap))) return rc;
+    if ((rc = devAlloc(c, c->wfAllocs, &c->Q.d, cap))) return rc;
+    if ((rc = devAlloc(c, c->wfAllocs, &c->Q.c, cap))) return rc;
+    c->radCap = (size_t)c->npx * c->frameBatch;
+    if ((rc = devAlloc(c, c->wfAllocs, &c->rad, c->radCap))) return rc;
+    if ((rc = devAlloc(c, c->wfAllocs, &c->ctr, 1))) return rc;
+    if ((rc = devAlloc(c, c->wfAllocs, &c->dOutRGBA, c->npx))) return rc;
+    if (hipHostMalloc((void**)&c->hctr, sizeof(Counters), hipHostMallocDefault) != hipSuccess)
+        return fail(c, SURF_ERR_OOM, "hipHostMalloc of the counter block failed");
+    /* grid: 8 workgroups of 256 per CU saturate the 256-CU chip; grid-stride beyond */
+    int cus = 256;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, c->device) == hipSuccess && prop.multiProcessorCount > 0) cus = prop.multiProcessorCount;
+    const uint64_t maxBlocks = (cap + kBlock - 1) / kBlock;
+    c->gridWork = (uint32_t)std::min<uint64_t>(maxBlocks, (uint64_t)cus * 8);
+    c->gridRegen = (uint32_t)std::min<uint64_t>(maxBlocks, (uint64_t)cus * 8);
+    c->allocated = true;
+    return SURF_OK;
+}
+
+void launchPhase(surf_ctx* c, int par) {
+    const size_t lds = stackBytes(c);
+    hipLaunchKernelGGL(k_extend, dim3(c->gridWork), dim3(kBlock), lds, c->stream, c->S, c->pool[par], c->hitTUV, c->hitInst,
+                       (const Counters*)c->ctr, par);
+    hipLaunchKernelGGL(k_shade, dim3(c->gridWork), dim3(kBlock), 0, c->stream, c->S, c->pool[par], c->pool[par ^ 1], c->hitTUV,
+                       (const uint32_t*)c->hitInst, c->Q, c->rad, c->ctr, par);
+    hipLaunchKernelGGL(k_connect, dim3(c->gridWork), dim3(kBlock), lds, c->stream, c->S, c->Q, c->rad, c->ctr, par);
+    hipLaunchKernelGGL(k_regen, dim3(c->gridRegen), dim3(kBlock), 0, c->stream, c->cam, c->pool[par ^ 1], c->rad, c->ctr, par,
+                       c->capacity, (const uint32_t*)c->dRows, c->width, c->npx);
+}
+
+int buildGraph(surf_ctx* c) {
+    if (c->graphExec) return SURF_OK;
+    SURF_CHECK(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+    for (int ph = 0; ph < kPhasesPerGraph; ++ph) launchPhase(c, ph & 1);
+    hipError_t e = hipStreamEndCapture(c->stream, &c->graph);
+    if (e != hipSuccess) return fail(c, SURF_ERR_HIP, std::string("graph capture: ") + hipGetErrorString(e));
+    SURF_CHECK(c, hipGraphInstantiate(&c->graphExec, c->graph, nullptr, nullptr, 0));
+    return SURF_OK;
+}
+
+/* Which rows a shard owns. */
+std::vector<uint32_t> shardRows(uint32_t height, uint32_t shard, uint32_t shards, uint32_t block) {
+    std::vector<uint32_t> rows;
+    if (block == 0) {
+        const uint32_t r0 = (uint32_t)((uint64_t)height * shard / shards), r1 = (uint32_t)((uint64_t)height * (shard + 1) / shards);
+        for (uint32_t r = r0; r < r1; ++r) rows.push_back(r);
+    } else {
+        for (uint32_t r = 0; r < height; ++r)
+            if ((r / block) % shards == shard) rows.push_back(r);
+    }
+    return rows;
+}
+
+int createCtx(int dev, uint32_t w, uint32_t h, std::vector<uint32_t> rows, surf_ctx** out) {
+    if (!out) return fail(nullptr, SURF_ERR_INVALID, "out is NULL");
+    *out = nullptr;
+    if (w == 0 || h == 0 || rows.empty()) return fail(nullptr, SURF_ERR_INVALID, "empty frame or shard");
+    if ((uint64_t)w * rows.size() > (1ull << 31)) return fail(nullptr, SURF_ERR_INVALID, "shard too large");
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || dev < 0 || dev >= count) return fail(nullptr, SURF_ERR_NO_DEVICE, "no HIP device " + std::to_string(dev));
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return fail(nullptr, SURF_ERR_NO_DEVICE, "hipGetDeviceProperties failed");
+    if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos)
+        return fail(nullptr, SURF_ERR_NO_DEVICE, std::string("device is ") + prop.gcnArchName + ", this build targets gfx950");
+    auto* c = new surf_ctx();
+    c->device = dev;
+    c->width = w;
+    c->height = h;
+    c->rows = std::move(rows);
+    c->npx = (uint32_t)(w * c->rows.size());
+    if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+        delete c;
+        return fail(nullptr, SURF_ERR_HIP, "stream/event creation failed");
+    }
+    if (hipMalloc(&c->acc, (size_t)c->npx * sizeof(float4)) != hipSuccess ||
+        hipMalloc(&c->dRows, c->rows.size() * sizeof(uint32_t)) != hipSuccess) {
+        surf_destroy(c);
+        return fail(nullptr, SURF_ERR_OOM, "accumulator allocation failed");
+    }
+    (void)hipMemset(c->acc, 0, (size_t)c->npx * sizeof(float4));
+    (void)hipMemcpy(c->dRows, c->rows.data(), c->rows.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+    *out = c;
+    return SURF_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int surf_abi_version(void) { return SURF_ABI_VERSION; }
+
+int surf_device_count(int* count) {
+    if (!count) return SURF_ERR_INVALID;
+    *count = 0;
+    if (hipGetDeviceCount(count) != hipSuccess) { *count = 0; return fail(nullptr, SURF_ERR_NO_DEVICE, "hipGetDeviceCount failed"); }
+    return SURF_OK;
+}
+
+int surf_create(int dev, uint32_t w, uint32_t h, uint32_t r0, uint32_t r1, surf_ctx** out) {
+    if (r0 >= r1 || r1 > h) return fail(nullptr, SURF_ERR_INVALID, "row range out of frame");
+    std::vector<uint32_t> rows;
+    for (uint32_t r = r0; r < r1; ++r) rows.push_back(r);
+    return createCtx(dev, w, h, std::move(rows), out);
+}
+
+int surf_create_sharded(int dev, uint32_t w, uint32_t h, uint32_t shard, uint32_t shards, uint32_t block, surf_ctx** out) {
+    if (shards == 0 || shard >= shards) return fail(nullptr, SURF_ERR_INVALID, "bad shard index");
+    return createCtx(dev, w, h, shardRows(h, shard, shards, block), out);
+}
+
+void surf_destroy(surf_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    destroyGraph(c);
+    freeList(c->sceneAllocs);
+    freeList(c->wfAllocs);
+    if (c->hctr) (void)hipHostFree(c->hctr);
+    if (c->acc) (void)hipFree(c->acc);
+    if (c->dRows) (void)hipFree(c->dRows);
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const char* surf_last_error(const surf_ctx* c) {
+    if (c) return c->err.c_str();
+    std::lock_guard<std::mutex> l(gErrMutex);
+    static thread_local std::string copy;
+    copy = gLastError;
+    return copy.c_str();
+}
+
+int surf_shard_rows(const surf_ctx* c, uint32_t* rows, uint32_t* count) {
+    if (!c || !count) return SURF_ERR_INVALID;
+    if (rows) std::memcpy(rows, c->rows.data(), c->rows.size() * sizeof(uint32_t));
+    *count = (uint32_t)c->rows.size();
+    return SURF_OK;
+}
+
+int surf_set_pool_capacity(surf_ctx* c, uint32_t paths) {
+    if (!c || paths < 64) return SURF_ERR_INVALID;
+    if (c->allocated) return fail(c, SURF_ERR_INVALID, "pool capacity is fixed after the first render");
+    c->capacity = paths;
+    return SURF_OK;
+}
+
+int surf_set_frame_batch(surf_ctx* c, uint32_t frames) {
+    if (!c || frames == 0 || (uint64_t)frames * c->npx > (1ull << 31)) return SURF_ERR_INVALID;
+    if (c->allocated) return fail(c, SURF_ERR_INVALID, "frame batch is fixed after the first render");
+    c->frameBatch = frames;
+    return SURF_OK;
+}
+
+int surf_set_profiling(surf_ctx* c, int enabled) {
+    if (!c) return SURF_ERR_INVALID;
+    c->profiling = enabled != 0;
+    return SURF_OK;
+}
+
+int surf_upload_scene(surf_ctx* c, const surf_scene_desc* d) {
+    if (!c || !d) return SURF_ERR_INVALID;
+    if (d->triangle_count == 0 || !d->triangles || !d->tri_ext || !d->blas_indices || !d->blas_nodes || !d->materials ||
+        !d->instances || d->instance_count == 0 || !d->tlas_indices || !d->tlas_nodes || d->tlas_node_count == 0 ||
+        !d->background || d->material_count == 0 || d->blas_node_count == 0 || d->blas_index_count == 0 ||
+        (d->light_count && !d->lights))
+        return fail(c, SURF_ERR_INVALID, "incomplete scene descriptor");
+    SURF_CHECK(c, hipSetDevice(c->device));
+    SURF_CHECK(c, hipStreamSynchronize(c->stream));
+    destroyGraph(c);
+    freeList(c->sceneAllocs);
+    c->hasScene = false;
+
+    /* instances */
+    std::vector<DevInstance> inst(d->instance_count);
+    std::vector<int64_t> idxTri(d->blas_index_count, -1);   /* idx slot -> tri offset owner */
+    std::vector<float4> nodes((size_t)d->blas_node_count * 4, make_float4(0, 0, 0, 0));
+    std::vector<uint8_t> seen(d->blas_index_count, 0), walked(d->blas_node_count, 0);
+    uint32_t maxBlasDepth = 0;
+    for (uint32_t i = 0; i < d->instance_count; ++i) {
+        const surf_gpu_instance& g = d->instances[i];
+        if (g.tri_offset >= d->triangle_count || g.material_offset >= d->material_count ||
+            g.bvh_node_offset >= d->blas_node_count || g.bvh_idx_offset >= d->blas_index_count)
+            return fail(c, SURF_ERR_INVALID, "instance " + std::to_string(i) + " offsets out of range");
+        DevInstance& D = inst[i];
+        std::memcpy(D.Minv, g.inv_transform, sizeof D.Minv);
+        std::memcpy(D.M, g.transform, sizeof D.M);
+        D.triOffset = g.tri_offset; D.idxOffset = g.bvh_idx_offset; D.nodeOffset = g.bvh_node_offset; D.material = g.material_offset;
+        D.area = g.area;
+        if (!walked[g.bvh_node_offset]) {
+            std::vector<uint8_t> leaf(d->blas_index_count, 0);
+            TreeWalk w = walkTree(d->blas_nodes, d->blas_node_count, g.bvh_node_offset, d->blas_index_count, g.bvh_idx_offset, nodes, leaf);
+            if (!w.ok) return fail(c, SURF_ERR_INVALID, "instance " + std::to_string(i) + ": " + w.why);
+            maxBlasDepth = std::max(maxBlasDepth, w.depth);
+            walked[g.bvh_node_offset] = 1;
+            for (uint32_t k = 0; k < d->blas_index_count; ++k)
+                if (leaf[k]) {
+                    if (idxTri[k] >= 0 && idxTri[k] != (int64_t)g.tri_offset) return fail(c, SURF_ERR_INVALID, "BLAS index range shared by two meshes");
+                    idxTri[k] = g.tri_offset;
+                }
+        }
+    }
+    /* BVH-ordered triangles: (v0, prim), e1 = v1 - v0, e2 = v2 - v0 (mesh.cpp:25-26) */
+    std::vector<float4> tris((size_t)d->blas_index_count * 3, make_float4(0, 0, 0, 0));
+    for (uint32_t k = 0; k < d->blas_index_count; ++k) {
+        if (idxTri[k] < 0) continue;
+        const uint64_t t = (uint64_t)idxTri[k] + d->blas_indices[k];
+        if (t >= d->triangle_count) return fail(c, SURF_ERR_INVALID, "BLAS index " + std::to_string(k) + " out of range");
+        const surf_triangle& T = d->triangles[t];
+        tris[3 * (size_t)k + 0] = make_float4(T.v0.x, T.v0.y, T.v0.z, u2f(d->blas_indices[k]));
+        tris[3 * (size_t)k + 1] = make_float4(T.v1.x - T.v0.x, T.v1.y - T.v0.y, T.v1.z - T.v0.z, 0.0f);
+        tris[3 * (size_t)k + 2] = make_float4(T.v2.x - T.v0.x, T.v2.y - T.v0.y, T.v2.z - T.v0.z, 0.0f);
+    }
+    std::vector<float4> normals((size_t)d->triangle_count * 3), verts((size_t)d->triangle_count * 4);
+    for (uint32_t t = 0; t < d->triangle_count; ++t) {
+        const surf_tri_extension& x = d->tri_ext[t];
+        normals[3 * (size_t)t + 0] = make_float4(x.n0.x, x.n0.y, x.n0.z, 0.0f);
+        normals[3 * (size_t)t + 1] = make_float4(x.n1.x, x.n1.y, x.n1.z, 0.0f);
+        normals[3 * (size_t)t + 2] = make_float4(x.n2.x, x.n2.y, x.n2.z, 0.0f);
+        const surf_triangle& T = d->triangles[t];
+        verts[4 * (size_t)t + 0] = make_float4(T.v0.x, T.v0.y, T.v0.z, 0.0f);
+        verts[4 * (size_t)t + 1] = make_float4(T.v1.x, T.v1.y, T.v1.z, 0.0f);
+        verts[4 * (size_t)t + 2] = make_float4(T.v2.x, T.v2.y, T.v2.z, 0.0f);
+        verts[4 * (size_t)t + 3] = make_float4(T.centroid.x, T.centroid.y, T.centroid.z, 0.0f);
+    }
+    /* TLAS */
+    std::vector<float4> tnodes((size_t)d->tlas_node_count * 4, make_float4(0, 0, 0, 0));
+    std::vector<uint8_t> tseen(d->instance_count, 0);
+    TreeWalk tw = walkTree(d->tlas_nodes, d->tlas_node_count, 0, d->instance_count, 0, tnodes, tseen);
+    if (!tw.ok) return fail(c, SURF_ERR_INVALID, "TLAS: " + tw.why);
+    std::vector<uint32_t> tidx(d->tlas_indices, d->tlas_indices + d->instance_count);
+    for (uint32_t v : tidx) if (v >= d->instance_count) return fail(c, SURF_ERR_INVALID, "TLAS index out of range");
+    std::vector<uint2> lights(d->light_count);
+    for (uint32_t l = 0; l < d->light_count; ++l) {
+        const surf_light& L = d->lights[l];
+        if (L.light_instance_idx >= d->instance_count || L.primitive_count == 0 ||
+            (uint64_t)d->instances[L.light_instance_idx].tri_offset + L.primitive_count > d->triangle_count)
+            return fail(c, SURF_ERR_INVALID, "light " + std::to_string(l) + " out of range");
+        lights[l] = make_uint2(L.light_instance_idx, L.primitive_count);
+    }
+    std::vector<DevMaterial> mats(d->material_count);
+    std::memcpy(mats.data(), d->materials, d->material_count * sizeof(DevMaterial));
+
+    const uint32_t depth = tw.depth + maxBlasDepth + 1;
+    if (depth > kMaxStack) return fail(c, SURF_ERR_LIMIT, "BVH too deep for the LDS traversal stack (" + std::to_string(depth) + " entries)");
+
+    DevScene S{};
+    int rc;
+    if ((rc = upload(c, nodes, &S.nodes))) return rc;
+    if ((rc = upload(c, tris, &S.tris))) return rc;
+    if ((rc = upload(c, normals, &S.normals))) return rc;
+    if ((rc = upload(c, verts, &S.verts))) return rc;
+    if ((rc = upload(c, tnodes, &S.tlasNodes))) return rc;
+    if ((rc = upload(c, tidx, &S.tlasIdx))) return rc;
+    if ((rc = upload(c, inst, &S.inst))) return rc;
+    if ((rc = upload(c, mats, &S.mats))) return rc;
+    if ((rc = upload(c, lights, &S.lights))) return rc;
+    S.nLights = d->light_count;
+    const surf_background& bg = *d->background;
+    S.bgType = bg.type;
+    S.bgColor[0] = bg.color.x; S.bgColor[1] = bg.color.y; S.bgColor[2] = bg.color.z;
+    S.bgA[0] = bg.gradient_a.x; S.bgA[1] = bg.gradient_a.y; S.bgA[2] = bg.gradient_a.z;
+    S.bgB[0] = bg.gradient_b.x; S.bgB[1] = bg.gradient_b.y; S.bgB[2] = bg.gradient_b.z;
+    c->S = S;
+    c->stackDepth = depth;
+    c->nInstances = d->instance_count;
+    c->nTriangles = d->triangle_count;
+    c->hasScene = true;
+    return SURF_OK;
+}
+
+int surf_update_instances(surf_ctx* c, const surf_gpu_instance* instances, uint32_t n, const uint32_t* tlasIdx,
+                          const surf_bvh_node* tlasNodes, uint32_t nTlas, const surf_light* lights, uint32_t nLights) {
+    (void)instances; (void)n; (void)tlasIdx; (void)tlasNodes; (void)nTlas; (void)lights; (void)nLights;
+    return fail(c, SURF_ERR_INVALID, "surf_update_instances: re-upload the scene with surf_upload_scene (animation row f3 not built yet)");
+}
+
+int surf_set_camera(surf_ctx* c, const surf_camera_ubo* u) {
+    if (!c || !u) return SURF_ERR_INVALID;
+    if (!(u->resolution[0] > 0.0f) || !(u->resolution[1] > 0.0f)) return fail(c, SURF_ERR_INVALID, "camera resolution must be positive");
+    DevCamera k{};
+    const float pos[3] = {u->position.x, u->position.y, u->position.z};
+    std::memcpy(k.pos, pos, sizeof pos);
+    k.firstPixel[0] = u->first_pixel.x; k.firstPixel[1] = u->first_pixel.y; k.firstPixel[2] = u->first_pixel.z;
+    k.uVec[0] = u->u_vector.x; k.uVec[1] = u->u_vector.y; k.uVec[2] = u->u_vector.z;
+    k.vVec[0] = u->v_vector.x; k.vVec[1] = u->v_vector.y; k.vVec[2] = u->v_vector.z;
+    k.invW = 1.0f / u->resolution[0];
+    k.invH = 1.0f / u->resolution[1];
+    k.defocus = (u->defocus_angle == 0.0f) ? 0u : 1u;
+    /* sampleDefocusDisk constants (camera.h:73-75), computed once on the host */
+    const V3 up = mk3(u->up.x, u->up.y, u->up.z), fwd = mk3(u->fwd.x, u->fwd.y, u->fwd.z);
+    const V3 right = normalize(cross(up, fwd));
+    const float deg = u->defocus_angle / 2.0f;
+    const float radius = u->focal_length * tanf((deg * 3.14159265358979323846264f) * 0.005555555555555f);
+    const V3 du = scl(right, radius), dv = scl(lscl(-1.0f, up), radius);
+    k.diskU[0] = du.x; k.diskU[1] = du.y; k.diskU[2] = du.z;
+    k.diskV[0] = dv.x; k.diskV[1] = dv.y; k.diskV[2] = dv.z;
+    c->cam = k;
+    c->hasCamera = true;
+    destroyGraph(c);     /* camera is a kernel argument of the captured graph */
+    return SURF_OK;
+}
+
+int surf_render(surf_ctx* c, uint32_t frames, uint32_t firstFrame, uint32_t maxSeg, uint32_t spp) {
+    if (!c) return SURF_ERR_INVALID;
+    if (spp != 1) return fail(c, SURF_ERR_INVALID, "samples_per_frame must be 1 (render consecutive frames instead)");
+    if (!c->hasScene) return fail(c, SURF_ERR_NO_SCENE, "no scene uploaded");
+    if (!c->hasCamera) return fail(c, SURF_ERR_NO_SCENE, "no camera set");
+    if (frames == 0) return SURF_OK;
+    SURF_CHECK(c, hipSetDevice(c->device));
+    int rc = allocWavefront(c);
+    if (rc) return rc;
+    if (!c->profiling && (rc = buildGraph(c))) return rc;
+    std::memset(&c->stats, 0, sizeof c->stats);
+    c->stats.stack_depth = c->stackDepth;
+    c->stats.pool_capacity = c->capacity;
+    const size_t lds = stackBytes(c);
+    unsigned long long evTot[8] = {0};
+    uint64_t iterations = 0;
+    float msExt = 0, msShade = 0, msConn = 0, msRegen = 0, msAcc = 0;
+    hipEvent_t e[5];
+    if (c->profiling) for (auto& x : e) SURF_CHECK(c, hipEventCreate(&x));
+    SURF_CHECK(c, hipEventRecord(c->ev0, c->stream));
+    for (uint32_t b = 0; b < frames; b += c->frameBatch) {
+        const uint32_t F = std::min(c->frameBatch, frames - b);
+        Counters h{};
+        h.total = F * c->npx;
+        h.firstFrame = firstFrame + b;
+        h.maxSeg = maxSeg;
+        *c->hctr = h;
+        SURF_CHECK(c, hipMemcpyAsync(c->ctr, c->hctr, sizeof(Counters), hipMemcpyHostToDevice, c->stream));
+        /* kick: fill pool 0 as if phase parity 1 had just finished */
+        hipLaunchKernelGGL(k_regen, dim3(c->gridRegen), dim3(kBlock), 0, c->stream, c->cam, c->pool[0], c->rad, c->ctr, 1,
+                           c->capacity, (const uint32_t*)c->dRows, c->width, c->npx);
+        SURF_CHECK(c, hipGetLastError());
+        for (;;) {
+            if (c->profiling) {
+                for (int ph = 0; ph < 2; ++ph) {
+                    const int par = ph;
+                    SURF_CHECK(c, hipEventRecord(e[0], c->stream));
+                    hipLaunchKernelGGL(k_extend, dim3(c->gridWork), dim3(kBlock), lds, c->stream, c->S, c->pool[par], c->hitTUV,
+                                       c->hitInst, (const Counters*)c->ctr, par);
+                    SURF_CHECK(c, hipEventRecord(e[1], c->stream));
+                    hipLaunchKernelGGL(k_shade, dim3(c->gridWork), dim3(kBlock), 0, c->stream, c->S, c->pool[par], c->pool[par ^ 1],
+                                       c->hitTUV, (const uint32_t*)c->hitInst, c->Q, c->rad, c->ctr, par);
+                    SURF_CHECK(c, hipEventRecord(e[2], c->stream));
+                    hipLaunchKernelGGL(k_connect, dim3(c->gridWork), dim3(kBlock), lds, c->stream, c->S, c->Q, c->rad, c->ctr, par);
+                    SURF_CHECK(c, hipEventRecord(e[3], c->stream));
+                    hipLaunchKernelGGL(k_regen, dim3(c->gridRegen), dim3(kBlock), 0, c->stream, c->cam, c->pool[par ^ 1], c->rad, c->ctr,
+                                       par, c->capacity, (const uint32_t*)c->dRows, c->width, c->npx);
+                    SURF_CHECK(c, hipEventRecord(e[4], c->stream));
+                    SURF_CHECK(c, hipEventSynchronize(e[4]));
+                    float t;
+                    (void)hipEventElapsedTime(&t, e[0], e[1]); msExt += t;
+                    (void)hipEventElapsedTime(&t, e[1], e[2]); msShade += t;
+                    (void)hipEventElapsedTime(&t, e[2], e[3]); msConn += t;
+                    (void)hipEventElapsedTime(&t, e[3], e[4]); msRegen += t;
+                    c->stats.launches_extend++;
+                }
+                iterations += 2;
+            } else {
+                SURF_CHECK(c, hipGraphLaunch(c->graphExec, c->stream));
+                iterations += kPhasesPerGraph;
+            }
+            SURF_CHECK(c, hipMemcpyAsync(c->hctr, c->ctr, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
+            SURF_CHECK(c, hipStreamSynchronize(c->stream));
+            if (c->hctr->nIn[0] == 0) break;
+            if (iterations > kMaxIterations)
+                return fail(c, SURF_ERR_LIMIT, "wavefront did not drain after " + std::to_string(iterations) + " iterations");
+        }
+        for (int k = 0; k < 8; ++k) evTot[k] += c->hctr->ev[k];
+        if (c->profiling) SURF_CHECK(c, hipEventRecord(e[0], c->stream));
+        hipLaunchKernelGGL(k_accumulate, dim3((c->npx + kBlock - 1) / kBlock), dim3(kBlock), 0, c->stream,
+                           (const float4*)c->rad, c->acc, c->npx, F);
+        SURF_CHECK(c, hipGetLastError());
+        if (c->profiling) {
+            SURF_CHECK(c, hipEventRecord(e[1], c->stream));
+            SURF_CHECK(c, hipEventSynchronize(e[1]));
+            float t; (void)hipEventElapsedTime(&t, e[0], e[1]); msAcc += t;
+        }
+    }
+    SURF_CHECK(c, hipEventRecord(c->ev1, c->stream));
+    SURF_CHECK(c, hipEventSynchronize(c->ev1));
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, c->ev0, c->ev1);
+    if (c->profiling) for (auto& x : e) (void)hipEventDestroy(x);
+    c->totalSamples += frames;
+    surf_stats& s = c->stats;
+    s.samples = (uint64_t)frames * c->npx;
+    s.n_ext = evTot[0]; s.n_hit = evTot[1]; s.n_cont = evTot[2]; s.n_shadow = evTot[3]; s.n_acc = evTot[4]; s.n_unocc = evTot[5];
+    s.tail_paths = evTot[6];
+    s.iterations = iterations;
+    s.ms_total = ms;
+    s.ms_extend = msExt; s.ms_shade = msShade; s.ms_connect = msConn; s.ms_regen = msRegen; s.ms_accum = msAcc;
+    return SURF_OK;
+}
+
+int surf_clear_accumulator(surf_ctx* c) {
+    if (!c) return SURF_ERR_INVALID;
+    SURF_CHECK(c, hipSetDevice(c->device));
+    SURF_CHECK(c, hipMemsetAsync(c->acc, 0, (size_t)c->npx * sizeof(float4), c->stream));
+    SURF_CHECK(c, hipStreamSynchronize(c->stream));
+    c->totalSamples = 0;
+    return SURF_OK;
+}
+
+int surf_read_accumulator(surf_ctx* c, float* out) {
+    if (!c || !out) return SURF_ERR_INVALID;
+    SURF_CHECK(c, hipSetDevice(c->device));
+    SURF_CHECK(c, hipMemcpyAsync(out, c->acc, (size_t)c->npx * sizeof(float4), hipMemcpyDeviceToHost, c->stream));
+    SURF_CHECK(c, hipStreamSynchronize(c->stream));
+    return SURF_OK;
+}
+
+int surf_copy_accumulator_device(surf_ctx* c, void* dst) {
+    if (!c || !dst) return SURF_ERR_INVALID;
+    SURF_CHECK(c, hipSetDevice(c->device));
+    SURF_CHECK(c, hipMemcpyAsync(dst, c->acc, (size_t)c->npx * sizeof(float4), hipMemcpyDeviceToDevice, c->stream));
+    SURF_CHECK(c, hipStreamSynchronize(c->stream));
+    return SURF_OK;
+}
+
+int surf_finalize_rgba8(surf_ctx* c, uint32_t* out) {
+    if (!c || !out) return SURF_ERR_INVALID;
+    if (c->totalSamples == 0) return fail(c, SURF_ERR_INVALID, "nothing rendered since the last clear");
+    SURF_CHECK(c, hipSetDevice(c->device));
+    int rc = allocWavefront(c);
+    if (rc) return rc;
+    const float inv = 1.0f / (float)c->totalSamples;     /* renderer.cpp:160 */
+    hipLaunchKernelGGL(k_finalize, dim3((c->npx + kBlock - 1) / kBlock), dim3(kBlock), 0, c->stream, (const float4*)c->acc,
+                       c->dOutRGBA, c->npx, inv);
+    SURF_CHECK(c, hipGetLastError());
+    SURF_CHECK(c, hipMemcpyAsync(out, c->dOutRGBA, (size_t)c->npx * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+    SURF_CHECK(c, hipStreamSynchronize(c->stream));
+    return SURF_OK;
+}
+
+int surf_get_stats(surf_ctx* c, surf_stats* out) {
+    if (!c || !out) return SURF_ERR_INVALID;
+    *out = c->stats;
+    if (c->totalSamples) {
+        /* Lumen energy, renderer.cpp:191-201 (serial sum of r+g+b of acc/N) */
+        std::vector<float> acc((size_t)c->npx * 4);
+        int rc = surf_read_accumulator(c, acc.data());
+        if (rc) return rc;
+        const float inv = 1.0f / (float)c->totalSamples;
+        float e = 0.0f;
+        for (size_t p = 0; p < c->npx; ++p) e = e + (((acc[4 * p] * inv) + (acc[4 * p + 1] * inv)) + (acc[4 * p + 2] * inv));
+        out->energy = e;
+    }
+    return SURF_OK;
+}
+
+int surf_synchronize(surf_ctx* c) {
+    if (!c) return SURF_ERR_INVALID;
+    SURF_CHECK(c, hipSetDevice(c->device));
+    SURF_CHECK(c, hipStreamSynchronize(c->stream));
+    return SURF_OK;
+}
+
+int surf_trace_closest(surf_ctx* c, uint32_t n, const float* o, const float* d, float* ot, float* ou, float* ov,
+                       uint32_t* oi, uint32_t* op) {
+    if (!c || (n && (!o || !d || !ot || !ou || !ov || !oi || !op))) return SURF_ERR_INVALID;
+    if (!c->hasScene) return fail(c, SURF_ERR_NO_SCENE, "no scene uploaded");
+    if (n == 0) return SURF_OK;
+    SURF_CHECK(c, hipSetDevice(c->device));
+    std::vector<void*> tmp;
+    float *dO, *dD; float4* dT; uint2* dI;
+    int rc;
+    if ((rc = devAlloc(c, tmp, &dO, 3 * (size_t)n)) || (rc = devAlloc(c, tmp, &dD, 3 * (size_t)n)) ||
+        (rc = devAlloc(c, tmp, &dT, n)) || (rc = devAlloc(c, tmp, &dI, n))) { freeList(tmp); return rc; }
+    (void)hipMemcpyAsync(dO, o, 12 * (size_t)n, hipMemcpyHostToDevice, c->stream);
+    (void)hipMemcpyAsync(dD, d, 12 * (size_t)n, hipMemcpyHostToDevice, c->stream);
+    hipLaunchKernelGGL(k_trace_closest, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), stackBytes(c), c->stream, c->S,
+                       (const float*)dO, (const float*)dD, n, dT, dI);
+    std::vector<float4> t(n);
+    std::vector<uint2> ip(n);
+    (void)hipMemcpyAsync(t.data(), dT, 16 * (size_t)n, hipMemcpyDeviceToHost, c->stream);
+    (void)hipMemcpyAsync(ip.data(), dI, 8 * (size_t)n, hipMemcpyDeviceToHost, c->stream);
+    hipError_t e = hipStreamSynchronize(c->stream);
+    freeList(tmp);
+    if (e != hipSuccess) return fail(c, SURF_ERR_HIP, std::string("trace_closest: ") + hipGetErrorString(e));
+    for (uint32_t i = 0; i < n; ++i) { ot[i] = t[i].x; ou[i] = t[i].y; ov[i] = t[i].z; oi[i] = ip[i].x; op[i] = ip[i].y; }
+    return SURF_OK;
+}
+
+int surf_trace_any(surf_ctx* c, uint32_t n, const float* o, const float* d, const float* tm, uint8_t* occ) {
+    if (!c || (n && (!o || !d || !tm || !occ))) return SURF_ERR_INVALID;
+    if (!c->hasScene) return fail(c, SURF_ERR_NO_SCENE, "no scene uploaded");
+    if (n == 0) return SURF_OK;
+    SURF_CHECK(c, hipSetDevice(c->device));
+    std::vector<void*> tmp;
+    float *dO, *dD, *dM; uint8_t* dR;
+    int rc;
+    if ((rc = devAlloc(c, tmp, &dO, 3 * (size_t)n)) || (rc = devAlloc(c, tmp, &dD, 3 * (size_t)n)) ||
+        (rc = devAlloc(c, tmp, &dM, n)) || (rc = devAlloc(c, tmp, &dR, n))) { freeList(tmp); return rc; }
+    (void)hipMemcpyAsync(dO, o, 12 * (size_t)n, hipMemcpyHostToDevice, c->stream);
+    (void)hipMemcpyAsync(dD, d, 12 * (size_t)n, hipMemcpyHostToDevice, c->stream);
+    (void)hipMemcpyAsync(dM, tm, 4 * (size_t)n, hipMemcpyHostToDevice, c->stream);
+    hipLaunchKernelGGL(k_trace_any, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), stackBytes(c), c->stream, c->S,
+                       (const float*)dO, (const float*)dD, (const float*)dM, n, dR);
+    (void)hipMemcpyAsync(occ, dR, n, hipMemcpyDeviceToHost, c->stream);
+    hipError_t e = hipStreamSynchronize(c->stream);
+    freeList(tmp);
+    if (e != hipSuccess) return fail(c, SURF_ERR_HIP, std::string("trace_any: ") + hipGetErrorString(e));
+    return SURF_OK;
+}
+
+/* Host restatements of the glibc kernels' libm, for CPU tests (same source as the device). */
+float surf_ref_sinf(float x) { return surfdev::gSinf(x); }
+float surf_ref_cosf(float x) { return surfdev::gCosf(x); }
+float surf_ref_expf(float x) { return surfdev::gExpf(x); }
+
+}  // extern "C"

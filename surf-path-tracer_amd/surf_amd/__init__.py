@@ -1,0 +1,307 @@
+"""ctypes binding of libsurf_hip.so (include/surf_hip.h).
+
+Python is test/bench plumbing here: the product is the C-ABI library (HIP
+kernels for gfx950 + C++ host API).  Importing this module never falls back
+to anything: if the library is missing, `load()` raises.
+
+Mirrors the reference interface for the hot path:
+  Scene.indoor(...)            main.cpp:161-346 scene (Mesh/BvhBLAS/Instance/GPUScene)
+  Renderer(...)                WaveFrontRenderer (renderer.h:207-436)
+    .render(frames, first)     render loop, one sample per pixel per frame
+    .clear_accumulator()       IRenderer::clearAccumulator
+    .accumulator()             float RGBA accumulator (rows of this shard)
+    .finalize_rgba8()          wavefront_finalize.comp + RgbaToU32
+    .trace_closest/.trace_any  ray_extend / ray_connect traversal (tests)
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+_PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(_PKG, "lib", "libsurf_hip.so")
+REPO_ROOT = os.path.dirname(_PKG)
+ASSETS_DIR = os.path.join(REPO_ROOT, "assets")
+
+SURF_OK = 0
+_STATUS = {
+    -1: "SURF_ERR_INVALID", -2: "SURF_ERR_HIP", -3: "SURF_ERR_NO_DEVICE", -4: "SURF_ERR_NO_SCENE",
+    -5: "SURF_ERR_OOM", -6: "SURF_ERR_IO", -7: "SURF_ERR_LIMIT",
+}
+
+
+class SurfError(RuntimeError):
+    def __init__(self, code: int, what: str, detail: str):
+        super().__init__(f"{what} failed: {_STATUS.get(code, code)}: {detail}")
+        self.code = code
+
+
+class SceneDesc(C.Structure):
+    _fields_ = [
+        ("triangles", C.c_void_p), ("triangle_count", C.c_uint32),
+        ("tri_ext", C.c_void_p),
+        ("blas_indices", C.c_void_p), ("blas_index_count", C.c_uint32),
+        ("blas_nodes", C.c_void_p), ("blas_node_count", C.c_uint32),
+        ("materials", C.c_void_p), ("material_count", C.c_uint32),
+        ("instances", C.c_void_p), ("instance_count", C.c_uint32),
+        ("tlas_indices", C.c_void_p),
+        ("tlas_nodes", C.c_void_p), ("tlas_node_count", C.c_uint32),
+        ("lights", C.c_void_p), ("light_count", C.c_uint32),
+        ("background", C.c_void_p),
+    ]
+
+
+class Stats(C.Structure):
+    _fields_ = [
+        ("samples", C.c_uint64), ("n_ext", C.c_uint64), ("n_hit", C.c_uint64), ("n_cont", C.c_uint64),
+        ("n_shadow", C.c_uint64), ("n_acc", C.c_uint64), ("n_unocc", C.c_uint64), ("iterations", C.c_uint64),
+        ("tail_paths", C.c_uint64),
+        ("ms_total", C.c_double), ("ms_extend", C.c_double), ("ms_shade", C.c_double), ("ms_connect", C.c_double),
+        ("ms_regen", C.c_double), ("ms_tail", C.c_double), ("ms_accum", C.c_double),
+        ("launches_extend", C.c_uint64),
+        ("stack_depth", C.c_uint32), ("pool_capacity", C.c_uint32),
+        ("energy", C.c_float), ("_pad", C.c_uint32),
+    ]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_ if not k.startswith("_")}
+
+
+CameraUBO = C.c_uint8 * 128
+
+_lib = None
+
+# Byte sizes of the reference records (include/surf_hip.h static_asserts).
+RECORD_BYTES = {"triangles": 64, "tri_ext": 80, "blas_indices": 4, "blas_nodes": 48, "materials": 64,
+                "instances": 160, "tlas_indices": 4, "tlas_nodes": 48, "lights": 8, "background": 64}
+
+
+def load() -> C.CDLL:
+    """Loads libsurf_hip.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise FileNotFoundError(f"{LIB_PATH} not built: run `make -C surf-path-tracer_amd` or __graft_entry__.build()")
+    lib = C.CDLL(LIB_PATH)
+    P, U32, I32, F = C.c_void_p, C.c_uint32, C.c_int, C.c_float
+    sig = {
+        "surf_abi_version": ([], I32), "surf_device_count": ([C.POINTER(I32)], I32),
+        "surf_create": ([I32, U32, U32, U32, U32, C.POINTER(P)], I32),
+        "surf_create_sharded": ([I32, U32, U32, U32, U32, U32, C.POINTER(P)], I32),
+        "surf_destroy": ([P], None), "surf_last_error": ([P], C.c_char_p),
+        "surf_shard_rows": ([P, P, C.POINTER(U32)], I32),
+        "surf_set_pool_capacity": ([P, U32], I32), "surf_set_frame_batch": ([P, U32], I32),
+        "surf_set_profiling": ([P, I32], I32),
+        "surf_upload_scene": ([P, C.POINTER(SceneDesc)], I32),
+        "surf_set_camera": ([P, P], I32),
+        "surf_render": ([P, U32, U32, U32, U32], I32),
+        "surf_clear_accumulator": ([P], I32), "surf_read_accumulator": ([P, P], I32),
+        "surf_copy_accumulator_device": ([P, P], I32), "surf_finalize_rgba8": ([P, P], I32),
+        "surf_get_stats": ([P, C.POINTER(Stats)], I32), "surf_synchronize": ([P], I32),
+        "surf_trace_closest": ([P, U32, P, P, P, P, P, P, P], I32),
+        "surf_trace_any": ([P, U32, P, P, P, P], I32),
+        "surf_scene_build_indoor": ([C.c_char_p, I32, C.POINTER(P)], I32),
+        "surf_scene_desc_get": ([P, C.POINTER(SceneDesc)], I32),
+        "surf_scene_camera": ([P, U32, U32, P], I32),
+        "surf_scene_bvh_depths": ([P, C.POINTER(U32), C.POINTER(U32)], I32),
+        "surf_scene_destroy": ([P], None),
+        "surf_ref_sinf": ([F], F), "surf_ref_cosf": ([F], F), "surf_ref_expf": ([F], F),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    _lib = lib
+    return lib
+
+
+def _check(rc: int, what: str, ctx=None):
+    if rc != SURF_OK:
+        detail = load().surf_last_error(ctx)
+        raise SurfError(rc, what, detail.decode() if detail else "")
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    rc = load().surf_device_count(C.byref(n))
+    return n.value if rc == SURF_OK else 0
+
+
+class Scene:
+    """Host scene built by the product's C++ host API (OBJ -> BVH -> GPUBatcher layout)."""
+
+    def __init__(self, handle):
+        self._h = handle
+
+    @classmethod
+    def indoor(cls, assets_dir: str = ASSETS_DIR, variant: int = 0) -> "Scene":
+        h = C.c_void_p()
+        _check(load().surf_scene_build_indoor(assets_dir.encode(), variant, C.byref(h)), "surf_scene_build_indoor")
+        return cls(h)
+
+    @property
+    def handle(self):
+        return self._h
+
+    def desc(self) -> SceneDesc:
+        d = SceneDesc()
+        _check(load().surf_scene_desc_get(self._h, C.byref(d)), "surf_scene_desc_get")
+        return d
+
+    def camera(self, width: int, height: int) -> bytes:
+        ubo = CameraUBO()
+        _check(load().surf_scene_camera(self._h, width, height, ubo), "surf_scene_camera")
+        return bytes(ubo)
+
+    def bvh_depths(self) -> tuple[int, int]:
+        t, b = C.c_uint32(), C.c_uint32()
+        _check(load().surf_scene_bvh_depths(self._h, C.byref(t), C.byref(b)), "surf_scene_bvh_depths")
+        return t.value, b.value
+
+    def buffers(self) -> dict[str, bytes]:
+        """The ten reference-layout buffers of the GPUScene, as bytes."""
+        d = self.desc()
+        counts = {"triangles": d.triangle_count, "tri_ext": d.triangle_count, "blas_indices": d.blas_index_count,
+                  "blas_nodes": d.blas_node_count, "materials": d.material_count, "instances": d.instance_count,
+                  "tlas_indices": d.instance_count, "tlas_nodes": d.tlas_node_count, "lights": d.light_count,
+                  "background": 1}
+        out = {}
+        for k, n in counts.items():
+            ptr = getattr(d, k)
+            out[k] = C.string_at(ptr, n * RECORD_BYTES[k]) if n else b""
+        return out
+
+    def close(self):
+        if self._h:
+            load().surf_scene_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+@dataclass
+class ShardSpec:
+    shard: int = 0
+    shards: int = 1
+    row_block: int = 0      # 0: contiguous rows; N: interleaved blocks of N rows
+
+
+def shard_rows(height: int, spec: ShardSpec) -> np.ndarray:
+    """Rows a shard owns -- same rule as surf_create_sharded."""
+    r = np.arange(height, dtype=np.int64)
+    if spec.row_block == 0:
+        lo = height * spec.shard // spec.shards
+        hi = height * (spec.shard + 1) // spec.shards
+        return r[lo:hi]
+    return r[(r // spec.row_block) % spec.shards == spec.shard]
+
+
+def assemble_shards(width: int, height: int, parts: list[np.ndarray], specs: list[ShardSpec]) -> np.ndarray:
+    """Places per-shard accumulator rows (shard order) into a full (H, W, 4) frame."""
+    full = np.zeros((height, width, 4), dtype=np.float32)
+    for part, spec in zip(parts, specs):
+        rows = shard_rows(height, spec)
+        full[rows] = np.asarray(part, dtype=np.float32).reshape(len(rows), width, 4)
+    return full
+
+
+class Renderer:
+    """One surf_ctx: a shard of a width x height frame on one HIP device."""
+
+    def __init__(self, scene: Scene, width: int, height: int, device: int = 0, shard: ShardSpec | None = None,
+                 pool_capacity: int | None = None, frame_batch: int | None = None, camera: bytes | None = None):
+        lib = load()
+        self.width, self.height = width, height
+        self.shard = shard or ShardSpec()
+        h = C.c_void_p()
+        _check(lib.surf_create_sharded(device, width, height, self.shard.shard, self.shard.shards,
+                                       self.shard.row_block, C.byref(h)), "surf_create_sharded")
+        self._h = h
+        n = C.c_uint32()
+        _check(lib.surf_shard_rows(h, None, C.byref(n)), "surf_shard_rows", h)
+        self.rows = np.zeros(n.value, dtype=np.uint32)
+        _check(lib.surf_shard_rows(h, _ptr(self.rows), C.byref(n)), "surf_shard_rows", h)
+        if pool_capacity:
+            _check(lib.surf_set_pool_capacity(h, pool_capacity), "surf_set_pool_capacity", h)
+        if frame_batch:
+            _check(lib.surf_set_frame_batch(h, frame_batch), "surf_set_frame_batch", h)
+        d = scene.desc()
+        _check(lib.surf_upload_scene(h, C.byref(d)), "surf_upload_scene", h)
+        ubo = camera if camera is not None else scene.camera(width, height)
+        buf = CameraUBO.from_buffer_copy(ubo)
+        _check(lib.surf_set_camera(h, buf), "surf_set_camera", h)
+
+    @property
+    def handle(self):
+        return self._h
+
+    def set_profiling(self, on: bool):
+        _check(load().surf_set_profiling(self._h, 1 if on else 0), "surf_set_profiling", self._h)
+
+    def render(self, frames: int, first_frame: int = 0, max_segments: int = 0):
+        _check(load().surf_render(self._h, frames, first_frame, max_segments, 1), "surf_render", self._h)
+
+    def synchronize(self):
+        _check(load().surf_synchronize(self._h), "surf_synchronize", self._h)
+
+    def clear_accumulator(self):
+        _check(load().surf_clear_accumulator(self._h), "surf_clear_accumulator", self._h)
+
+    def accumulator(self) -> np.ndarray:
+        out = np.zeros((len(self.rows), self.width, 4), dtype=np.float32)
+        _check(load().surf_read_accumulator(self._h, _ptr(out)), "surf_read_accumulator", self._h)
+        return out
+
+    def copy_accumulator_to(self, device_ptr: int):
+        _check(load().surf_copy_accumulator_device(self._h, C.c_void_p(device_ptr)), "surf_copy_accumulator_device", self._h)
+
+    def finalize_rgba8(self) -> np.ndarray:
+        out = np.zeros((len(self.rows), self.width), dtype=np.uint32)
+        _check(load().surf_finalize_rgba8(self._h, _ptr(out)), "surf_finalize_rgba8", self._h)
+        return out
+
+    def stats(self) -> dict:
+        s = Stats()
+        _check(load().surf_get_stats(self._h, C.byref(s)), "surf_get_stats", self._h)
+        return s.as_dict()
+
+    def trace_closest(self, o: np.ndarray, d: np.ndarray):
+        o = np.ascontiguousarray(o, dtype=np.float32).reshape(-1, 3)
+        d = np.ascontiguousarray(d, dtype=np.float32).reshape(-1, 3)
+        n = len(o)
+        t, u, v = (np.zeros(n, np.float32) for _ in range(3))
+        inst, prim = np.zeros(n, np.uint32), np.zeros(n, np.uint32)
+        _check(load().surf_trace_closest(self._h, n, _ptr(o), _ptr(d), _ptr(t), _ptr(u), _ptr(v), _ptr(inst), _ptr(prim)),
+               "surf_trace_closest", self._h)
+        return t, u, v, inst, prim
+
+    def trace_any(self, o: np.ndarray, d: np.ndarray, tmax: np.ndarray) -> np.ndarray:
+        o = np.ascontiguousarray(o, dtype=np.float32).reshape(-1, 3)
+        d = np.ascontiguousarray(d, dtype=np.float32).reshape(-1, 3)
+        tmax = np.ascontiguousarray(tmax, dtype=np.float32)
+        occ = np.zeros(len(o), np.uint8)
+        _check(load().surf_trace_any(self._h, len(o), _ptr(o), _ptr(d), _ptr(tmax), _ptr(occ)), "surf_trace_any", self._h)
+        return occ
+
+    def close(self):
+        if self._h:
+            load().surf_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

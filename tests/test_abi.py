@@ -1,0 +1,54 @@
+"""The C-ABI library loads and exports every symbol include/surf_hip.h declares
+(no compute calls: this runs without a GPU)."""
+import os
+import re
+import subprocess
+
+import surf_amd
+
+HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "surf_hip.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(surf_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_declares_the_boundary():
+    fns = declared_functions()
+    for must in ["surf_create", "surf_upload_scene", "surf_set_camera", "surf_render", "surf_clear_accumulator",
+                 "surf_read_accumulator", "surf_finalize_rgba8", "surf_get_stats", "surf_last_error", "surf_destroy"]:
+        assert must in fns
+
+
+def test_library_exports_every_declared_symbol():
+    lib = surf_amd.load()
+    missing = [f for f in declared_functions() if not hasattr(lib, f)]
+    assert not missing, missing
+    assert lib.surf_abi_version() == 1
+
+
+def test_exports_are_c_linkage():
+    out = subprocess.run(["nm", "-D", "--defined-only", surf_amd.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    syms = {line.split()[-1] for line in out.splitlines() if line.strip()}
+    for f in declared_functions():
+        assert f in syms, f
+
+
+def test_code_object_targets_gfx950():
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf" if os.path.exists("/opt/rocm/lib/llvm/bin/llvm-readelf") else "readelf",
+                          "-S", surf_amd.LIB_PATH], capture_output=True, text=True).stdout
+    assert ".hip_fatbin" in out
+    blob = open(surf_amd.LIB_PATH, "rb").read()
+    assert b"gfx950" in blob
+
+
+def test_errors_are_returned_not_raised():
+    lib = surf_amd.load()
+    import ctypes as C
+    h = C.c_void_p()
+    # bad arguments never abort: they return SURF_ERR_INVALID
+    assert lib.surf_create(0, 0, 0, 0, 0, C.byref(h)) == -1
+    assert lib.surf_render(None, 1, 0, 0, 1) == -1
+    assert lib.surf_scene_build_indoor(b"/nonexistent", 0, C.byref(h)) == -6
