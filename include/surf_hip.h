@@ -111,7 +111,7 @@ typedef struct {
 } surf_scene_desc;
 
 typedef struct {
-    uint64_t samples;          /* camera samples finished (Mrays/s numerator, main.cpp:431) */
+    uint64_t samples;          /* camera samples rendered since the last clear (Mrays/s numerator, main.cpp:431) */
     uint64_t n_ext;            /* extension rays traced */
     uint64_t n_hit;            /* extension rays that hit geometry */
     uint64_t n_cont;           /* continuation rays */
@@ -120,9 +120,9 @@ typedef struct {
     uint64_t n_unocc;          /* unoccluded shadow rays */
     uint64_t iterations;       /* wavefront iterations (extend->shade->connect->regen) */
     uint64_t tail_paths;       /* paths finished by the tail kernel */
-    double   ms_total;         /* device time of the last surf_render */
+    double   ms_total;         /* device time of render + drain calls since the last clear */
     double   ms_extend, ms_shade, ms_connect, ms_regen, ms_tail, ms_accum;  /* per-kernel (surf_set_profiling) */
-    uint64_t launches_extend;  /* extend launches that did work (profiling mode) */
+    uint64_t launches_extend;  /* k_extend launches timed (profiling mode) */
     uint32_t stack_depth;      /* traversal stack entries reserved per ray */
     uint32_t pool_capacity;    /* paths in flight */
     float    energy;           /* sum of acc.rgb / samples over the shard ("Lumen", renderer.cpp:191-201) */
@@ -153,8 +153,23 @@ int surf_shard_rows(const surf_ctx* ctx, uint32_t* rows, uint32_t* row_count);
 /* Paths in flight (default: sized from the shard, >= 1M when possible). Must be
  * called before the first render. */
 int surf_set_pool_capacity(surf_ctx* ctx, uint32_t paths);
-/* Frames rendered concurrently per internal batch (default 16). */
+/* Frame window (default 256, at most 16 GiB of radiance slots): frames whose
+ * samples may be in flight at once.
+ * Sample radiance is held per (frame slot, pixel) until a frame completes and
+ * is accumulated in frame order; long Russian-roulette paths of old frames
+ * overlap the bulk of newer ones instead of stalling each render call. */
 int surf_set_frame_batch(surf_ctx* ctx, uint32_t frames);
+/* Zero-throughput cutoff (default on): a path whose throughput T is exactly
+ * (0,0,0) ends early.  Every later contribution would be T * finite = +0, so
+ * the radiance is bit-identical to the reference's (tests check it against the
+ * oracle run without the cutoff); only n_ext/n_cont/... shrink.  It bounds the
+ * total-internal-reflection orbits in the glass lens, which the reference
+ * traces for up to millions of segments. */
+int surf_set_zero_cutoff(surf_ctx* ctx, int enabled);
+/* Diagnostics: how many paths the segment cap ended in the current sample
+ * stream, and the sample ids (frame slot * shard pixels + pixel) of the first
+ * min(count, 64, max). */
+int surf_debug_capped(surf_ctx* ctx, uint32_t* sample_ids, uint32_t max, uint64_t* count);
 /* When enabled, per-kernel device times are measured with HIP events on the
  * render stream (slower: disables the graph replay). */
 int surf_set_profiling(surf_ctx* ctx, int enabled);
@@ -173,7 +188,10 @@ int surf_set_camera(surf_ctx* ctx, const surf_camera_ubo* camera);
  * (renderer.cpp:169) and accumulates (rgb, 1) per sample in frame order.
  * max_segments: 0 = unbounded + Russian roulette (reference semantics);
  * N > 0 caps each path at N extension rays.  samples_per_frame must be 1
- * (multi-sample frames are expressed as consecutive frames). */
+ * (multi-sample frames are expressed as consecutive frames).  Returns once every
+ * sample is issued: consecutive calls form one sample stream, so the last long
+ * paths of a call overlap the next call; any read (accumulator, stats,
+ * finalize, synchronize) drains the stream first. */
 int surf_render(surf_ctx* ctx, uint32_t frames, uint32_t first_frame_index,
                 uint32_t max_segments, uint32_t samples_per_frame);
 int surf_clear_accumulator(surf_ctx* ctx);

@@ -56,6 +56,7 @@ def load():
         "orc_init_seed": ([U32], U32), "orc_random_u32": ([C.POINTER(U32)], U32),
         "orc_random_f32": ([C.POINTER(U32)], F),
         "orc_finalize_rgba8": ([P, U32, F, P], None),
+        "orc_set_zero_cutoff": ([I32], None),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)
@@ -164,6 +165,11 @@ class OracleScene:
             self.close()
         except Exception:
             pass
+
+
+def set_zero_cutoff(on: bool):
+    """Radiance-neutral early end of zero-throughput paths (default off = reference)."""
+    load().orc_set_zero_cutoff(1 if on else 0)
 
 
 def init_seed(s: int) -> int:

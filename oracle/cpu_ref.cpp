@@ -670,6 +670,18 @@ struct Recorder {
 
 struct Counters { uint64_t ext = 0, hit = 0, cont = 0, sh = 0, acc = 0, unocc = 0, maxSeg = 0; };
 
+/* Optional early end of a path whose throughput T has every channel below
+ * FLT_MIN (zero or denormal).  Such a path is Russian-roulette-terminated with
+ * certainty at its next diffuse bounce (p = max(T) < the smallest positive
+ * randomF32, 2^-32), so at most two more contributions remain, each below
+ * 1.2e-38 * (emission or light term): radiance-neutral in f32 except for a
+ * pixel whose energy is itself ~1e-38.  It ends the total-internal-reflection
+ * orbits in the glass lens that the reference traces forever (throughput stuck
+ * at the smallest denormal: 1.4e-45 * 0.69 rounds back up).  Off by default:
+ * the reference has no such exit (renderer.cpp:336-460) and the CPU baseline
+ * times the reference algorithm. */
+bool gZeroCutoff = false;
+
 /* Renderer::trace, iterative branch (renderer.cpp:332-463). */
 V3 trace(const Scene& S, uint32_t& seed, V3 o, V3 d, uint32_t maxSeg, Counters& C, Recorder* rec, uint32_t& stackMax) {
     V3 energy = splat(0.0f), T = splat(1.0f);
@@ -791,6 +803,7 @@ V3 trace(const Scene& S, uint32_t& seed, V3 o, V3 d, uint32_t maxSeg, Counters& 
             T = T * ((((cosT * invPdf) * brdf) * medium) * rr);
         }
         if (maxSeg != 0 && seg >= maxSeg) break;     /* C2 path-length cap */
+        if (gZeroCutoff && T.x < 1.17549435e-38f && T.y < 1.17549435e-38f && T.z < 1.17549435e-38f) break;
         C.cont++;
         o = I + kEps * R;                                                  /* :458-460 */
         d = R;
@@ -993,6 +1006,8 @@ void orc_bvh_depths(const orc_scene* h, uint32_t* td, uint32_t* bd) {
     for (auto* b : S.blases) { uint32_t d = bvhDepth(b->bvh, 0); if (d > m) m = d; }
     *bd = m;
 }
+
+void orc_set_zero_cutoff(int on) { gZeroCutoff = on != 0; }
 
 uint32_t orc_init_seed(uint32_t s) { return seedOf(s); }
 uint32_t orc_random_u32(uint32_t* s) { return rndU(*s); }

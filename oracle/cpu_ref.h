@@ -94,6 +94,10 @@ void orc_record_rays(orc_scene*, uint32_t width, uint32_t height, uint32_t frame
 /* Deepest root-to-leaf edge count of the TLAS and of every BLAS. */
 void orc_bvh_depths(const orc_scene*, uint32_t* tlas_depth, uint32_t* max_blas_depth);
 
+/* Ends paths whose throughput is exactly zero (radiance-neutral; see cpu_ref.cpp).
+ * Default off = reference semantics. */
+void orc_set_zero_cutoff(int on);
+
 /* RNG of surf_math.cpp:31-95, for known-answer tests. */
 uint32_t orc_init_seed(uint32_t seed);
 uint32_t orc_random_u32(uint32_t* seed);

@@ -74,18 +74,25 @@ struct DevCamera {
 struct Pool { float4* o; float4* d; float4* T; };
 struct ShadowQ { float4* o; float4* d; float4* c; };
 
-/* Device counters of one frame batch.  Double-buffered by phase parity so no
+/* Device counters of the sample stream.  Double-buffered by phase parity so no
  * kernel writes a word another block of the same launch still reads. */
 struct Counters {
-    uint32_t nIn[2];          /* paths in pool[p] when a phase reads it */
-    uint32_t nApp[2];         /* continuation append cursor into pool[p] */
-    uint32_t ns[2];           /* next sample to generate (per parity) */
-    uint32_t nSh[2];          /* shadow queue length of phase parity p */
-    uint32_t total;           /* samples in this batch */
-    uint32_t firstFrame;      /* frame index of batch sample 0 */
-    uint32_t maxSeg;          /* 0 = unbounded */
-    uint32_t _pad[5];
-    unsigned long long ev[8]; /* ext, hit, cont, shadow, acc, unocc, tail, spare */
+    uint32_t nIn[2];                 /* paths in pool[p] when a phase reads it */
+    uint32_t nApp[2];                /* continuation append cursor into pool[p] */
+    uint32_t nSh[2];                 /* shadow queue length of phase parity p */
+    uint32_t maxSeg;                 /* 0 = unbounded */
+    uint32_t zeroCutoff;             /* end paths whose throughput is exactly 0 (radiance-neutral) */
+    unsigned long long issued[2];    /* stream samples issued, per parity */
+    unsigned long long limit;        /* host-written issue limit (frame window) */
+    unsigned long long baseFrame;    /* absolute frame index of stream frame 0 */
+    unsigned long long ev[8];        /* ext, hit, cont, shadow, acc, unocc, tail paths, capped paths */
+    uint32_t capped[64];             /* sample ids of the first paths ended by the segment cap (diagnostics) */
+};
+
+/* Where a stream sample lives: radiance slot sid = (frame % window) * npx + pixel. */
+struct StreamGeom {
+    const uint32_t* rows;            /* shard rows */
+    uint32_t width, npx, window;
 };
 
 SURF_HD V3 ld3(const float* p) { return mk3(p[0], p[1], p[2]); }
@@ -248,171 +255,212 @@ __device__ __forceinline__ void addRadiance(float4* rad, uint32_t sid, V3 c) {
     rad[sid] = r;
 }
 
-/* One bounce of Renderer::trace's loop body (renderer.cpp:338-460). */
+/* Result of shading one hit: what the path does next. */
+struct ShadeOut {
+    bool cont, shadow, hitGeom, accd, capped;
+    float4 o, d, T;                  /* continuation path record */
+    float4 so, sd, sc;               /* shadow ray: (origin, tmax), (dir, sid), (T*Ld, 0) */
+};
+
+/* One bounce of Renderer::trace's loop body (renderer.cpp:338-460) for one path
+ * whose extension ray has been traced (h4 = t,u,v,prim; inst = ~0 on a miss). */
+__device__ __forceinline__ void shadePath(const DevScene& S, float4 o4, float4 d4, float4 T4, float4 h4, uint32_t inst,
+                                          float4* __restrict__ rad, uint32_t maxSeg, uint32_t zeroCutoff, ShadeOut& r) {
+    r.cont = r.shadow = r.hitGeom = r.accd = r.capped = false;
+    const uint32_t sid = f2u(o4.w);
+    uint32_t flags = f2u(d4.w);
+    uint32_t seed = f2u(T4.w);
+    const V3 o = xyz(o4), d = xyz(d4);
+    V3 T = xyz(T4);
+    bool lastSpecular = (flags & kFlagSpecular) != 0u;
+    const bool inMedium = (flags & kFlagMedium) != 0u;
+    const uint32_t seg = flags >> 2;
+    if (inst == kUnset) {
+        /* miss: energy += T * background (scene.cpp:35-51) */
+        V3 bg = mk3(0.0f, 0.0f, 0.0f);
+        if (S.bgType == 0u) bg = ld3(S.bgColor);
+        else if (S.bgType == 1u) {
+            const float a = 0.5f * (1.0f + d.y);
+            bg = add(lscl(a, ld3(S.bgB)), lscl(1.0f - a, ld3(S.bgA)));
+        }
+        addRadiance(rad, sid, mul(T, bg));
+        r.accd = true;
+        return;
+    }
+    r.hitGeom = true;
+    const DevInstance& I = S.inst[inst];
+    const DevMaterial& m = S.mats[I.material];
+    const bool isLight = m.emit > 0.0f && (m.ec[0] > 0.0f || m.ec[1] > 0.0f || m.ec[2] > 0.0f);
+    if (isLight) {
+        const V3 le = lscl(m.emit, ld3(m.ec));
+        addRadiance(rad, sid, lastSpecular ? mul(T, le) : mk3(0.0f, 0.0f, 0.0f));
+        r.accd = lastSpecular;
+        return;
+    }
+    const float t = h4.x, hu = h4.y, hv = h4.z;
+    const uint32_t prim = f2u(h4.w);
+    V3 medium = mk3(1.0f, 1.0f, 1.0f);
+    if (inMedium) {
+        const float nd = -t;
+        medium = mk3(gExpf(m.absorb[0] * nd), gExpf(m.absorb[1] * nd), gExpf(m.absorb[2] * nd));
+    }
+    const V3 P = add(o, lscl(t, d));
+    /* Instance::normal: M (u n0 + v n2 + w n1, 0), glm::normalize(vec4) */
+    const float4* nr = S.normals + 3u * (I.triOffset + prim);
+    const float4 n0 = nr[0], n1 = nr[1], n2 = nr[2];
+    const float w = (1.0f - hu) - hv;
+    const V3 no = add(add(lscl(hu, xyz(n0)), lscl(hv, xyz(n2))), lscl(w, xyz(n1)));
+    const float* M = I.M;
+    const float nx4 = mrow(M, 0, no.x, no.y, no.z, 0.0f), ny4 = mrow(M, 1, no.x, no.y, no.z, 0.0f);
+    const float nz4 = mrow(M, 2, no.x, no.y, no.z, 0.0f), nw4 = mrow(M, 3, no.x, no.y, no.z, 0.0f);
+    const float nn = (nx4 * nx4 + ny4 * ny4) + (nz4 * nz4 + nw4 * nw4);
+    const float ninv = 1.0f / sqrtf(nn);
+    V3 N = mk3(nx4 * ninv, ny4 * ninv, nz4 * ninv);
+    const float rng = rndF(seed);
+    V3 R = mk3(0.0f, 0.0f, 0.0f);
+    bool nextMedium = inMedium;
+    bool alive = true;
+    if (dot(d, N) > 0.0f) N = scl(N, -1.0f);
+    if (rng < m.refl) {
+        R = sub(d, lscl(2.0f * dot(N, d), N));
+        lastSpecular = true;
+        T = mul(T, mul(ld3(m.albedo), medium));
+    } else if (rng < (m.refl + m.refr)) {
+        bool mustRefract = false;
+        R = sub(d, lscl(2.0f * dot(N, d), N));
+        const float n1f = inMedium ? m.ior : 1.0f, n2f = inMedium ? 1.0f : m.ior;
+        const float ratio = n1f / n2f;
+        const float cosI = -dot(d, N);
+        const float cos2 = 1.0f - (ratio * ratio) * (1.0f - cosI * cosI);
+        if (cos2 > 0.0f) {
+            const float a = n1f - n2f, b = n1f + n2f;
+            const float r0 = (a * a) / (b * b);
+            const float c = 1.0f - cosI;
+            const float fres = r0 + (1.0f - r0) * ((((c * c) * c) * c) * c);
+            mustRefract = rndF(seed) > fres;
+            if (mustRefract) R = add(lscl(ratio, d), lscl(ratio * cosI - sqrtf(fabsf(cos2)), N));
+        }
+        lastSpecular = true;
+        T = mul(T, mul(ld3(m.albedo), medium));
+        nextMedium = mustRefract ? !inMedium : inMedium;
+    } else {
+        R = cosineSample(seed, N);
+        const float cosT = dot(N, R);
+        const float pdf = cosT * kInvPi;
+        const V3 brdf = scl(ld3(m.albedo), kInvPi);
+        if (S.nLights > 0u) {
+            /* Scene::sampleLights + Instance::samplePoint (scene.h:53, bvh.cpp:533-552) */
+            const uint2 L = S.lights[rndRangeU(seed, 0u, S.nLights)];
+            const DevInstance& LI = S.inst[L.x];
+            const float lu = rndRange(seed, 0.0f, 1.0f);
+            const float lv = rndRange(seed, 0.0f, 1.0f - lu);
+            const uint32_t ti = rndRangeU(seed, 0u, L.y);
+            const float4* tv = S.verts + 4u * (LI.triOffset + ti);
+            const float4* tn = S.normals + 3u * (LI.triOffset + ti);
+            const float lw = (1.0f - lu) - lv;
+            const V3 lp = add(add(lscl(lu, xyz(tv[0])), lscl(lv, xyz(tv[2]))), lscl(lw, xyz(tv[1])));
+            const V3 ln = add(add(lscl(lu, xyz(tn[0])), lscl(lv, xyz(tn[2]))), lscl(lw, xyz(tn[1])));
+            const float* LM = LI.M;
+            const float pw = mrow(LM, 3, lp.x, lp.y, lp.z, 1.0f);
+            const V3 Pl = divs(mk3(mrow(LM, 0, lp.x, lp.y, lp.z, 1.0f), mrow(LM, 1, lp.x, lp.y, lp.z, 1.0f),
+                                   mrow(LM, 2, lp.x, lp.y, lp.z, 1.0f)), pw);
+            const V3 LN = normalize(mk3(mrow(LM, 0, ln.x, ln.y, ln.z, 0.0f), mrow(LM, 1, ln.x, ln.y, ln.z, 0.0f),
+                                        mrow(LM, 2, ln.x, ln.y, ln.z, 0.0f)));
+            const V3 IL = sub(Pl, P);
+            const V3 Ld = normalize(IL);
+            const V3 SO = add(P, lscl(kEps, Ld));
+            const float srDepth = sqrtf(dot(IL, IL)) - 2.0f * kEps;
+            const float falloff = 1.0f / dot(IL, IL);
+            const float cosO = dot(N, Ld);
+            const float cosL = dot(LN, lscl(-1.0f, Ld));
+            if (cosO > 0.0f && cosL > 0.0f) {
+                const float SA = (cosL * LI.area) * falloff;
+                const float lightPdf = 1.0f / SA;
+                const float invPdf = 1.0f / lightPdf;
+                const DevMaterial& lm = S.mats[LI.material];
+                const V3 le = lscl(lm.emit, ld3(lm.ec));
+                const V3 Lc = scl(scl(mul(scl(le, invPdf), brdf), cosO), (float)S.nLights);
+                const V3 contrib = mul(T, Lc);
+                r.shadow = true;
+                r.so = make_float4(SO.x, SO.y, SO.z, srDepth);
+                r.sd = make_float4(Ld.x, Ld.y, Ld.z, u2f(sid));
+                r.sc = make_float4(contrib.x, contrib.y, contrib.z, 0.0f);
+            }
+        }
+        const float pm = tmax(T.x, tmax(T.y, T.z));
+        const float pr = pm < 0.0f ? 0.0f : (pm > 1.0f ? 1.0f : pm);   /* clamp(max(T), 0, 1) */
+        if (pr < rndF(seed)) alive = false;
+        else {
+            const float rr = 1.0f / pr;
+            const float invPdf = 1.0f / pdf;
+            lastSpecular = false;
+            T = mul(T, scl(mul(lscl(cosT * invPdf, brdf), medium), rr));
+        }
+    }
+    /* throughput cutoff: every channel of T below FLT_MIN.  Russian roulette ends
+     * such a path with certainty at its next diffuse bounce (p < 2^-32 <= rand),
+     * so at most two contributions of < 1.2e-38 * L remain; it also ends the
+     * TIR orbits in the glass lens that never terminate in the reference. */
+    if (zeroCutoff && T.x < 1.17549435e-38f && T.y < 1.17549435e-38f && T.z < 1.17549435e-38f) alive = false;
+    r.capped = alive && (maxSeg != 0u && seg >= maxSeg);
+    if (alive && !(maxSeg != 0u && seg >= maxSeg)) {
+        r.cont = true;
+        const V3 O = add(P, lscl(kEps, R));
+        flags = (nextMedium ? kFlagMedium : 0u) | (lastSpecular ? kFlagSpecular : 0u) | ((seg + 1u) << 2);
+        r.o = make_float4(O.x, O.y, O.z, u2f(sid));
+        r.d = make_float4(R.x, R.y, R.z, u2f(flags));
+        r.T = make_float4(T.x, T.y, T.z, u2f(seed));
+    }
+}
+
+/* Frame completion: one atomic per distinct frame slot in the wave (lanes of a
+ * wave almost always share one frame). */
+__device__ __forceinline__ void frameDoneAdd(uint32_t* frameDone, bool done, uint32_t slot) {
+    unsigned long long pending = __ballot(done);
+    while (pending) {
+        const int leader = __ffsll((long long)pending) - 1;
+        const uint32_t ls = (uint32_t)__shfl((int)slot, leader);
+        const unsigned long long same = __ballot(done && slot == ls) & pending;
+        if (laneId() == (uint32_t)leader) atomicAdd(&frameDone[ls], (uint32_t)__popcll(same));
+        pending &= ~same;
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void k_shade(DevScene S, Pool cur, Pool nxt, const float4* __restrict__ hitTUV,
                                                   const uint32_t* __restrict__ hitInst, ShadowQ Q,
-                                                  float4* __restrict__ rad, Counters* C, int par) {
+                                                  float4* __restrict__ rad, uint32_t* __restrict__ frameDone,
+                                                  uint32_t npx, Counters* C, int par) {
     const uint32_t n = C->nIn[par];
-    const uint32_t maxSeg = C->maxSeg;
+    const uint32_t maxSeg = C->maxSeg, zeroCutoff = C->zeroCutoff;
     const int nx = par ^ 1;
     unsigned long long cHit = 0, cCont = 0, cSh = 0, cAcc = 0;
     for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
         const uint32_t i = base + threadIdx.x;
-        bool cont = false, shadow = false, hitGeom = false, accd = false;
-        float4 oOut = make_float4(0, 0, 0, 0), dOut = oOut, tOut = oOut;
-        float4 sO = oOut, sD = oOut, sC = oOut;
-        if (i < n) {
-            const float4 o4 = cur.o[i], d4 = cur.d[i], T4 = cur.T[i];
-            const float4 h4 = hitTUV[i];
-            const uint32_t inst = hitInst[i];
-            const uint32_t sid = f2u(o4.w);
-            uint32_t flags = f2u(d4.w);
-            uint32_t seed = f2u(T4.w);
-            const V3 o = xyz(o4), d = xyz(d4);
-            V3 T = xyz(T4);
-            bool lastSpecular = (flags & kFlagSpecular) != 0u;
-            const bool inMedium = (flags & kFlagMedium) != 0u;
-            const uint32_t seg = flags >> 2;
-            if (inst == kUnset) {
-                /* miss: energy += T * background (scene.cpp:35-51) */
-                V3 bg = mk3(0.0f, 0.0f, 0.0f);
-                if (S.bgType == 0u) bg = ld3(S.bgColor);
-                else if (S.bgType == 1u) {
-                    const float a = 0.5f * (1.0f + d.y);
-                    bg = add(lscl(a, ld3(S.bgB)), lscl(1.0f - a, ld3(S.bgA)));
-                }
-                addRadiance(rad, sid, mul(T, bg));
-                accd = true;
-            } else {
-                hitGeom = true;
-                const DevInstance& I = S.inst[inst];
-                const DevMaterial& m = S.mats[I.material];
-                const bool isLight = m.emit > 0.0f && (m.ec[0] > 0.0f || m.ec[1] > 0.0f || m.ec[2] > 0.0f);
-                if (isLight) {
-                    const V3 le = lscl(m.emit, ld3(m.ec));
-                    addRadiance(rad, sid, lastSpecular ? mul(T, le) : mk3(0.0f, 0.0f, 0.0f));
-                    accd = lastSpecular;
-                } else {
-                    const float t = h4.x, hu = h4.y, hv = h4.z;
-                    const uint32_t prim = f2u(h4.w);
-                    V3 medium = mk3(1.0f, 1.0f, 1.0f);
-                    if (inMedium) {
-                        const float nd = -t;
-                        medium = mk3(gExpf(m.absorb[0] * nd), gExpf(m.absorb[1] * nd), gExpf(m.absorb[2] * nd));
-                    }
-                    const V3 P = add(o, lscl(t, d));
-                    /* Instance::normal: M (u n0 + v n2 + w n1, 0), glm::normalize(vec4) */
-                    const float4* nr = S.normals + 3u * (I.triOffset + prim);
-                    const float4 n0 = nr[0], n1 = nr[1], n2 = nr[2];
-                    const float w = (1.0f - hu) - hv;
-                    const V3 no = add(add(lscl(hu, xyz(n0)), lscl(hv, xyz(n2))), lscl(w, xyz(n1)));
-                    const float* M = I.M;
-                    const float nx4 = mrow(M, 0, no.x, no.y, no.z, 0.0f), ny4 = mrow(M, 1, no.x, no.y, no.z, 0.0f);
-                    const float nz4 = mrow(M, 2, no.x, no.y, no.z, 0.0f), nw4 = mrow(M, 3, no.x, no.y, no.z, 0.0f);
-                    const float nn = (nx4 * nx4 + ny4 * ny4) + (nz4 * nz4 + nw4 * nw4);
-                    const float ninv = 1.0f / sqrtf(nn);
-                    V3 N = mk3(nx4 * ninv, ny4 * ninv, nz4 * ninv);
-                    const float rng = rndF(seed);
-                    V3 R = mk3(0.0f, 0.0f, 0.0f);
-                    bool nextMedium = inMedium;
-                    bool alive = true;
-                    if (dot(d, N) > 0.0f) N = scl(N, -1.0f);
-                    if (rng < m.refl) {
-                        R = sub(d, lscl(2.0f * dot(N, d), N));
-                        lastSpecular = true;
-                        T = mul(T, mul(ld3(m.albedo), medium));
-                    } else if (rng < (m.refl + m.refr)) {
-                        bool mustRefract = false;
-                        R = sub(d, lscl(2.0f * dot(N, d), N));
-                        const float n1f = inMedium ? m.ior : 1.0f, n2f = inMedium ? 1.0f : m.ior;
-                        const float ratio = n1f / n2f;
-                        const float cosI = -dot(d, N);
-                        const float cos2 = 1.0f - (ratio * ratio) * (1.0f - cosI * cosI);
-                        if (cos2 > 0.0f) {
-                            const float a = n1f - n2f, b = n1f + n2f;
-                            const float r0 = (a * a) / (b * b);
-                            const float c = 1.0f - cosI;
-                            const float fres = r0 + (1.0f - r0) * ((((c * c) * c) * c) * c);
-                            mustRefract = rndF(seed) > fres;
-                            if (mustRefract) R = add(lscl(ratio, d), lscl(ratio * cosI - sqrtf(fabsf(cos2)), N));
-                        }
-                        lastSpecular = true;
-                        T = mul(T, mul(ld3(m.albedo), medium));
-                        nextMedium = mustRefract ? !inMedium : inMedium;
-                    } else {
-                        R = cosineSample(seed, N);
-                        const float cosT = dot(N, R);
-                        const float pdf = cosT * kInvPi;
-                        const V3 brdf = scl(ld3(m.albedo), kInvPi);
-                        if (S.nLights > 0u) {
-                            /* Scene::sampleLights + Instance::samplePoint (scene.h:53, bvh.cpp:533-552) */
-                            const uint2 L = S.lights[rndRangeU(seed, 0u, S.nLights)];
-                            const DevInstance& LI = S.inst[L.x];
-                            const float lu = rndRange(seed, 0.0f, 1.0f);
-                            const float lv = rndRange(seed, 0.0f, 1.0f - lu);
-                            const uint32_t ti = rndRangeU(seed, 0u, L.y);
-                            const float4* tv = S.verts + 4u * (LI.triOffset + ti);
-                            const float4* tn = S.normals + 3u * (LI.triOffset + ti);
-                            const float lw = (1.0f - lu) - lv;
-                            const V3 lp = add(add(lscl(lu, xyz(tv[0])), lscl(lv, xyz(tv[2]))), lscl(lw, xyz(tv[1])));
-                            const V3 ln = add(add(lscl(lu, xyz(tn[0])), lscl(lv, xyz(tn[2]))), lscl(lw, xyz(tn[1])));
-                            const float* LM = LI.M;
-                            const float pw = mrow(LM, 3, lp.x, lp.y, lp.z, 1.0f);
-                            const V3 Pl = divs(mk3(mrow(LM, 0, lp.x, lp.y, lp.z, 1.0f), mrow(LM, 1, lp.x, lp.y, lp.z, 1.0f),
-                                                   mrow(LM, 2, lp.x, lp.y, lp.z, 1.0f)), pw);
-                            const V3 LN = normalize(mk3(mrow(LM, 0, ln.x, ln.y, ln.z, 0.0f), mrow(LM, 1, ln.x, ln.y, ln.z, 0.0f),
-                                                        mrow(LM, 2, ln.x, ln.y, ln.z, 0.0f)));
-                            const V3 IL = sub(Pl, P);
-                            const V3 Ld = normalize(IL);
-                            const V3 SO = add(P, lscl(kEps, Ld));
-                            const float srDepth = sqrtf(dot(IL, IL)) - 2.0f * kEps;
-                            const float falloff = 1.0f / dot(IL, IL);
-                            const float cosO = dot(N, Ld);
-                            const float cosL = dot(LN, lscl(-1.0f, Ld));
-                            if (cosO > 0.0f && cosL > 0.0f) {
-                                const float SA = (cosL * LI.area) * falloff;
-                                const float lightPdf = 1.0f / SA;
-                                const float invPdf = 1.0f / lightPdf;
-                                const DevMaterial& lm = S.mats[LI.material];
-                                const V3 le = lscl(lm.emit, ld3(lm.ec));
-                                const V3 Lc = scl(scl(mul(scl(le, invPdf), brdf), cosO), (float)S.nLights);
-                                const V3 contrib = mul(T, Lc);
-                                shadow = true;
-                                sO = make_float4(SO.x, SO.y, SO.z, srDepth);
-                                sD = make_float4(Ld.x, Ld.y, Ld.z, u2f(sid));
-                                sC = make_float4(contrib.x, contrib.y, contrib.z, 0.0f);
-                            }
-                        }
-                        const float pm = tmax(T.x, tmax(T.y, T.z));
-                        const float pr = pm < 0.0f ? 0.0f : (pm > 1.0f ? 1.0f : pm);
-                        if (pr < rndF(seed)) alive = false;
-                        else {
-                            const float rr = 1.0f / pr;
-                            const float invPdf = 1.0f / pdf;
-                            lastSpecular = false;
-                            T = mul(T, scl(mul(lscl(cosT * invPdf, brdf), medium), rr));
-                        }
-                    }
-                    if (alive && !(maxSeg != 0u && seg >= maxSeg)) {
-                        cont = true;
-                        const V3 O = add(P, lscl(kEps, R));
-                        flags = (nextMedium ? kFlagMedium : 0u) | (lastSpecular ? kFlagSpecular : 0u) | ((seg + 1u) << 2);
-                        oOut = make_float4(O.x, O.y, O.z, u2f(sid));
-                        dOut = make_float4(R.x, R.y, R.z, u2f(flags));
-                        tOut = make_float4(T.x, T.y, T.z, u2f(seed));
-                    }
-                }
-            }
+        ShadeOut r;
+        r.cont = r.shadow = r.hitGeom = r.accd = r.capped = false;
+        uint32_t slot = 0;
+        const bool active = i < n;
+        if (active) {
+            const float4 o4 = cur.o[i];
+            slot = f2u(o4.w) / npx;
+            shadePath(S, o4, cur.d[i], cur.T[i], hitTUV[i], hitInst[i], rad, maxSeg, zeroCutoff, r);
         }
-        const unsigned long long mCont = __ballot(cont), mSh = __ballot(shadow);
+        const unsigned long long mCont = __ballot(r.cont), mSh = __ballot(r.shadow);
         const uint32_t jc = waveAppend(&C->nApp[nx], mCont);
         const uint32_t js = waveAppend(&C->nSh[par], mSh);
-        if (cont) { nxt.o[jc] = oOut; nxt.d[jc] = dOut; nxt.T[jc] = tOut; }
-        if (shadow) { Q.o[js] = sO; Q.d[js] = sD; Q.c[js] = sC; }
-        cHit += (unsigned long long)__popcll(__ballot(hitGeom));
+        if (r.cont) { nxt.o[jc] = r.o; nxt.d[jc] = r.d; nxt.T[jc] = r.T; }
+        if (r.shadow) { Q.o[js] = r.so; Q.d[js] = r.sd; Q.c[js] = r.sc; }
+        /* a path that ends here may still have this phase's shadow ray pending:
+         * connect runs before the host reads frameDone (end of the phase). */
+        frameDoneAdd(frameDone, active && !r.cont, slot);
+        if (r.capped) {
+            const unsigned long long k = atomicAdd(&C->ev[7], 1ull);
+            if (k < 64) C->capped[k] = f2u(cur.o[i].w);
+        }
+        cHit += (unsigned long long)__popcll(__ballot(r.hitGeom));
         cCont += (unsigned long long)__popcll(mCont);
         cSh += (unsigned long long)__popcll(mSh);
-        cAcc += (unsigned long long)__popcll(__ballot(accd));
+        cAcc += (unsigned long long)__popcll(__ballot(r.accd));
     }
     waveCount(&C->ev[1], cHit);
     waveCount(&C->ev[2], cCont);
@@ -447,24 +495,34 @@ __global__ __launch_bounds__(kBlock) void k_connect(DevScene S, ShadowQ Q, float
 }
 
 /* Camera::getPrimaryRay + sampleDefocusDisk (camera.h:59-87), jitter of
- * renderer.cpp:173-177; draw order of g++ (last argument first). */
+ * renderer.cpp:173-177; draw order of g++ (last argument first).  Fills
+ * pool[par^1] after the continuing paths, up to capacity and the issue limit. */
 __global__ __launch_bounds__(kBlock) void k_regen(DevCamera cam, Pool nxt, float4* __restrict__ rad, Counters* C, int par,
-                                                  uint32_t capacity, const uint32_t* __restrict__ rows,
-                                                  uint32_t width, uint32_t npx) {
+                                                  uint32_t capacity, StreamGeom G) {
     const int nx = par ^ 1;
     const uint32_t cont = C->nApp[nx];
-    const uint32_t ns = C->ns[par];
-    const uint32_t total = C->total;
-    const uint32_t frame0 = C->firstFrame;
-    const uint32_t room = capacity - cont, left = total - ns;
-    const uint32_t nnew = room < left ? room : left;
+    const unsigned long long iss = C->issued[par];
+    const unsigned long long lim = C->limit;
+    const unsigned long long base = C->baseFrame;
+    const uint32_t room = capacity - cont;
+    const unsigned long long left = lim > iss ? lim - iss : 0ull;
+    const uint32_t nnew = (unsigned long long)room < left ? room : (uint32_t)left;
     const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+    /* frame / pixel of the first new sample, then step without 64-bit divisions */
+    const unsigned long long f0 = iss / G.npx;
+    const uint32_t lp0 = (uint32_t)(iss - f0 * G.npx);
     for (uint32_t k = gid; k < nnew; k += gridDim.x * blockDim.x) {
-        const uint32_t s = ns + k;
-        const uint32_t f = s / npx, lp = s - f * npx;
-        const uint32_t row = rows[lp / width], x = lp - (lp / width) * width;
-        const uint32_t p = x + row * width;
-        uint32_t seed = initSeed(p + (frame0 + f) * 1799u);
+        uint32_t lp = lp0 + k;
+        const uint32_t df = lp / G.npx;
+        lp -= df * G.npx;
+        const unsigned long long f = f0 + df;
+        const uint32_t slot = (uint32_t)(f % G.window);
+        const uint32_t rowi = lp / G.width;
+        const uint32_t x = lp - rowi * G.width;
+        const uint32_t row = G.rows[rowi];
+        const uint32_t p = x + row * G.width;
+        const uint32_t sid = slot * G.npx + lp;
+        uint32_t seed = initSeed(p + (uint32_t)(base + f) * 1799u);
         const float jy = rndRange(seed, -0.5f, 0.5f);
         const float jx = rndRange(seed, -0.5f, 0.5f);
         const float u = ((float)x + jx) * cam.invW, v = ((float)row + jy) * cam.invH;
@@ -479,29 +537,78 @@ __global__ __launch_bounds__(kBlock) void k_regen(DevCamera cam, Pool nxt, float
         }
         const V3 plane = add(add(ld3(cam.firstPixel), lscl(u, ld3(cam.uVec))), lscl(v, ld3(cam.vVec)));
         const V3 dir = normalize(sub(plane, origin));
-        const uint32_t slot = cont + k;
-        nxt.o[slot] = make_float4(origin.x, origin.y, origin.z, u2f(s));
-        nxt.d[slot] = make_float4(dir.x, dir.y, dir.z, u2f(kFlagSpecular | (1u << 2)));
-        nxt.T[slot] = make_float4(1.0f, 1.0f, 1.0f, u2f(seed));
-        rad[s] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        const uint32_t slotIdx = cont + k;
+        nxt.o[slotIdx] = make_float4(origin.x, origin.y, origin.z, u2f(sid));
+        nxt.d[slotIdx] = make_float4(dir.x, dir.y, dir.z, u2f(kFlagSpecular | (1u << 2)));
+        nxt.T[slotIdx] = make_float4(1.0f, 1.0f, 1.0f, u2f(seed));
+        rad[sid] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     }
     if (gid == 0) {
         C->nIn[nx] = cont + nnew;
-        C->ns[nx] = ns + nnew;
+        C->issued[nx] = iss + nnew;
         C->nApp[par] = 0;
         C->nSh[nx] = 0;
         C->ev[0] += cont + nnew;     /* extension rays of the next phase */
     }
 }
 
-/* acc[p] += (radiance, 1) for each frame of the batch, in frame order. */
+/* Finishes the last paths of the stream: one kernel, each active lane runs its
+ * path to termination (extend -> shade -> connect per segment), so the long
+ * Russian-roulette tail pays no per-bounce launch.  Same device functions as
+ * the wavefront kernels: identical results.  lanes < lpw of each wave work. */
+__global__ __launch_bounds__(64) void k_tail(DevScene S, Pool cur, uint32_t n, uint32_t lpw, float4* __restrict__ rad,
+                                             uint32_t* __restrict__ frameDone, uint32_t npx, Counters* C) {
+    extern __shared__ uint32_t lds[];
+    const uint32_t lane = threadIdx.x;
+    const uint32_t i = blockIdx.x * lpw + lane;
+    if (lane >= lpw || i >= n) return;
+    uint32_t* stk = lds + threadIdx.x;
+    const uint32_t stride = blockDim.x;
+    const uint32_t maxSeg = C->maxSeg, zeroCutoff = C->zeroCutoff;
+    float4 o4 = cur.o[i], d4 = cur.d[i], T4 = cur.T[i];
+    const uint32_t slot = f2u(o4.w) / npx;
+    unsigned long long nExt = 0, nHit = 0, nCont = 0, nSh = 0, nAcc = 0, nUn = 0;
+    for (;;) {
+        float depth = kFarAway, u = 0.0f, v = 0.0f;
+        uint32_t inst = kUnset, prim = kUnset;
+        const bool hit = traceScene<false>(S, xyz(o4), xyz(d4), depth, u, v, inst, prim, stk, stride);
+        ++nExt;
+        ShadeOut r;
+        shadePath(S, o4, d4, T4, make_float4(depth, u, v, u2f(prim)), hit ? inst : kUnset, rad, maxSeg, zeroCutoff, r);
+        nHit += r.hitGeom; nAcc += r.accd;
+        if (r.shadow) {
+            ++nSh;
+            float sdep = r.so.w, su = 0.0f, sv = 0.0f;
+            uint32_t si = kUnset, sp = kUnset;
+            if (!traceScene<true>(S, xyz(r.so), xyz(r.sd), sdep, su, sv, si, sp, stk, stride)) {
+                addRadiance(rad, f2u(r.sd.w), xyz(r.sc));
+                ++nUn; ++nAcc;
+            }
+        }
+        if (r.capped) {
+            const unsigned long long k = atomicAdd(&C->ev[7], 1ull);
+            if (k < 64) C->capped[k] = f2u(o4.w);
+        }
+        if (!r.cont) break;
+        ++nCont;
+        o4 = r.o; d4 = r.d; T4 = r.T;
+    }
+    atomicAdd(&frameDone[slot], 1u);
+    atomicAdd(&C->ev[0], nExt - 1ull); atomicAdd(&C->ev[1], nHit); atomicAdd(&C->ev[2], nCont);
+    atomicAdd(&C->ev[3], nSh); atomicAdd(&C->ev[4], nAcc); atomicAdd(&C->ev[5], nUn);
+    atomicAdd(&C->ev[6], 1ull);
+}
+
+/* acc[p] += (radiance, 1) for frames [f0, f0+count) of the stream, in frame
+ * order (renderer.cpp:180); frame f's radiance lives in slot f % window. */
 __global__ __launch_bounds__(kBlock) void k_accumulate(const float4* __restrict__ rad, float4* __restrict__ acc,
-                                                       uint32_t npx, uint32_t frames) {
+                                                       uint32_t npx, unsigned long long f0, uint32_t count, uint32_t window) {
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= npx) return;
     float4 a = acc[p];
-    for (uint32_t f = 0; f < frames; ++f) {
-        const float4 r = rad[(size_t)f * npx + p];
+    for (uint32_t k = 0; k < count; ++k) {
+        const uint32_t slot = (uint32_t)((f0 + k) % window);
+        const float4 r = rad[(size_t)slot * npx + p];
         a.x = a.x + r.x; a.y = a.y + r.y; a.z = a.z + r.z; a.w = a.w + 1.0f;
     }
     acc[p] = a;

@@ -49,7 +49,7 @@ struct surf_ctx {
     std::vector<uint32_t> rows;
     uint32_t npx = 0;
     uint32_t capacity = 0;
-    uint32_t frameBatch = 16;
+    uint32_t window = 0;           /* frames whose samples may be in flight (radiance slots); 0 = default */
     bool profiling = false;
     std::string err;
 
@@ -62,6 +62,7 @@ struct surf_ctx {
     /* camera */
     bool hasCamera = false;
     DevCamera cam{};
+    surf_camera_ubo camUbo{};
 
     /* wavefront state */
     bool allocated = false;
@@ -70,14 +71,24 @@ struct surf_ctx {
     uint32_t* hitInst = nullptr;
     ShadowQ Q{};
     float4* rad = nullptr;
-    size_t radCap = 0;
     float4* acc = nullptr;
     uint32_t* dRows = nullptr;
     Counters* ctr = nullptr;
     Counters* hctr = nullptr;      /* pinned */
+    uint32_t* frameDone = nullptr; /* [window] */
+    uint32_t* hFrameDone = nullptr;/* pinned */
     uint32_t* dOutRGBA = nullptr;
     std::vector<void*> wfAllocs;
-    uint64_t totalSamples = 0;
+    uint64_t totalSamples = 0;     /* frames rendered since the last clear (samples per pixel) */
+
+    /* sample stream: frames [baseFrame, baseFrame + targetFrames) requested */
+    bool streamActive = false;
+    uint64_t baseFrame = 0;
+    uint64_t targetFrames = 0;     /* relative frames requested */
+    uint64_t accFrames = 0;        /* relative frames accumulated */
+    uint32_t streamMaxSeg = 0;
+    bool zeroCutoff = true;        /* radiance-neutral early end of T == 0 paths */
+    uint64_t pushedLimit = 0;
 
     /* graph */
     hipGraphExec_t graphExec = nullptr;
@@ -85,7 +96,9 @@ struct surf_ctx {
     uint32_t gridWork = 0, gridRegen = 0;
 
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t pev[kPhasesPerGraph * 4 + 1] = {};
     surf_stats stats{};
+    unsigned long long evBase[8] = {};   /* event counts of finished streams since the last clear */
 };
 
 #define SURF_CHECK(ctx, call)                                                             \
@@ -191,9 +204,14 @@ int upload(surf_ctx* c, const std::vector<T>& host, const T** devOut) {
 int allocWavefront(surf_ctx* c) {
     if (c->allocated) return SURF_OK;
     if (c->capacity == 0) {
-        /* default: enough paths to keep the chip busy through the RR tail */
-        const uint64_t want = (uint64_t)c->npx * std::max<uint32_t>(1u, std::min<uint32_t>(c->frameBatch, 4u));
+        /* default: ~4 frames of paths in flight keeps 256 CUs busy, bounded at 4M paths */
+        const uint64_t want = (uint64_t)c->npx * 4;
         c->capacity = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(want, 65536), 1u << 22);
+    }
+    if (c->window == 0) {
+        /* default: 256 frames, radiance ring capped at 16 GiB of the 288 GB HBM */
+        const uint64_t maxFrames = (16ull << 30) / ((uint64_t)c->npx * sizeof(float4));
+        c->window = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(256, maxFrames));
     }
     const size_t cap = c->capacity;
     int rc;
@@ -207,12 +225,14 @@ int allocWavefront(surf_ctx* c) {
     if ((rc = devAlloc(c, c->wfAllocs, &c->Q.o, cap))) return rc;
     if ((rc = devAlloc(c, c->wfAllocs, &c->Q.d, cap))) return rc;
     if ((rc = devAlloc(c, c->wfAllocs, &c->Q.c, cap))) return rc;
-    c->radCap = (size_t)c->npx * c->frameBatch;
-    if ((rc = devAlloc(c, c->wfAllocs, &c->rad, c->radCap))) return rc;
+    if ((rc = devAlloc(c, c->wfAllocs, &c->rad, (size_t)c->npx * c->window))) return rc;
     if ((rc = devAlloc(c, c->wfAllocs, &c->ctr, 1))) return rc;
+    if ((rc = devAlloc(c, c->wfAllocs, &c->frameDone, c->window))) return rc;
     if ((rc = devAlloc(c, c->wfAllocs, &c->dOutRGBA, c->npx))) return rc;
-    if (hipHostMalloc((void**)&c->hctr, sizeof(Counters), hipHostMallocDefault) != hipSuccess)
+    if (hipHostMalloc((void**)&c->hctr, sizeof(Counters), hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void**)&c->hFrameDone, c->window * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess)
         return fail(c, SURF_ERR_OOM, "hipHostMalloc of the counter block failed");
+    for (auto& e : c->pev) SURF_CHECK(c, hipEventCreate(&e));
     /* grid: 8 workgroups of 256 per CU saturate the 256-CU chip; grid-stride beyond */
     int cus = 256;
     hipDeviceProp_t prop;
@@ -224,24 +244,190 @@ int allocWavefront(surf_ctx* c) {
     return SURF_OK;
 }
 
-void launchPhase(surf_ctx* c, int par) {
+StreamGeom geom(const surf_ctx* c) { return StreamGeom{c->dRows, c->width, c->npx, c->window}; }
+
+/* One wavefront phase: extend -> shade -> connect -> regen.  With ev != null,
+ * an event is recorded before each kernel and after the last (profiling). */
+void launchPhase(surf_ctx* c, int par, hipEvent_t* ev) {
     const size_t lds = stackBytes(c);
+    if (ev) (void)hipEventRecord(ev[0], c->stream);
     hipLaunchKernelGGL(k_extend, dim3(c->gridWork), dim3(kBlock), lds, c->stream, c->S, c->pool[par], c->hitTUV, c->hitInst,
                        (const Counters*)c->ctr, par);
+    if (ev) (void)hipEventRecord(ev[1], c->stream);
     hipLaunchKernelGGL(k_shade, dim3(c->gridWork), dim3(kBlock), 0, c->stream, c->S, c->pool[par], c->pool[par ^ 1], c->hitTUV,
-                       (const uint32_t*)c->hitInst, c->Q, c->rad, c->ctr, par);
+                       (const uint32_t*)c->hitInst, c->Q, c->rad, c->frameDone, c->npx, c->ctr, par);
+    if (ev) (void)hipEventRecord(ev[2], c->stream);
     hipLaunchKernelGGL(k_connect, dim3(c->gridWork), dim3(kBlock), lds, c->stream, c->S, c->Q, c->rad, c->ctr, par);
+    if (ev) (void)hipEventRecord(ev[3], c->stream);
     hipLaunchKernelGGL(k_regen, dim3(c->gridRegen), dim3(kBlock), 0, c->stream, c->cam, c->pool[par ^ 1], c->rad, c->ctr, par,
-                       c->capacity, (const uint32_t*)c->dRows, c->width, c->npx);
+                       c->capacity, geom(c));
+    if (ev) (void)hipEventRecord(ev[4], c->stream);
 }
 
 int buildGraph(surf_ctx* c) {
     if (c->graphExec) return SURF_OK;
     SURF_CHECK(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-    for (int ph = 0; ph < kPhasesPerGraph; ++ph) launchPhase(c, ph & 1);
+    for (int ph = 0; ph < kPhasesPerGraph; ++ph) launchPhase(c, ph & 1, nullptr);
     hipError_t e = hipStreamEndCapture(c->stream, &c->graph);
     if (e != hipSuccess) return fail(c, SURF_ERR_HIP, std::string("graph capture: ") + hipGetErrorString(e));
     SURF_CHECK(c, hipGraphInstantiate(&c->graphExec, c->graph, nullptr, nullptr, 0));
+    return SURF_OK;
+}
+
+/* ---- sample stream ------------------------------------------------------ */
+int startStream(surf_ctx* c, uint64_t baseFrame, uint32_t maxSeg) {
+    Counters h{};
+    h.maxSeg = maxSeg;
+    h.zeroCutoff = c->zeroCutoff ? 1u : 0u;
+    h.baseFrame = baseFrame;
+    *c->hctr = h;
+    SURF_CHECK(c, hipMemcpyAsync(c->ctr, c->hctr, sizeof(Counters), hipMemcpyHostToDevice, c->stream));
+    SURF_CHECK(c, hipMemsetAsync(c->frameDone, 0, c->window * sizeof(uint32_t), c->stream));
+    c->streamActive = true;
+    c->baseFrame = baseFrame;
+    c->targetFrames = 0;
+    c->accFrames = 0;
+    c->streamMaxSeg = maxSeg;
+    c->pushedLimit = 0;
+    return SURF_OK;
+}
+
+uint64_t issueLimit(const surf_ctx* c) {
+    return std::min<uint64_t>(c->targetFrames, c->accFrames + c->window) * (uint64_t)c->npx;
+}
+
+int pushLimit(surf_ctx* c) {
+    const uint64_t lim = issueLimit(c);
+    if (lim == c->pushedLimit) return SURF_OK;
+    c->hctr->limit = lim;
+    SURF_CHECK(c, hipMemcpyAsync(&c->ctr->limit, &c->hctr->limit, sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
+    c->pushedLimit = lim;
+    return SURF_OK;
+}
+
+/* Reads counters + per-frame completion (one sync) and accumulates, in frame
+ * order, every leading frame whose samples have all finished. */
+int syncAndAccumulate(surf_ctx* c) {
+    SURF_CHECK(c, hipMemcpyAsync(c->hctr, c->ctr, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
+    SURF_CHECK(c, hipMemcpyAsync(c->hFrameDone, c->frameDone, c->window * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+    SURF_CHECK(c, hipStreamSynchronize(c->stream));
+    /* a frame is complete when all its samples were issued and all finished; a
+     * slot is reused only after its frame is accumulated, so frames beyond the
+     * issued range must not be tested (their slot may still count an older frame) */
+    uint64_t f = c->accFrames;
+    const uint64_t issuedFrames = c->hctr->issued[0] / c->npx;
+    while (f < c->targetFrames && f < issuedFrames && c->hFrameDone[f % c->window] == c->npx) ++f;
+    if (f == c->accFrames) return SURF_OK;
+    const uint32_t count = (uint32_t)(f - c->accFrames);
+    hipLaunchKernelGGL(k_accumulate, dim3((c->npx + kBlock - 1) / kBlock), dim3(kBlock), 0, c->stream, (const float4*)c->rad,
+                       c->acc, c->npx, (unsigned long long)c->accFrames, count, c->window);
+    SURF_CHECK(c, hipGetLastError());
+    for (uint64_t g = c->accFrames; g < f; ++g) c->hFrameDone[g % c->window] = 0;
+    SURF_CHECK(c, hipMemcpyAsync(c->frameDone, c->hFrameDone, c->window * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+    c->accFrames = f;
+    return pushLimit(c);
+}
+
+/* One unit of forward progress: kPhasesPerGraph phases (graph replay, or
+ * direct launches with per-kernel events when profiling). */
+int advance(surf_ctx* c) {
+    if (c->profiling) {
+        for (int ph = 0; ph < kPhasesPerGraph; ++ph) launchPhase(c, ph & 1, &c->pev[4 * ph]);
+        SURF_CHECK(c, hipGetLastError());
+        SURF_CHECK(c, hipEventSynchronize(c->pev[4 * (kPhasesPerGraph - 1) + 4]));
+        for (int ph = 0; ph < kPhasesPerGraph; ++ph) {
+            float t[4];
+            for (int k = 0; k < 4; ++k) (void)hipEventElapsedTime(&t[k], c->pev[4 * ph + k], c->pev[4 * ph + k + 1]);
+            c->stats.ms_extend += t[0]; c->stats.ms_shade += t[1]; c->stats.ms_connect += t[2]; c->stats.ms_regen += t[3];
+            c->stats.launches_extend++;
+        }
+    } else {
+        SURF_CHECK(c, hipGraphLaunch(c->graphExec, c->stream));
+    }
+    c->stats.iterations += kPhasesPerGraph;
+    if (c->stats.iterations > kMaxIterations)
+        return fail(c, SURF_ERR_LIMIT, "wavefront did not drain after " + std::to_string(c->stats.iterations) + " iterations");
+    return SURF_OK;
+}
+
+/* Finishes every path of pool 0 in one k_tail launch (counters at an even
+ * phase boundary: pool 0 is the next to be extended, nothing else pending). */
+int runTail(surf_ctx* c) {
+    const uint32_t n = c->hctr->nIn[0];
+    if (n == 0) return SURF_OK;
+    const uint32_t lpw = std::min<uint32_t>(64u, std::max<uint32_t>(1u, (n + 4095u) / 4096u));
+    const uint32_t blocks = (n + lpw - 1) / lpw;
+    if (c->profiling) SURF_CHECK(c, hipEventRecord(c->pev[0], c->stream));
+    hipLaunchKernelGGL(k_tail, dim3(blocks), dim3(64), (size_t)c->stackDepth * 64 * sizeof(uint32_t), c->stream, c->S, c->pool[0],
+                       n, lpw, c->rad, c->frameDone, c->npx, c->ctr);
+    SURF_CHECK(c, hipGetLastError());
+    if (c->profiling) {
+        SURF_CHECK(c, hipEventRecord(c->pev[1], c->stream));
+        SURF_CHECK(c, hipEventSynchronize(c->pev[1]));
+        float t; (void)hipEventElapsedTime(&t, c->pev[0], c->pev[1]);
+        c->stats.ms_tail += t;
+    }
+    /* pool 0 is now empty: the next phase starts from regen's refill */
+    const uint32_t zero = 0;
+    c->hctr->nIn[0] = 0;
+    SURF_CHECK(c, hipMemcpyAsync(&c->ctr->nIn[0], &zero, sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+    SURF_CHECK(c, hipStreamSynchronize(c->stream));
+    return SURF_OK;
+}
+
+uint32_t tailThreshold(const surf_ctx* c) { return std::max<uint32_t>(c->capacity / 16, 4096u); }
+
+/* Runs until every requested sample is issued (drain = false) or until every
+ * requested frame is accumulated (drain = true). */
+int pump(surf_ctx* c, bool drain) {
+    int rc;
+    if ((rc = pushLimit(c))) return rc;
+    const uint64_t target = c->targetFrames * (uint64_t)c->npx;
+    for (;;) {
+        const uint64_t issued = c->hctr->issued[0];
+        const uint32_t inflight = c->hctr->nIn[0];
+        if (!drain && issued >= target) return SURF_OK;
+        if (drain && c->accFrames >= c->targetFrames) return SURF_OK;
+        const bool starved = issued >= c->pushedLimit;     /* nothing more may be issued right now */
+        const uint64_t accBefore = c->accFrames;
+        if (starved && inflight > 0 && inflight <= tailThreshold(c)) {
+            if ((rc = runTail(c))) return rc;
+        } else if (starved && inflight == 0) {
+            /* every issued sample finished: accumulating re-opens the window */
+        } else if ((rc = advance(c))) {
+            return rc;
+        }
+        if ((rc = syncAndAccumulate(c))) return rc;
+        if (starved && inflight == 0 && c->accFrames == accBefore)
+            return fail(c, SURF_ERR_HIP, "sample stream stalled: pool empty but frames incomplete");
+    }
+}
+
+int ensureDrained(surf_ctx* c) {
+    if (!c->streamActive || c->accFrames >= c->targetFrames) return SURF_OK;
+    SURF_CHECK(c, hipSetDevice(c->device));
+    if (!c->profiling) {
+        int rc = buildGraph(c);
+        if (rc) return rc;
+    }
+    SURF_CHECK(c, hipEventRecord(c->ev0, c->stream));
+    int rc = pump(c, true);
+    if (rc) return rc;
+    SURF_CHECK(c, hipEventRecord(c->ev1, c->stream));
+    SURF_CHECK(c, hipEventSynchronize(c->ev1));
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, c->ev0, c->ev1);
+    c->stats.ms_total += ms;
+    return SURF_OK;
+}
+
+/* A stream ends when its pool is empty and all its frames are accumulated. */
+int endStream(surf_ctx* c) {
+    int rc = ensureDrained(c);
+    if (rc) return rc;
+    if (c->streamActive)
+        for (int k = 0; k < 8; ++k) c->evBase[k] += c->hctr->ev[k];
+    c->streamActive = false;
     return SURF_OK;
 }
 
@@ -324,6 +510,8 @@ void surf_destroy(surf_ctx* c) {
     freeList(c->sceneAllocs);
     freeList(c->wfAllocs);
     if (c->hctr) (void)hipHostFree(c->hctr);
+    if (c->hFrameDone) (void)hipHostFree(c->hFrameDone);
+    for (auto& e : c->pev) if (e) (void)hipEventDestroy(e);
     if (c->acc) (void)hipFree(c->acc);
     if (c->dRows) (void)hipFree(c->dRows);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -355,14 +543,36 @@ int surf_set_pool_capacity(surf_ctx* c, uint32_t paths) {
 }
 
 int surf_set_frame_batch(surf_ctx* c, uint32_t frames) {
-    if (!c || frames == 0 || (uint64_t)frames * c->npx > (1ull << 31)) return SURF_ERR_INVALID;
-    if (c->allocated) return fail(c, SURF_ERR_INVALID, "frame batch is fixed after the first render");
-    c->frameBatch = frames;
+    if (!c || frames == 0 || (uint64_t)frames * c->npx >= (1ull << 32)) return SURF_ERR_INVALID;
+    if (c->allocated) return fail(c, SURF_ERR_INVALID, "frame window is fixed after the first render");
+    c->window = frames;
+    return SURF_OK;
+}
+
+/* Diagnostics: sample ids (slot * npx + shard pixel) of the first paths the
+ * segment cap ended in the current stream, and how many were capped. */
+int surf_debug_capped(surf_ctx* c, uint32_t* sids, uint32_t max, uint64_t* count) {
+    if (!c || !count) return SURF_ERR_INVALID;
+    int rc = ensureDrained(c);
+    if (rc) return rc;
+    *count = c->hctr ? c->hctr->ev[7] : 0;
+    const uint32_t n = (uint32_t)std::min<uint64_t>(std::min<uint64_t>(*count, 64), max);
+    if (sids && c->hctr) std::memcpy(sids, c->hctr->capped, n * sizeof(uint32_t));
+    return SURF_OK;
+}
+
+int surf_set_zero_cutoff(surf_ctx* c, int enabled) {
+    if (!c) return SURF_ERR_INVALID;
+    int rc = endStream(c);
+    if (rc) return rc;
+    c->zeroCutoff = enabled != 0;
     return SURF_OK;
 }
 
 int surf_set_profiling(surf_ctx* c, int enabled) {
     if (!c) return SURF_ERR_INVALID;
+    int rc = endStream(c);
+    if (rc) return rc;
     c->profiling = enabled != 0;
     return SURF_OK;
 }
@@ -375,6 +585,8 @@ int surf_upload_scene(surf_ctx* c, const surf_scene_desc* d) {
         (d->light_count && !d->lights))
         return fail(c, SURF_ERR_INVALID, "incomplete scene descriptor");
     SURF_CHECK(c, hipSetDevice(c->device));
+    int rc0 = endStream(c);
+    if (rc0) return rc0;
     SURF_CHECK(c, hipStreamSynchronize(c->stream));
     destroyGraph(c);
     freeList(c->sceneAllocs);
@@ -486,6 +698,9 @@ int surf_update_instances(surf_ctx* c, const surf_gpu_instance* instances, uint3
 
 int surf_set_camera(surf_ctx* c, const surf_camera_ubo* u) {
     if (!c || !u) return SURF_ERR_INVALID;
+    if (c->hasCamera && std::memcmp(u, &c->camUbo, sizeof *u) == 0) return SURF_OK;   /* unchanged: keep the stream */
+    int rc0 = endStream(c);
+    if (rc0) return rc0;
     if (!(u->resolution[0] > 0.0f) || !(u->resolution[1] > 0.0f)) return fail(c, SURF_ERR_INVALID, "camera resolution must be positive");
     DevCamera k{};
     const float pos[3] = {u->position.x, u->position.y, u->position.z};
@@ -505,6 +720,7 @@ int surf_set_camera(surf_ctx* c, const surf_camera_ubo* u) {
     k.diskU[0] = du.x; k.diskU[1] = du.y; k.diskU[2] = du.z;
     k.diskV[0] = dv.x; k.diskV[1] = dv.y; k.diskV[2] = dv.z;
     c->cam = k;
+    c->camUbo = *u;
     c->hasCamera = true;
     destroyGraph(c);     /* camera is a kernel argument of the captured graph */
     return SURF_OK;
@@ -520,102 +736,41 @@ int surf_render(surf_ctx* c, uint32_t frames, uint32_t firstFrame, uint32_t maxS
     int rc = allocWavefront(c);
     if (rc) return rc;
     if (!c->profiling && (rc = buildGraph(c))) return rc;
-    std::memset(&c->stats, 0, sizeof c->stats);
-    c->stats.stack_depth = c->stackDepth;
-    c->stats.pool_capacity = c->capacity;
-    const size_t lds = stackBytes(c);
-    unsigned long long evTot[8] = {0};
-    uint64_t iterations = 0;
-    float msExt = 0, msShade = 0, msConn = 0, msRegen = 0, msAcc = 0;
-    hipEvent_t e[5];
-    if (c->profiling) for (auto& x : e) SURF_CHECK(c, hipEventCreate(&x));
+    /* continue the open stream only for the next consecutive frames of the same kind */
+    if (c->streamActive && (firstFrame != c->baseFrame + c->targetFrames || maxSeg != c->streamMaxSeg))
+        if ((rc = endStream(c))) return rc;
+    if (!c->streamActive && (rc = startStream(c, firstFrame, maxSeg))) return rc;
     SURF_CHECK(c, hipEventRecord(c->ev0, c->stream));
-    for (uint32_t b = 0; b < frames; b += c->frameBatch) {
-        const uint32_t F = std::min(c->frameBatch, frames - b);
-        Counters h{};
-        h.total = F * c->npx;
-        h.firstFrame = firstFrame + b;
-        h.maxSeg = maxSeg;
-        *c->hctr = h;
-        SURF_CHECK(c, hipMemcpyAsync(c->ctr, c->hctr, sizeof(Counters), hipMemcpyHostToDevice, c->stream));
-        /* kick: fill pool 0 as if phase parity 1 had just finished */
-        hipLaunchKernelGGL(k_regen, dim3(c->gridRegen), dim3(kBlock), 0, c->stream, c->cam, c->pool[0], c->rad, c->ctr, 1,
-                           c->capacity, (const uint32_t*)c->dRows, c->width, c->npx);
-        SURF_CHECK(c, hipGetLastError());
-        for (;;) {
-            if (c->profiling) {
-                for (int ph = 0; ph < 2; ++ph) {
-                    const int par = ph;
-                    SURF_CHECK(c, hipEventRecord(e[0], c->stream));
-                    hipLaunchKernelGGL(k_extend, dim3(c->gridWork), dim3(kBlock), lds, c->stream, c->S, c->pool[par], c->hitTUV,
-                                       c->hitInst, (const Counters*)c->ctr, par);
-                    SURF_CHECK(c, hipEventRecord(e[1], c->stream));
-                    hipLaunchKernelGGL(k_shade, dim3(c->gridWork), dim3(kBlock), 0, c->stream, c->S, c->pool[par], c->pool[par ^ 1],
-                                       c->hitTUV, (const uint32_t*)c->hitInst, c->Q, c->rad, c->ctr, par);
-                    SURF_CHECK(c, hipEventRecord(e[2], c->stream));
-                    hipLaunchKernelGGL(k_connect, dim3(c->gridWork), dim3(kBlock), lds, c->stream, c->S, c->Q, c->rad, c->ctr, par);
-                    SURF_CHECK(c, hipEventRecord(e[3], c->stream));
-                    hipLaunchKernelGGL(k_regen, dim3(c->gridRegen), dim3(kBlock), 0, c->stream, c->cam, c->pool[par ^ 1], c->rad, c->ctr,
-                                       par, c->capacity, (const uint32_t*)c->dRows, c->width, c->npx);
-                    SURF_CHECK(c, hipEventRecord(e[4], c->stream));
-                    SURF_CHECK(c, hipEventSynchronize(e[4]));
-                    float t;
-                    (void)hipEventElapsedTime(&t, e[0], e[1]); msExt += t;
-                    (void)hipEventElapsedTime(&t, e[1], e[2]); msShade += t;
-                    (void)hipEventElapsedTime(&t, e[2], e[3]); msConn += t;
-                    (void)hipEventElapsedTime(&t, e[3], e[4]); msRegen += t;
-                    c->stats.launches_extend++;
-                }
-                iterations += 2;
-            } else {
-                SURF_CHECK(c, hipGraphLaunch(c->graphExec, c->stream));
-                iterations += kPhasesPerGraph;
-            }
-            SURF_CHECK(c, hipMemcpyAsync(c->hctr, c->ctr, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
-            SURF_CHECK(c, hipStreamSynchronize(c->stream));
-            if (c->hctr->nIn[0] == 0) break;
-            if (iterations > kMaxIterations)
-                return fail(c, SURF_ERR_LIMIT, "wavefront did not drain after " + std::to_string(iterations) + " iterations");
-        }
-        for (int k = 0; k < 8; ++k) evTot[k] += c->hctr->ev[k];
-        if (c->profiling) SURF_CHECK(c, hipEventRecord(e[0], c->stream));
-        hipLaunchKernelGGL(k_accumulate, dim3((c->npx + kBlock - 1) / kBlock), dim3(kBlock), 0, c->stream,
-                           (const float4*)c->rad, c->acc, c->npx, F);
-        SURF_CHECK(c, hipGetLastError());
-        if (c->profiling) {
-            SURF_CHECK(c, hipEventRecord(e[1], c->stream));
-            SURF_CHECK(c, hipEventSynchronize(e[1]));
-            float t; (void)hipEventElapsedTime(&t, e[0], e[1]); msAcc += t;
-        }
-    }
+    c->targetFrames += frames;
+    if ((rc = pump(c, false))) return rc;
     SURF_CHECK(c, hipEventRecord(c->ev1, c->stream));
     SURF_CHECK(c, hipEventSynchronize(c->ev1));
     float ms = 0;
     (void)hipEventElapsedTime(&ms, c->ev0, c->ev1);
-    if (c->profiling) for (auto& x : e) (void)hipEventDestroy(x);
+    c->stats.ms_total += ms;
     c->totalSamples += frames;
-    surf_stats& s = c->stats;
-    s.samples = (uint64_t)frames * c->npx;
-    s.n_ext = evTot[0]; s.n_hit = evTot[1]; s.n_cont = evTot[2]; s.n_shadow = evTot[3]; s.n_acc = evTot[4]; s.n_unocc = evTot[5];
-    s.tail_paths = evTot[6];
-    s.iterations = iterations;
-    s.ms_total = ms;
-    s.ms_extend = msExt; s.ms_shade = msShade; s.ms_connect = msConn; s.ms_regen = msRegen; s.ms_accum = msAcc;
+    c->stats.samples += (uint64_t)frames * c->npx;
     return SURF_OK;
 }
 
 int surf_clear_accumulator(surf_ctx* c) {
     if (!c) return SURF_ERR_INVALID;
     SURF_CHECK(c, hipSetDevice(c->device));
+    int rc = endStream(c);
+    if (rc) return rc;
     SURF_CHECK(c, hipMemsetAsync(c->acc, 0, (size_t)c->npx * sizeof(float4), c->stream));
     SURF_CHECK(c, hipStreamSynchronize(c->stream));
     c->totalSamples = 0;
+    std::memset(&c->stats, 0, sizeof c->stats);
+    std::memset(c->evBase, 0, sizeof c->evBase);
     return SURF_OK;
 }
 
 int surf_read_accumulator(surf_ctx* c, float* out) {
     if (!c || !out) return SURF_ERR_INVALID;
     SURF_CHECK(c, hipSetDevice(c->device));
+    int rc = ensureDrained(c);
+    if (rc) return rc;
     SURF_CHECK(c, hipMemcpyAsync(out, c->acc, (size_t)c->npx * sizeof(float4), hipMemcpyDeviceToHost, c->stream));
     SURF_CHECK(c, hipStreamSynchronize(c->stream));
     return SURF_OK;
@@ -624,6 +779,8 @@ int surf_read_accumulator(surf_ctx* c, float* out) {
 int surf_copy_accumulator_device(surf_ctx* c, void* dst) {
     if (!c || !dst) return SURF_ERR_INVALID;
     SURF_CHECK(c, hipSetDevice(c->device));
+    int rc = ensureDrained(c);
+    if (rc) return rc;
     SURF_CHECK(c, hipMemcpyAsync(dst, c->acc, (size_t)c->npx * sizeof(float4), hipMemcpyDeviceToDevice, c->stream));
     SURF_CHECK(c, hipStreamSynchronize(c->stream));
     return SURF_OK;
@@ -635,6 +792,7 @@ int surf_finalize_rgba8(surf_ctx* c, uint32_t* out) {
     SURF_CHECK(c, hipSetDevice(c->device));
     int rc = allocWavefront(c);
     if (rc) return rc;
+    if ((rc = ensureDrained(c))) return rc;
     const float inv = 1.0f / (float)c->totalSamples;     /* renderer.cpp:160 */
     hipLaunchKernelGGL(k_finalize, dim3((c->npx + kBlock - 1) / kBlock), dim3(kBlock), 0, c->stream, (const float4*)c->acc,
                        c->dOutRGBA, c->npx, inv);
@@ -646,23 +804,33 @@ int surf_finalize_rgba8(surf_ctx* c, uint32_t* out) {
 
 int surf_get_stats(surf_ctx* c, surf_stats* out) {
     if (!c || !out) return SURF_ERR_INVALID;
-    *out = c->stats;
+    int rc = ensureDrained(c);
+    if (rc) return rc;
+    surf_stats s = c->stats;
+    unsigned long long ev[8];
+    for (int k = 0; k < 8; ++k) ev[k] = c->evBase[k] + ((c->streamActive && c->hctr) ? c->hctr->ev[k] : 0ull);
+    s.n_ext = ev[0]; s.n_hit = ev[1]; s.n_cont = ev[2]; s.n_shadow = ev[3]; s.n_acc = ev[4]; s.n_unocc = ev[5];
+    s.tail_paths = ev[6];
+    s.stack_depth = c->stackDepth;
+    s.pool_capacity = c->capacity;
     if (c->totalSamples) {
         /* Lumen energy, renderer.cpp:191-201 (serial sum of r+g+b of acc/N) */
         std::vector<float> acc((size_t)c->npx * 4);
-        int rc = surf_read_accumulator(c, acc.data());
-        if (rc) return rc;
+        if ((rc = surf_read_accumulator(c, acc.data()))) return rc;
         const float inv = 1.0f / (float)c->totalSamples;
         float e = 0.0f;
         for (size_t p = 0; p < c->npx; ++p) e = e + (((acc[4 * p] * inv) + (acc[4 * p + 1] * inv)) + (acc[4 * p + 2] * inv));
-        out->energy = e;
+        s.energy = e;
     }
+    *out = s;
     return SURF_OK;
 }
 
 int surf_synchronize(surf_ctx* c) {
     if (!c) return SURF_ERR_INVALID;
     SURF_CHECK(c, hipSetDevice(c->device));
+    int rc = ensureDrained(c);
+    if (rc) return rc;
     SURF_CHECK(c, hipStreamSynchronize(c->stream));
     return SURF_OK;
 }

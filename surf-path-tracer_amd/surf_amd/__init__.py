@@ -95,7 +95,8 @@ def load() -> C.CDLL:
         "surf_destroy": ([P], None), "surf_last_error": ([P], C.c_char_p),
         "surf_shard_rows": ([P, P, C.POINTER(U32)], I32),
         "surf_set_pool_capacity": ([P, U32], I32), "surf_set_frame_batch": ([P, U32], I32),
-        "surf_set_profiling": ([P, I32], I32),
+        "surf_set_profiling": ([P, I32], I32), "surf_set_zero_cutoff": ([P, I32], I32),
+        "surf_debug_capped": ([P, P, U32, C.POINTER(C.c_uint64)], I32),
         "surf_upload_scene": ([P, C.POINTER(SceneDesc)], I32),
         "surf_set_camera": ([P, P], I32),
         "surf_render": ([P, U32, U32, U32, U32], I32),
@@ -246,6 +247,16 @@ class Renderer:
     @property
     def handle(self):
         return self._h
+
+    def debug_capped(self):
+        """(count, sample ids) of paths ended by the segment cap in the current stream."""
+        ids = np.zeros(64, np.uint32)
+        n = C.c_uint64()
+        _check(load().surf_debug_capped(self._h, _ptr(ids), 64, C.byref(n)), "surf_debug_capped", self._h)
+        return int(n.value), ids[: min(int(n.value), 64)]
+
+    def set_zero_cutoff(self, on: bool):
+        _check(load().surf_set_zero_cutoff(self._h, 1 if on else 0), "surf_set_zero_cutoff", self._h)
 
     def set_profiling(self, on: bool):
         _check(load().surf_set_profiling(self._h, 1 if on else 0), "surf_set_profiling", self._h)

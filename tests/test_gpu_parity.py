@@ -60,11 +60,21 @@ def test_any_hit_bitexact(oracle_scene, product_scene):
 
 
 def _render_both(oracle_scene, product_scene, W, H, frames, first=0, max_seg=0, **kw):
+    """GPU render (zero-throughput cutoff on, the product default) against the
+    oracle in reference semantics (no cutoff) for radiance, and against the
+    oracle with the cutoff for event counts (the cutoff only removes segments)."""
     r = surf_amd.Renderer(product_scene, W, H, **kw)
     r.render(frames, first, max_seg)
     g = r.accumulator()
     stats = r.stats()
-    c, cnt, _ = oracle_scene.render(W, H, frames, first_frame=first, max_segments=max_seg)
+    oracle.set_zero_cutoff(False)
+    c, _, _ = oracle_scene.render(W, H, frames, first_frame=first, max_segments=max_seg)
+    oracle.set_zero_cutoff(True)
+    try:
+        c2, cnt, _ = oracle_scene.render(W, H, frames, first_frame=first, max_segments=max_seg)
+    finally:
+        oracle.set_zero_cutoff(False)
+    assert np.array_equal(c.view(np.uint32), c2.view(np.uint32)), "cutoff changed the oracle's radiance"
     return g, c, stats, cnt, r
 
 
@@ -159,6 +169,19 @@ def test_finalize_rgba8_matches_oracle(product_scene):
     for p in acc.reshape(-1, 4) * (np.float32(1.0) / np.float32(F)):
         e = np.float32(e + np.float32(np.float32(p[0] + p[1]) + p[2]))
     assert st["energy"] == pytest.approx(float(e), rel=1e-6)
+
+
+def test_cutoff_off_matches_reference_counts(oracle_scene, product_scene):
+    """With the cutoff disabled the GPU traces exactly the reference's segments."""
+    W, H, F = 64, 48, 2
+    r = surf_amd.Renderer(product_scene, W, H)
+    r.set_zero_cutoff(False)
+    r.render(F)
+    g = r.accumulator()
+    st = r.stats()
+    c, cnt, _ = oracle_scene.render(W, H, F)
+    _assert_bitexact(g, c, "cutoff off")
+    _assert_counts(st, cnt)
 
 
 def test_deterministic_rerun(product_scene):

@@ -126,6 +126,23 @@ def test_render_golden_fixture(oracle_scene):
     assert [cnt[k] for k in ("n_ext", "n_hit", "n_cont", "n_shadow", "n_acc", "n_unocc")] == list(g["counts"])
 
 
+def test_zero_throughput_cutoff_is_radiance_neutral(oracle_scene):
+    """Ending paths whose throughput is exactly (0,0,0) must not change a bit of
+    the accumulated radiance (the product enables it by default)."""
+    oracle.set_zero_cutoff(False)
+    a, ca, _ = oracle_scene.render(96, 64, 6)
+    b0, _, _ = oracle_scene.render(1280, 720, 1, rows=(300, 306))
+    oracle.set_zero_cutoff(True)
+    try:
+        b, cb, _ = oracle_scene.render(96, 64, 6)
+        b1, _, _ = oracle_scene.render(1280, 720, 1, rows=(300, 306))
+    finally:
+        oracle.set_zero_cutoff(False)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    assert np.array_equal(b0.view(np.uint32), b1.view(np.uint32))
+    assert cb["n_ext"] < ca["n_ext"]          # it does remove segments
+
+
 def test_segment_cap(oracle_scene):
     acc, cnt, _ = oracle_scene.render(32, 16, 2, max_segments=8)
     assert cnt["max_segments"] <= 8
