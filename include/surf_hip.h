@@ -126,7 +126,7 @@ typedef struct {
     uint32_t stack_depth;      /* traversal stack entries reserved per ray */
     uint32_t pool_capacity;    /* paths in flight */
     float    energy;           /* sum of acc.rgb / samples over the shard ("Lumen", renderer.cpp:191-201) */
-    uint32_t _pad;
+    uint32_t max_segments;     /* longest path seen (extension rays), diagnostics */
 } surf_stats;
 
 typedef struct surf_ctx surf_ctx;       /* one per HIP device */
@@ -166,6 +166,10 @@ int surf_set_frame_batch(surf_ctx* ctx, uint32_t frames);
  * total-internal-reflection orbits in the glass lens, which the reference
  * traces for up to millions of segments. */
 int surf_set_zero_cutoff(surf_ctx* ctx, int enabled);
+/* Drain policy: when no new sample may be issued and at most `threshold_paths`
+ * paths are in flight, one k_tail launch finishes them, `lanes_per_wave`
+ * paths per 64-lane wave (0 = automatic for either). */
+int surf_set_tail_policy(surf_ctx* ctx, uint32_t threshold_paths, uint32_t lanes_per_wave);
 /* Diagnostics: how many paths the segment cap ended in the current sample
  * stream, and the sample ids (frame slot * shard pixels + pixel) of the first
  * min(count, 64, max). */

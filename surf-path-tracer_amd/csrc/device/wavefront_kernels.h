@@ -42,7 +42,9 @@ struct DevInstance {          /* 160 B */
     float M[16];
     uint32_t triOffset, idxOffset, nodeOffset, material;
     float area;
-    uint32_t _pad[3];
+    uint32_t affineInv;       /* Minv row 3 == (0,0,0,1): w == 1 exactly for finite points */
+    uint32_t affine;          /* M row 3 == (0,0,0,1) */
+    uint32_t _pad;
 };
 
 struct DevMaterial {          /* = Material (64 B) */
@@ -61,6 +63,8 @@ struct DevScene {
     const DevMaterial* mats;
     const uint2* lights;      /* (instance, primitive count) */
     uint32_t nLights;
+    uint32_t nInst, nMats;
+    uint32_t tlasLeafCount;   /* TLAS root is a leaf with this many instances (0: general TLAS) */
     uint32_t bgType;
     float bgColor[3], bgA[3], bgB[3];
 };
@@ -82,6 +86,8 @@ struct Counters {
     uint32_t nSh[2];                 /* shadow queue length of phase parity p */
     uint32_t maxSeg;                 /* 0 = unbounded */
     uint32_t zeroCutoff;             /* end paths whose throughput is exactly 0 (radiance-neutral) */
+    uint32_t segMax;                 /* longest finished path (extension rays), diagnostics */
+    uint32_t _pad;
     unsigned long long issued[2];    /* stream samples issued, per parity */
     unsigned long long limit;        /* host-written issue limit (frame window) */
     unsigned long long baseFrame;    /* absolute frame index of stream frame 0 */
@@ -106,30 +112,58 @@ SURF_HD V3 xyz(float4 v) { return mk3(v.x, v.y, v.z); }
  * leaves in index order, LIFO pops.  Node record (64 B) of node n holds its
  * own leftFirst/count and, if interior, both children's boxes:
  *   q0 = (left.min.xyz,  leftFirst)   q1 = (left.max.xyz,  count)
- *   q2 = (right.min.xyz, 0)           q3 = (right.max.xyz, 0)          */
+ *   q2 = (right.min.xyz, 0)           q3 = (right.max.xyz, 0)
+ * The root record is read once per instance before the per-lane loop: when
+ * the instance index is wave-uniform (single-leaf TLAS) those are scalar
+ * loads, as are the triangles of a root leaf (the room's planes). */
 template <bool ANY>
-__device__ __forceinline__ bool blasTrace(const DevScene& S, const DevInstance& I, V3 o, V3 d, float& depth,
+__device__ __forceinline__ bool leafTest(const float4* tri, uint32_t lf, uint32_t cnt, V3 o, V3 d, float& depth,
+                                         float& hu, float& hv, uint32_t& hprim) {
+    bool any = false;
+    for (uint32_t k = 0; k < cnt; ++k) {
+        const float4 a = tri[3u * (lf + k)], b = tri[3u * (lf + k) + 1u], c = tri[3u * (lf + k) + 2u];
+        float u, v;
+        if (triHit(xyz(a), xyz(b), xyz(c), o, d, depth, u, v)) {
+            if (ANY) return true;
+            any = true;
+            hu = u; hv = v; hprim = f2u(a.w);
+        }
+    }
+    return any;
+}
+
+template <bool ANY>
+__device__ __forceinline__ bool blasTrace(const DevScene& S, uint32_t nodeOff, uint32_t idxOff, V3 o, V3 d, float& depth,
                                           float& hu, float& hv, uint32_t& hprim,
                                           uint32_t* stk, uint32_t stride, uint32_t base) {
     const V3 rd = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-    const uint32_t nodeOff = I.nodeOffset;
-    const float4* tri = S.tris + 3u * I.idxOffset;
+    const float4* tri = S.tris + 3u * idxOff;
+    /* root: never box-tested (bvh.cpp:131), only its children are */
+    const float4* rn = S.nodes + 4u * nodeOff;
+    const float4 r0 = rn[0], r1 = rn[1];
+    const uint32_t rlf = f2u(r0.w), rcnt = f2u(r1.w);
+    if (rcnt != 0u) return leafTest<ANY>(tri, rlf, rcnt, o, d, depth, hu, hv, hprim);
     uint32_t sp = base;
-    uint32_t node = nodeOff;
+    uint32_t node;
     bool any = false;
+    {
+        const float4 r2 = rn[2], r3 = rn[3];
+        float dn = slab(r0.x, r0.y, r0.z, r1.x, r1.y, r1.z, o, rd, depth);
+        float df = slab(r2.x, r2.y, r2.z, r3.x, r3.y, r3.z, o, rd, depth);
+        uint32_t cn = nodeOff + rlf, cf = cn + 1u;
+        if (dn > df) { const float t = dn; dn = df; df = t; const uint32_t c = cn; cn = cf; cf = c; }
+        if (dn == kFarAway) return false;
+        node = cn;
+        if (df != kFarAway) stk[(sp++) * stride] = cf;
+    }
     for (;;) {
         const float4* nd = S.nodes + 4u * node;
         const float4 q0 = nd[0], q1 = nd[1];
         const uint32_t lf = f2u(q0.w), cnt = f2u(q1.w);
         if (cnt != 0u) {
-            for (uint32_t k = 0; k < cnt; ++k) {
-                const float4 a = tri[3u * (lf + k)], b = tri[3u * (lf + k) + 1u], c = tri[3u * (lf + k) + 2u];
-                float u, v;
-                if (triHit(xyz(a), xyz(b), xyz(c), o, d, depth, u, v)) {
-                    if (ANY) return true;
-                    any = true;
-                    hu = u; hv = v; hprim = f2u(a.w);
-                }
+            if (leafTest<ANY>(tri, lf, cnt, o, d, depth, hu, hv, hprim)) {
+                if (ANY) return true;
+                any = true;
             }
             if (sp == base) break;
             node = stk[(--sp) * stride];
@@ -151,15 +185,40 @@ __device__ __forceinline__ bool blasTrace(const DevScene& S, const DevInstance& 
     return any;
 }
 
-/* BvhTLAS::intersect / intersectAny (bvh.cpp:654-778) with the instance
- * transform of Instance::intersect(Any) (bvh.cpp:481-513): origin
- * (M^-1 (o,1)).xyz / w, direction (M^-1 (d,0)).xyz, not renormalized. */
+/* Instance::intersect(Any) (bvh.cpp:481-513): origin (M^-1 (o,1)).xyz / w,
+ * direction (M^-1 (d,0)).xyz (not renormalized: t is shared with world space).
+ * For an affine M^-1 (row 3 = 0,0,0,1) w is exactly 1 for finite o and x/1 = x,
+ * so the division is skipped without changing a bit. */
+template <bool ANY>
+__device__ __forceinline__ bool instanceTrace(const DevScene& S, const DevInstance& I, V3 o, V3 d, float& depth, float& hu,
+                                              float& hv, uint32_t& hprim, uint32_t* stk, uint32_t stride, uint32_t base) {
+    const float* m = I.Minv;
+    V3 oo = mk3(mrow(m, 0, o.x, o.y, o.z, 1.0f), mrow(m, 1, o.x, o.y, o.z, 1.0f), mrow(m, 2, o.x, o.y, o.z, 1.0f));
+    if (!I.affineInv) oo = divs(oo, mrow(m, 3, o.x, o.y, o.z, 1.0f));
+    const V3 dd = mk3(mrow(m, 0, d.x, d.y, d.z, 0.0f), mrow(m, 1, d.x, d.y, d.z, 0.0f), mrow(m, 2, d.x, d.y, d.z, 0.0f));
+    return blasTrace<ANY>(S, I.nodeOffset, I.idxOffset, oo, dd, depth, hu, hv, hprim, stk, stride, base);
+}
+
+/* BvhTLAS::intersect / intersectAny (bvh.cpp:654-778). */
 template <bool ANY>
 __device__ __forceinline__ bool traceScene(const DevScene& S, V3 o, V3 d, float& depth, float& hu, float& hv,
                                            uint32_t& hinst, uint32_t& hprim, uint32_t* stk, uint32_t stride) {
+    bool any = false;
+    if (S.tlasLeafCount) {
+        /* single-leaf TLAS (the bundled scene): every lane visits the same
+         * instances in the same order -> wave-uniform loop, scalar loads */
+        for (uint32_t k = 0; k < S.tlasLeafCount; ++k) {
+            const uint32_t ii = S.tlasIdx[k];
+            if (instanceTrace<ANY>(S, S.inst[ii], o, d, depth, hu, hv, hprim, stk, stride, 0u)) {
+                if (ANY) return true;
+                any = true;
+                hinst = ii;
+            }
+        }
+        return any;
+    }
     const V3 rd = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     uint32_t sp = 0, node = 0;
-    bool any = false;
     for (;;) {
         const float4* nd = S.tlasNodes + 4u * node;
         const float4 q0 = nd[0], q1 = nd[1];
@@ -167,14 +226,7 @@ __device__ __forceinline__ bool traceScene(const DevScene& S, V3 o, V3 d, float&
         if (cnt != 0u) {
             for (uint32_t k = 0; k < cnt; ++k) {
                 const uint32_t ii = S.tlasIdx[lf + k];
-                const DevInstance& I = S.inst[ii];
-                const float* m = I.Minv;
-                const float w = mrow(m, 3, o.x, o.y, o.z, 1.0f);
-                const V3 oo = divs(mk3(mrow(m, 0, o.x, o.y, o.z, 1.0f), mrow(m, 1, o.x, o.y, o.z, 1.0f),
-                                       mrow(m, 2, o.x, o.y, o.z, 1.0f)), w);
-                const V3 dd = mk3(mrow(m, 0, d.x, d.y, d.z, 0.0f), mrow(m, 1, d.x, d.y, d.z, 0.0f),
-                                  mrow(m, 2, d.x, d.y, d.z, 0.0f));
-                if (blasTrace<ANY>(S, I, oo, dd, depth, hu, hv, hprim, stk, stride, sp)) {
+                if (instanceTrace<ANY>(S, S.inst[ii], o, d, depth, hu, hv, hprim, stk, stride, sp)) {
                     if (ANY) return true;
                     any = true;
                     hinst = ii;
@@ -258,14 +310,33 @@ __device__ __forceinline__ void addRadiance(float4* rad, uint32_t sid, V3 c) {
 /* Result of shading one hit: what the path does next. */
 struct ShadeOut {
     bool cont, shadow, hitGeom, accd, capped;
+    uint32_t seg;                    /* extension rays of the path so far */
     float4 o, d, T;                  /* continuation path record */
     float4 so, sd, sc;               /* shadow ray: (origin, tmax), (dir, sid), (T*Ld, 0) */
 };
 
 /* One bounce of Renderer::trace's loop body (renderer.cpp:338-460) for one path
  * whose extension ray has been traced (h4 = t,u,v,prim; inst = ~0 on a miss). */
-__device__ __forceinline__ void shadePath(const DevScene& S, float4 o4, float4 d4, float4 T4, float4 h4, uint32_t inst,
-                                          float4* __restrict__ rad, uint32_t maxSeg, uint32_t zeroCutoff, ShadeOut& r) {
+/* Scene tables shading reads by per-lane (divergent) index: LDS copies when
+ * they fit (k_shade / k_tail stage them per workgroup), else global. */
+struct ShadeTables {
+    const DevInstance* inst;
+    const DevMaterial* mats;
+    const uint2* lights;
+};
+
+constexpr uint32_t kLdsInst = 64, kLdsMats = 64, kLdsLights = 64;
+
+__device__ __forceinline__ void stageTables(const DevScene& S, DevInstance* sInst, DevMaterial* sMat, uint2* sLights) {
+    const uint32_t nI = S.nInst * (sizeof(DevInstance) / 16), nM = S.nMats * (sizeof(DevMaterial) / 16);
+    for (uint32_t k = threadIdx.x; k < nI; k += blockDim.x) reinterpret_cast<float4*>(sInst)[k] = reinterpret_cast<const float4*>(S.inst)[k];
+    for (uint32_t k = threadIdx.x; k < nM; k += blockDim.x) reinterpret_cast<float4*>(sMat)[k] = reinterpret_cast<const float4*>(S.mats)[k];
+    for (uint32_t k = threadIdx.x; k < S.nLights; k += blockDim.x) sLights[k] = S.lights[k];
+    __syncthreads();
+}
+
+__device__ __forceinline__ void shadePath(const DevScene& S, const ShadeTables& Tb, float4 o4, float4 d4, float4 T4, float4 h4,
+                                          uint32_t inst, float4* __restrict__ rad, uint32_t maxSeg, uint32_t zeroCutoff, ShadeOut& r) {
     r.cont = r.shadow = r.hitGeom = r.accd = r.capped = false;
     const uint32_t sid = f2u(o4.w);
     uint32_t flags = f2u(d4.w);
@@ -275,6 +346,7 @@ __device__ __forceinline__ void shadePath(const DevScene& S, float4 o4, float4 d
     bool lastSpecular = (flags & kFlagSpecular) != 0u;
     const bool inMedium = (flags & kFlagMedium) != 0u;
     const uint32_t seg = flags >> 2;
+    r.seg = seg;
     if (inst == kUnset) {
         /* miss: energy += T * background (scene.cpp:35-51) */
         V3 bg = mk3(0.0f, 0.0f, 0.0f);
@@ -288,8 +360,8 @@ __device__ __forceinline__ void shadePath(const DevScene& S, float4 o4, float4 d
         return;
     }
     r.hitGeom = true;
-    const DevInstance& I = S.inst[inst];
-    const DevMaterial& m = S.mats[I.material];
+    const DevInstance& I = Tb.inst[inst];
+    const DevMaterial& m = Tb.mats[I.material];
     const bool isLight = m.emit > 0.0f && (m.ec[0] > 0.0f || m.ec[1] > 0.0f || m.ec[2] > 0.0f);
     if (isLight) {
         const V3 le = lscl(m.emit, ld3(m.ec));
@@ -350,8 +422,8 @@ __device__ __forceinline__ void shadePath(const DevScene& S, float4 o4, float4 d
         const V3 brdf = scl(ld3(m.albedo), kInvPi);
         if (S.nLights > 0u) {
             /* Scene::sampleLights + Instance::samplePoint (scene.h:53, bvh.cpp:533-552) */
-            const uint2 L = S.lights[rndRangeU(seed, 0u, S.nLights)];
-            const DevInstance& LI = S.inst[L.x];
+            const uint2 L = Tb.lights[rndRangeU(seed, 0u, S.nLights)];
+            const DevInstance& LI = Tb.inst[L.x];
             const float lu = rndRange(seed, 0.0f, 1.0f);
             const float lv = rndRange(seed, 0.0f, 1.0f - lu);
             const uint32_t ti = rndRangeU(seed, 0u, L.y);
@@ -361,9 +433,8 @@ __device__ __forceinline__ void shadePath(const DevScene& S, float4 o4, float4 d
             const V3 lp = add(add(lscl(lu, xyz(tv[0])), lscl(lv, xyz(tv[2]))), lscl(lw, xyz(tv[1])));
             const V3 ln = add(add(lscl(lu, xyz(tn[0])), lscl(lv, xyz(tn[2]))), lscl(lw, xyz(tn[1])));
             const float* LM = LI.M;
-            const float pw = mrow(LM, 3, lp.x, lp.y, lp.z, 1.0f);
-            const V3 Pl = divs(mk3(mrow(LM, 0, lp.x, lp.y, lp.z, 1.0f), mrow(LM, 1, lp.x, lp.y, lp.z, 1.0f),
-                                   mrow(LM, 2, lp.x, lp.y, lp.z, 1.0f)), pw);
+            V3 Pl = mk3(mrow(LM, 0, lp.x, lp.y, lp.z, 1.0f), mrow(LM, 1, lp.x, lp.y, lp.z, 1.0f), mrow(LM, 2, lp.x, lp.y, lp.z, 1.0f));
+            if (!LI.affine) Pl = divs(Pl, mrow(LM, 3, lp.x, lp.y, lp.z, 1.0f));   /* w == 1 exactly when affine */
             const V3 LN = normalize(mk3(mrow(LM, 0, ln.x, ln.y, ln.z, 0.0f), mrow(LM, 1, ln.x, ln.y, ln.z, 0.0f),
                                         mrow(LM, 2, ln.x, ln.y, ln.z, 0.0f)));
             const V3 IL = sub(Pl, P);
@@ -377,7 +448,7 @@ __device__ __forceinline__ void shadePath(const DevScene& S, float4 o4, float4 d
                 const float SA = (cosL * LI.area) * falloff;
                 const float lightPdf = 1.0f / SA;
                 const float invPdf = 1.0f / lightPdf;
-                const DevMaterial& lm = S.mats[LI.material];
+                const DevMaterial& lm = Tb.mats[LI.material];
                 const V3 le = lscl(lm.emit, ld3(lm.ec));
                 const V3 Lc = scl(scl(mul(scl(le, invPdf), brdf), cosO), (float)S.nLights);
                 const V3 contrib = mul(T, Lc);
@@ -426,10 +497,19 @@ __device__ __forceinline__ void frameDoneAdd(uint32_t* frameDone, bool done, uin
     }
 }
 
+template <bool LDS_TABLES>
 __global__ __launch_bounds__(kBlock) void k_shade(DevScene S, Pool cur, Pool nxt, const float4* __restrict__ hitTUV,
                                                   const uint32_t* __restrict__ hitInst, ShadowQ Q,
                                                   float4* __restrict__ rad, uint32_t* __restrict__ frameDone,
                                                   uint32_t npx, Counters* C, int par) {
+    __shared__ DevInstance sInst[LDS_TABLES ? kLdsInst : 1];
+    __shared__ DevMaterial sMat[LDS_TABLES ? kLdsMats : 1];
+    __shared__ uint2 sLights[LDS_TABLES ? kLdsLights : 1];
+    ShadeTables Tb{S.inst, S.mats, S.lights};
+    if (LDS_TABLES) {
+        stageTables(S, sInst, sMat, sLights);
+        Tb = ShadeTables{sInst, sMat, sLights};
+    }
     const uint32_t n = C->nIn[par];
     const uint32_t maxSeg = C->maxSeg, zeroCutoff = C->zeroCutoff;
     const int nx = par ^ 1;
@@ -438,12 +518,13 @@ __global__ __launch_bounds__(kBlock) void k_shade(DevScene S, Pool cur, Pool nxt
         const uint32_t i = base + threadIdx.x;
         ShadeOut r;
         r.cont = r.shadow = r.hitGeom = r.accd = r.capped = false;
+        r.seg = 0;
         uint32_t slot = 0;
         const bool active = i < n;
         if (active) {
             const float4 o4 = cur.o[i];
             slot = f2u(o4.w) / npx;
-            shadePath(S, o4, cur.d[i], cur.T[i], hitTUV[i], hitInst[i], rad, maxSeg, zeroCutoff, r);
+            shadePath(S, Tb, o4, cur.d[i], cur.T[i], hitTUV[i], hitInst[i], rad, maxSeg, zeroCutoff, r);
         }
         const unsigned long long mCont = __ballot(r.cont), mSh = __ballot(r.shadow);
         const uint32_t jc = waveAppend(&C->nApp[nx], mCont);
@@ -453,6 +534,7 @@ __global__ __launch_bounds__(kBlock) void k_shade(DevScene S, Pool cur, Pool nxt
         /* a path that ends here may still have this phase's shadow ray pending:
          * connect runs before the host reads frameDone (end of the phase). */
         frameDoneAdd(frameDone, active && !r.cont, slot);
+        if (active && !r.cont && r.seg > 32u) atomicMax(&C->segMax, r.seg);   /* rare: RR ends most paths early */
         if (r.capped) {
             const unsigned long long k = atomicAdd(&C->ev[7], 1ull);
             if (k < 64) C->capped[k] = f2u(cur.o[i].w);
@@ -556,9 +638,18 @@ __global__ __launch_bounds__(kBlock) void k_regen(DevCamera cam, Pool nxt, float
  * path to termination (extend -> shade -> connect per segment), so the long
  * Russian-roulette tail pays no per-bounce launch.  Same device functions as
  * the wavefront kernels: identical results.  lanes < lpw of each wave work. */
+template <bool LDS_TABLES>
 __global__ __launch_bounds__(64) void k_tail(DevScene S, Pool cur, uint32_t n, uint32_t lpw, float4* __restrict__ rad,
                                              uint32_t* __restrict__ frameDone, uint32_t npx, Counters* C) {
     extern __shared__ uint32_t lds[];
+    __shared__ DevInstance sInst[LDS_TABLES ? kLdsInst : 1];
+    __shared__ DevMaterial sMat[LDS_TABLES ? kLdsMats : 1];
+    __shared__ uint2 sLights[LDS_TABLES ? kLdsLights : 1];
+    ShadeTables Tb{S.inst, S.mats, S.lights};
+    if (LDS_TABLES) {
+        stageTables(S, sInst, sMat, sLights);
+        Tb = ShadeTables{sInst, sMat, sLights};
+    }
     const uint32_t lane = threadIdx.x;
     const uint32_t i = blockIdx.x * lpw + lane;
     if (lane >= lpw || i >= n) return;
@@ -574,7 +665,7 @@ __global__ __launch_bounds__(64) void k_tail(DevScene S, Pool cur, uint32_t n, u
         const bool hit = traceScene<false>(S, xyz(o4), xyz(d4), depth, u, v, inst, prim, stk, stride);
         ++nExt;
         ShadeOut r;
-        shadePath(S, o4, d4, T4, make_float4(depth, u, v, u2f(prim)), hit ? inst : kUnset, rad, maxSeg, zeroCutoff, r);
+        shadePath(S, Tb, o4, d4, T4, make_float4(depth, u, v, u2f(prim)), hit ? inst : kUnset, rad, maxSeg, zeroCutoff, r);
         nHit += r.hitGeom; nAcc += r.accd;
         if (r.shadow) {
             ++nSh;
@@ -589,7 +680,7 @@ __global__ __launch_bounds__(64) void k_tail(DevScene S, Pool cur, uint32_t n, u
             const unsigned long long k = atomicAdd(&C->ev[7], 1ull);
             if (k < 64) C->capped[k] = f2u(o4.w);
         }
-        if (!r.cont) break;
+        if (!r.cont) { atomicMax(&C->segMax, r.seg); break; }
         ++nCont;
         o4 = r.o; d4 = r.d; T4 = r.T;
     }

@@ -55,6 +55,7 @@ struct surf_ctx {
 
     /* scene */
     bool hasScene = false;
+    bool ldsTables = false;        /* instance/material/light tables fit the per-workgroup LDS copy */
     DevScene S{};
     std::vector<void*> sceneAllocs;
     uint32_t stackDepth = 0;
@@ -89,6 +90,9 @@ struct surf_ctx {
     uint32_t streamMaxSeg = 0;
     bool zeroCutoff = true;        /* radiance-neutral early end of T == 0 paths */
     uint64_t pushedLimit = 0;
+    uint32_t tailPaths = 0;        /* drain policy (surf_set_tail_policy), 0 = automatic */
+    uint32_t tailLanes = 0;
+    uint32_t segMaxBase = 0;       /* longest path of finished streams */
 
     /* graph */
     hipGraphExec_t graphExec = nullptr;
@@ -254,8 +258,12 @@ void launchPhase(surf_ctx* c, int par, hipEvent_t* ev) {
     hipLaunchKernelGGL(k_extend, dim3(c->gridWork), dim3(kBlock), lds, c->stream, c->S, c->pool[par], c->hitTUV, c->hitInst,
                        (const Counters*)c->ctr, par);
     if (ev) (void)hipEventRecord(ev[1], c->stream);
-    hipLaunchKernelGGL(k_shade, dim3(c->gridWork), dim3(kBlock), 0, c->stream, c->S, c->pool[par], c->pool[par ^ 1], c->hitTUV,
-                       (const uint32_t*)c->hitInst, c->Q, c->rad, c->frameDone, c->npx, c->ctr, par);
+    if (c->ldsTables)
+        hipLaunchKernelGGL(k_shade<true>, dim3(c->gridWork), dim3(kBlock), 0, c->stream, c->S, c->pool[par], c->pool[par ^ 1],
+                           c->hitTUV, (const uint32_t*)c->hitInst, c->Q, c->rad, c->frameDone, c->npx, c->ctr, par);
+    else
+        hipLaunchKernelGGL(k_shade<false>, dim3(c->gridWork), dim3(kBlock), 0, c->stream, c->S, c->pool[par], c->pool[par ^ 1],
+                           c->hitTUV, (const uint32_t*)c->hitInst, c->Q, c->rad, c->frameDone, c->npx, c->ctr, par);
     if (ev) (void)hipEventRecord(ev[2], c->stream);
     hipLaunchKernelGGL(k_connect, dim3(c->gridWork), dim3(kBlock), lds, c->stream, c->S, c->Q, c->rad, c->ctr, par);
     if (ev) (void)hipEventRecord(ev[3], c->stream);
@@ -355,11 +363,17 @@ int advance(surf_ctx* c) {
 int runTail(surf_ctx* c) {
     const uint32_t n = c->hctr->nIn[0];
     if (n == 0) return SURF_OK;
-    const uint32_t lpw = std::min<uint32_t>(64u, std::max<uint32_t>(1u, (n + 4095u) / 4096u));
+    const uint32_t lpw = c->tailLanes ? std::min<uint32_t>(64u, c->tailLanes)
+                                      : std::min<uint32_t>(64u, std::max<uint32_t>(1u, (n + 4095u) / 4096u));
     const uint32_t blocks = (n + lpw - 1) / lpw;
     if (c->profiling) SURF_CHECK(c, hipEventRecord(c->pev[0], c->stream));
-    hipLaunchKernelGGL(k_tail, dim3(blocks), dim3(64), (size_t)c->stackDepth * 64 * sizeof(uint32_t), c->stream, c->S, c->pool[0],
-                       n, lpw, c->rad, c->frameDone, c->npx, c->ctr);
+    const size_t lds = (size_t)c->stackDepth * 64 * sizeof(uint32_t);
+    if (c->ldsTables)
+        hipLaunchKernelGGL(k_tail<true>, dim3(blocks), dim3(64), lds, c->stream, c->S, c->pool[0], n, lpw, c->rad, c->frameDone,
+                           c->npx, c->ctr);
+    else
+        hipLaunchKernelGGL(k_tail<false>, dim3(blocks), dim3(64), lds, c->stream, c->S, c->pool[0], n, lpw, c->rad, c->frameDone,
+                           c->npx, c->ctr);
     SURF_CHECK(c, hipGetLastError());
     if (c->profiling) {
         SURF_CHECK(c, hipEventRecord(c->pev[1], c->stream));
@@ -375,7 +389,7 @@ int runTail(surf_ctx* c) {
     return SURF_OK;
 }
 
-uint32_t tailThreshold(const surf_ctx* c) { return std::max<uint32_t>(c->capacity / 16, 4096u); }
+uint32_t tailThreshold(const surf_ctx* c) { return c->tailPaths ? c->tailPaths : std::max<uint32_t>(c->capacity / 16, 4096u); }
 
 /* Runs until every requested sample is issued (drain = false) or until every
  * requested frame is accumulated (drain = true). */
@@ -425,8 +439,10 @@ int ensureDrained(surf_ctx* c) {
 int endStream(surf_ctx* c) {
     int rc = ensureDrained(c);
     if (rc) return rc;
-    if (c->streamActive)
+    if (c->streamActive) {
         for (int k = 0; k < 8; ++k) c->evBase[k] += c->hctr->ev[k];
+        c->segMaxBase = std::max(c->segMaxBase, c->hctr->segMax);
+    }
     c->streamActive = false;
     return SURF_OK;
 }
@@ -561,6 +577,14 @@ int surf_debug_capped(surf_ctx* c, uint32_t* sids, uint32_t max, uint64_t* count
     return SURF_OK;
 }
 
+int surf_set_tail_policy(surf_ctx* c, uint32_t threshold_paths, uint32_t lanes_per_wave) {
+    if (!c) return fail(nullptr, SURF_ERR_INVALID, "ctx is NULL");
+    if (lanes_per_wave > 64) return fail(c, SURF_ERR_INVALID, "lanes_per_wave must be <= 64");
+    c->tailPaths = threshold_paths;
+    c->tailLanes = lanes_per_wave;
+    return SURF_OK;
+}
+
 int surf_set_zero_cutoff(surf_ctx* c, int enabled) {
     if (!c) return SURF_ERR_INVALID;
     int rc = endStream(c);
@@ -608,6 +632,10 @@ int surf_upload_scene(surf_ctx* c, const surf_scene_desc* d) {
         std::memcpy(D.M, g.transform, sizeof D.M);
         D.triOffset = g.tri_offset; D.idxOffset = g.bvh_idx_offset; D.nodeOffset = g.bvh_node_offset; D.material = g.material_offset;
         D.area = g.area;
+        /* row 3 of a column-major matrix: elements 3, 7, 11, 15 */
+        auto affine = [](const float* m) { return m[3] == 0.0f && m[7] == 0.0f && m[11] == 0.0f && m[15] == 1.0f; };
+        D.affineInv = affine(g.inv_transform) ? 1u : 0u;
+        D.affine = affine(g.transform) ? 1u : 0u;
         if (!walked[g.bvh_node_offset]) {
             std::vector<uint8_t> leaf(d->blas_index_count, 0);
             TreeWalk w = walkTree(d->blas_nodes, d->blas_node_count, g.bvh_node_offset, d->blas_index_count, g.bvh_idx_offset, nodes, leaf);
@@ -677,12 +705,17 @@ int surf_upload_scene(surf_ctx* c, const surf_scene_desc* d) {
     if ((rc = upload(c, mats, &S.mats))) return rc;
     if ((rc = upload(c, lights, &S.lights))) return rc;
     S.nLights = d->light_count;
+    S.nInst = d->instance_count;
+    S.nMats = d->material_count;
+    S.tlasLeafCount = d->tlas_nodes[0].count;   /* root leaf: wave-uniform instance loop */
+    if (S.tlasLeafCount && d->tlas_nodes[0].left_first != 0) S.tlasLeafCount = 0;   /* general path unless indices start at 0 */
     const surf_background& bg = *d->background;
     S.bgType = bg.type;
     S.bgColor[0] = bg.color.x; S.bgColor[1] = bg.color.y; S.bgColor[2] = bg.color.z;
     S.bgA[0] = bg.gradient_a.x; S.bgA[1] = bg.gradient_a.y; S.bgA[2] = bg.gradient_a.z;
     S.bgB[0] = bg.gradient_b.x; S.bgB[1] = bg.gradient_b.y; S.bgB[2] = bg.gradient_b.z;
     c->S = S;
+    c->ldsTables = d->instance_count <= kLdsInst && d->material_count <= kLdsMats && d->light_count <= kLdsLights;
     c->stackDepth = depth;
     c->nInstances = d->instance_count;
     c->nTriangles = d->triangle_count;
@@ -763,6 +796,7 @@ int surf_clear_accumulator(surf_ctx* c) {
     c->totalSamples = 0;
     std::memset(&c->stats, 0, sizeof c->stats);
     std::memset(c->evBase, 0, sizeof c->evBase);
+    c->segMaxBase = 0;
     return SURF_OK;
 }
 
@@ -811,6 +845,7 @@ int surf_get_stats(surf_ctx* c, surf_stats* out) {
     for (int k = 0; k < 8; ++k) ev[k] = c->evBase[k] + ((c->streamActive && c->hctr) ? c->hctr->ev[k] : 0ull);
     s.n_ext = ev[0]; s.n_hit = ev[1]; s.n_cont = ev[2]; s.n_shadow = ev[3]; s.n_acc = ev[4]; s.n_unocc = ev[5];
     s.tail_paths = ev[6];
+    s.max_segments = std::max(c->segMaxBase, (c->streamActive && c->hctr) ? c->hctr->segMax : 0u);
     s.stack_depth = c->stackDepth;
     s.pool_capacity = c->capacity;
     if (c->totalSamples) {

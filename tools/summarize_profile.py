@@ -1,0 +1,57 @@
+"""Summarizes a tools/profile_round.sh output directory into a small JSON
+(kernel durations + HBM traffic per k_extend launch) for profiles/.
+
+FETCH_SIZE / WRITE_SIZE are in KiB.  gfx950 correction (MI355X_MICROARCH.md
+§HBM): FETCH_SIZE counts half the bytes of a wide (16 B/lane) coalesced read,
+so the read side is doubled; WRITE_SIZE is exact for 16-B stores.  The
+traversal's node/triangle fetches are 16-B vector loads too.
+usage: python tools/summarize_profile.py DIR OUT.json
+"""
+import csv
+import json
+import statistics
+import sys
+
+
+def short(name):
+    return name.split("(")[0].split("::")[-1]
+
+
+def kernel_stats(path):
+    out = {}
+    for r in csv.DictReader(open(path)):
+        out[short(r["Name"])] = {"calls": int(r["Calls"]), "total_ms": int(r["TotalDurationNs"]) / 1e6,
+                                 "avg_us": float(r["AverageNs"]) / 1e3, "pct": float(r["Percentage"])}
+    return out
+
+
+def counter(path, kernel, name):
+    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
+            if short(r["Kernel_Name"]) == kernel and r["Counter_Name"] == name]
+    return vals
+
+
+def main():
+    d, out = sys.argv[1], sys.argv[2]
+    ks = kernel_stats(f"{d}/trace/run_kernel_stats.csv")
+    fetch = counter(f"{d}/fetch/run_counter_collection.csv", "k_extend", "FETCH_SIZE")
+    write = counter(f"{d}/write/run_counter_collection.csv", "k_extend", "WRITE_SIZE")
+    bench = json.loads(open(f"{d}/bench_traced.json").read().strip().splitlines()[-1])
+    res = {
+        "command": "python3 bench.py --steps 16 --warmup 1 --no-cpu  (under rocprofv3 --kernel-trace --stats)",
+        "kernels": ks,
+        "bench_value_traced": bench["value"],
+        "k_extend_pmc": {
+            "launches": len(fetch),
+            "fetch_kib_avg_raw": statistics.mean(fetch) if fetch else None,
+            "write_kib_avg": statistics.mean(write) if write else None,
+            "hbm_bytes_per_launch_corrected": (2 * statistics.mean(fetch) + statistics.mean(write)) * 1024 if fetch and write else None,
+            "correction": "read side x2 (gfx950 FETCH_SIZE halves 16-B/lane reads), KiB x1024",
+        },
+    }
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
