@@ -43,7 +43,7 @@ def parse():
     ap.add_argument("--frames-per-step", type=int, default=16)
     ap.add_argument("--max-segments", type=int, default=0, help="0 = unbounded + RR (C3); 8 = C2")
     ap.add_argument("--row-block", type=int, default=16)
-    ap.add_argument("--cpu-frames", type=int, default=24, help="frames of the CPU baseline sample (full frame)")
+    ap.add_argument("--cpu-frames", type=int, default=48, help="frames of the CPU baseline sample (full frame)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--profile-pass", type=int, default=2, help="steps re-run with per-kernel HIP events (roofline)")
@@ -56,14 +56,14 @@ def cpu_baseline(args):
     if not os.path.exists(exe):
         subprocess.run(["make", "-s", "-C", os.path.join(REPO, "oracle")], check=True)
     env = dict(os.environ, OMP_NUM_THREADS=str(args.cpu_threads))
-    cmd = [exe, os.path.join(REPO, "assets"), str(args.width), str(args.height), str(args.cpu_frames),
+    cmd = [exe, "--cutoff", os.path.join(REPO, "assets"), str(args.width), str(args.height), str(args.cpu_frames),
            "0", str(args.height), str(args.max_segments), str(args.cpu_threads)]
     out = subprocess.run(cmd, capture_output=True, text=True, env=env, check=True).stdout.strip().splitlines()[-1]
     r = json.loads(out)
     return {"value": round(r["mrays_per_s"], 4), "unit": "Mrays/s", "cores": r["threads"], "kind": "port",
             "sample": f"{args.width}x{args.height}, frames 0..{args.cpu_frames - 1} (1 spp each), "
                       f"{'unbounded+RR' if args.max_segments == 0 else 'max %d segments' % args.max_segments}, "
-                      f"oracle/cpu_ref_bench, {r['seconds']:.2f} s",
+                      f"throughput cutoff on (as the GPU), oracle/cpu_ref_bench, {r['seconds']:.2f} s",
             "seconds": r["seconds"], "samples": r["samples"],
             "events": {k: r[k] for k in ("n_ext", "n_hit", "n_cont", "n_shadow", "n_acc", "n_unocc")}}
 

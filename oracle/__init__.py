@@ -51,6 +51,7 @@ def load():
         "orc_trace_closest": ([P, U32, P, P, P, P, P, P, P], None),
         "orc_trace_any": ([P, U32, P, P, P, P], None),
         "orc_trace_brute": ([P, U32, P, P, P, P, P], None),
+        "orc_trace_visits": ([P, U32, P, P, P, P], None),
         "orc_record_rays": ([P, U32, U32, U32, U32, U32, U32, P, P, P, U32, P, P, P, P], None),
         "orc_bvh_depths": ([P, C.POINTER(U32), C.POINTER(U32)], None),
         "orc_init_seed": ([U32], U32), "orc_random_u32": ([C.POINTER(U32)], U32),
@@ -140,6 +141,15 @@ class OracleScene:
         inst, prim = np.zeros(n, np.uint32), np.zeros(n, np.uint32)
         load().orc_trace_brute(self._h, n, _p(o), _p(d), _p(t), _p(inst), _p(prim))
         return t, inst, prim
+
+    def trace_visits(self, o, d):
+        """Per ray and instance: BLAS node visits and triangle tests of the closest-hit traversal."""
+        o = np.ascontiguousarray(o, np.float32).reshape(-1, 3)
+        d = np.ascontiguousarray(d, np.float32).reshape(-1, 3)
+        ni = self.instance_count()
+        nodes, tris = np.zeros((len(o), ni), np.uint32), np.zeros((len(o), ni), np.uint32)
+        load().orc_trace_visits(self._h, len(o), _p(o), _p(d), _p(nodes), _p(tris))
+        return nodes, tris
 
     def record_rays(self, width, height, frame, pix_begin, pix_end, max_ext=1 << 20, max_shadow=1 << 20):
         eo, ed = np.zeros((max_ext, 3), np.float32), np.zeros((max_ext, 3), np.float32)

@@ -459,6 +459,13 @@ struct Hit { float t, u, v; uint32_t inst, prim; };
 /* BvhBLAS::intersect (bvh.cpp:129-191) and intersectAny (:193-253), with the
  * instance world->object transform of Instance::intersect(Any) (:481-513).
  * Returns true when a triangle test succeeded; updates depth / hit. */
+/* Optional traversal statistics (orc_trace_visits): node visits and triangle
+ * tests of the current instance; never set during renders. */
+thread_local uint32_t* tVisitNodes = nullptr;
+thread_local uint32_t* tVisitTris = nullptr;
+thread_local uint32_t* tVisitBaseN = nullptr;   /* per-instance arrays of the current ray */
+thread_local uint32_t* tVisitBaseT = nullptr;
+
 template <bool ANY>
 bool blasTrace(const Blas& B, V3 o, V3 d, float& depth, Hit& hit, uint32_t& stackMax) {
     const Bvh& b = B.bvh;
@@ -467,7 +474,9 @@ bool blasTrace(const Blas& B, V3 o, V3 d, float& depth, Hit& hit, uint32_t& stac
     bool any = false;
     for (;;) {
         const Node& n = b.nodes[ni];
+        if (tVisitNodes) ++*tVisitNodes;
         if (n.cnt != 0) {
+            if (tVisitTris) *tVisitTris += n.cnt;
             for (uint32_t i = 0; i < n.cnt; ++i) {
                 uint32_t p = b.idx[n.lf + i];
                 float u, v;
@@ -524,6 +533,7 @@ bool tlasTrace(const Scene& S, V3 o, V3 d, float& depth, Hit& hit, uint32_t& sta
                 V4 tp = mul(in.Minv, v4(o, 1.0f)), td = mul(in.Minv, v4(d, 0.0f));
                 V3 oo = xyz(tp) / tp.w, dd = xyz(td);
                 uint32_t sm = 0;
+                if (tVisitBaseN) { tVisitNodes = tVisitBaseN + ii; tVisitTris = tVisitBaseT + ii; }
                 bool h = blasTrace<ANY>(*in.blas, oo, dd, depth, hit, sm);
                 if (sp + sm > stackMax) stackMax = sp + sm;
                 if (h) { if (ANY) return true; any = true; hit.inst = ii; }
@@ -948,6 +958,19 @@ void orc_trace_closest(const orc_scene* h, uint32_t n, const float* o, const flo
         bool hit = tlasTrace<false>(S, mk(o[3 * i], o[3 * i + 1], o[3 * i + 2]), mk(d[3 * i], d[3 * i + 1], d[3 * i + 2]), depth, hh, sm);
         ot[i] = depth; ou[i] = hit ? hh.u : 0.0f; ov[i] = hit ? hh.v : 0.0f;
         oi[i] = hit ? hh.inst : kUnset; op[i] = hit ? hh.prim : kUnset;
+    }
+}
+
+void orc_trace_visits(const orc_scene* h, uint32_t n, const float* o, const float* d, uint32_t* nodes, uint32_t* tris) {
+    const Scene& S = *h->s;
+    const size_t ni = S.inst.size();
+    for (int64_t i = 0; i < (int64_t)n; ++i) {
+        float depth = kFarAway;
+        Hit hh; hh.inst = kUnset; hh.prim = kUnset; hh.u = 0.0f; hh.v = 0.0f; hh.t = kFarAway;
+        uint32_t sm = 0;
+        tVisitBaseN = nodes + i * ni; tVisitBaseT = tris + i * ni;
+        tlasTrace<false>(S, mk(o[3 * i], o[3 * i + 1], o[3 * i + 2]), mk(d[3 * i], d[3 * i + 1], d[3 * i + 2]), depth, hh, sm);
+        tVisitBaseN = tVisitBaseT = tVisitNodes = tVisitTris = nullptr;
     }
 }
 

@@ -77,6 +77,9 @@ void orc_trace_closest(const orc_scene*, uint32_t n, const float* o, const float
 /* Any hit of n rays with depth tmax[i]. out[i] = 1 when occluded. */
 void orc_trace_any(const orc_scene*, uint32_t n, const float* o, const float* d,
                    const float* tmax, uint8_t* out);
+/* Closest-hit traversal statistics: per ray and instance (n x instance_count,
+ * instance-id order) BLAS node visits and triangle tests.  Diagnostics. */
+void orc_trace_visits(const orc_scene*, uint32_t n, const float* o, const float* d, uint32_t* nodes, uint32_t* tris);
 /* Brute force closest hit over every instance triangle (no BVH): property check. */
 void orc_trace_brute(const orc_scene*, uint32_t n, const float* o, const float* d,
                      float* out_t, uint32_t* out_inst, uint32_t* out_prim);

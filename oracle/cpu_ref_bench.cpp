@@ -3,16 +3,25 @@
  * (bench.py cpu_baseline leg) and a PFM writer for eyeballing renders.
  * TEST INFRASTRUCTURE ONLY (see cpu_ref.h).
  *
- * usage: cpu_ref_bench ASSETS W H FRAMES [ROW_BEGIN ROW_END [MAX_SEG [THREADS [OUT.pfm]]]]
+ * usage: cpu_ref_bench [--cutoff] ASSETS W H FRAMES [ROW_BEGIN ROW_END [MAX_SEG [THREADS [OUT.pfm]]]]
+ * --cutoff: end paths whose throughput fell below FLT_MIN (orc_set_zero_cutoff),
+ * as the GPU renderer does by default.
  * prints one JSON line: samples, seconds, mrays_per_s, threads, event counts.
  */
 #include "cpu_ref.h"
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 #include <omp.h>
 
 int main(int argc, char** argv) {
+    int cutoff = 0;
+    if (argc > 1 && std::string(argv[1]) == "--cutoff") {
+        cutoff = 1;
+        orc_set_zero_cutoff(1);
+        ++argv; --argc;
+    }
     if (argc < 5) { fprintf(stderr, "usage: %s ASSETS W H FRAMES [ROW_BEGIN ROW_END [MAX_SEG [THREADS [OUT.pfm]]]]\n", argv[0]); return 2; }
     const char* assets = argv[1];
     uint32_t W = (uint32_t)atoi(argv[2]), H = (uint32_t)atoi(argv[3]), F = (uint32_t)atoi(argv[4]);
@@ -28,11 +37,11 @@ int main(int argc, char** argv) {
     double sec = orc_render(s, W, H, r0, r1, 0, F, maxSeg, threads, acc.data(), &c);
     int used = threads > 0 ? threads : omp_get_max_threads();
     printf("{\"samples\": %llu, \"seconds\": %.6f, \"mrays_per_s\": %.4f, \"threads\": %d, "
-           "\"n_ext\": %llu, \"n_hit\": %llu, \"n_cont\": %llu, \"n_shadow\": %llu, \"n_acc\": %llu, \"n_unocc\": %llu, \"max_segments\": %llu}\n",
+           "\"n_ext\": %llu, \"n_hit\": %llu, \"n_cont\": %llu, \"n_shadow\": %llu, \"n_acc\": %llu, \"n_unocc\": %llu, \"max_segments\": %llu, \"cutoff\": %d}\n",
            (unsigned long long)c.samples, sec, (double)c.samples / sec / 1e6, used,
            (unsigned long long)c.n_ext, (unsigned long long)c.n_hit, (unsigned long long)c.n_cont,
            (unsigned long long)c.n_shadow, (unsigned long long)c.n_acc, (unsigned long long)c.n_unocc,
-           (unsigned long long)c.max_segments);
+           (unsigned long long)c.max_segments, cutoff);
     if (out) {
         FILE* f = fopen(out, "wb");
         if (f) {

@@ -171,6 +171,22 @@ SURF_HD float slab(float mnx, float mny, float mnz, float mxx, float mxy, float 
     return (t1 >= t0 && t0 < depth && t1 > 0.0f) ? t0 : kFarAway;
 }
 
+/* Same value as slab() (up to the sign of a zero, which only ever meets
+ * comparisons) when no NaN can arise: o, rd and the box finite.  Then every
+ * (b - o) * rd is finite or +-inf, never 0 * inf, so the ternary min/max of
+ * the reference equal IEEE min/max and fold to v_min3/v_max3. */
+SURF_HD float slabFinite(float mnx, float mny, float mnz, float mxx, float mxy, float mxz,
+                         V3 o, V3 rd, float depth) {
+    const float tx0 = (mnx - o.x) * rd.x, tx1 = (mxx - o.x) * rd.x;
+    const float ty0 = (mny - o.y) * rd.y, ty1 = (mxy - o.y) * rd.y;
+    const float tz0 = (mnz - o.z) * rd.z, tz1 = (mxz - o.z) * rd.z;
+    const float t0 = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fminf(tz0, tz1));
+    const float t1 = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
+    return (t1 >= t0 && t0 < depth && t1 > 0.0f) ? t0 : kFarAway;
+}
+
+SURF_HD bool finite3(V3 v) { return fabsf(v.x) <= 3.40282347e38f && fabsf(v.y) <= 3.40282347e38f && fabsf(v.z) <= 3.40282347e38f; }
+
 /* ---- Moller-Trumbore, mesh.cpp:23-62, with e1 = v1-v0, e2 = v2-v0 precomputed
  *      (the same f32 subtraction the reference performs per test). ---- */
 SURF_HD bool triHit(V3 v0, V3 e1, V3 e2, V3 o, V3 d, float& depth, float& hu, float& hv) {

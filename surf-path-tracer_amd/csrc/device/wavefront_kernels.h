@@ -36,6 +36,13 @@ namespace surfdev {
 constexpr uint32_t kUnset = 0xffffffffu;
 constexpr uint32_t kFlagMedium = 1u, kFlagSpecular = 2u;
 constexpr int kBlock = 256;
+/* Minimum waves per SIMD the register allocator must allow (occupancy). */
+#ifndef SURF_SHADE_WAVES
+#define SURF_SHADE_WAVES 3
+#endif
+#ifndef SURF_TRACE_WAVES
+#define SURF_TRACE_WAVES 1
+#endif
 
 struct DevInstance {          /* 160 B */
     float Minv[16];
@@ -52,7 +59,19 @@ struct DevMaterial {          /* = Material (64 B) */
     float ec[4], albedo[4], absorb[4];
 };
 
+/* Per-instance traversal record (144 B), host-built at upload: rows of M^-1
+ * (row i = m[i], m[4+i], m[8+i], m[12+i]), offsets, and the BLAS root record.
+ * Kernels stage the table in LDS, so the per-instance loop of every ray reads
+ * LDS instead of paying two dependent memory trips per instance. */
+struct TraceInst {
+    float4 m0, m1, m2, m3;
+    uint4 meta;               /* nodeOffset, idxOffset, affineInv, instance id */
+    float4 r0, r1, r2, r3;    /* root node record */
+};
+constexpr uint32_t kLdsTraceInst = 64;   /* instances staged in LDS (9 KB) */
+
 struct DevScene {
+    const TraceInst* tinst;   /* [nInst], instance-id order */
     const float4* nodes;      /* BLAS: 4 float4 per node (see upload) */
     const float4* tris;       /* 3 float4 per BLAS index slot: (v0, prim), e1, e2 */
     const float4* normals;    /* 3 float4 per global triangle: n0, n1, n2 */
@@ -65,6 +84,7 @@ struct DevScene {
     uint32_t nLights;
     uint32_t nInst, nMats;
     uint32_t tlasLeafCount;   /* TLAS root is a leaf with this many instances (0: general TLAS) */
+    uint32_t finiteBoxes;     /* every BLAS node box is finite: slabFinite is exact */
     uint32_t bgType;
     float bgColor[3], bgA[3], bgB[3];
 };
@@ -82,8 +102,8 @@ struct ShadowQ { float4* o; float4* d; float4* c; };
  * kernel writes a word another block of the same launch still reads. */
 struct Counters {
     uint32_t nIn[2];                 /* paths in pool[p] when a phase reads it */
-    uint32_t nApp[2];                /* continuation append cursor into pool[p] */
-    uint32_t nSh[2];                 /* shadow queue length of phase parity p */
+    unsigned long long app[2];       /* phase parity p: low 32 = paths appended to pool[p^1],
+                                        high 32 = shadow rays queued (one packed atomic per block) */
     uint32_t maxSeg;                 /* 0 = unbounded */
     uint32_t zeroCutoff;             /* end paths whose throughput is exactly 0 (radiance-neutral) */
     uint32_t segMax;                 /* longest finished path (extension rays), diagnostics */
@@ -93,7 +113,12 @@ struct Counters {
     unsigned long long baseFrame;    /* absolute frame index of stream frame 0 */
     unsigned long long ev[8];        /* ext, hit, cont, shadow, acc, unocc, tail paths, capped paths */
     uint32_t capped[64];             /* sample ids of the first paths ended by the segment cap (diagnostics) */
+    /* event counts striped over kStripes cache lines (block b adds to stripe
+     * b % kStripes): a counter shared by every block of a launch serializes its
+     * atomics (~12 ns each, measured); totals = ev + sum over stripes */
+    unsigned long long evS[32][16];
 };
+constexpr uint32_t kStripes = 32;    /* frameDone and event-count stripes */
 
 /* Where a stream sample lives: radiance slot sid = (frame % window) * npx + pixel. */
 struct StreamGeom {
@@ -116,9 +141,34 @@ SURF_HD V3 xyz(float4 v) { return mk3(v.x, v.y, v.z); }
  * The root record is read once per instance before the per-lane loop: when
  * the instance index is wave-uniform (single-leaf TLAS) those are scalar
  * loads, as are the triangles of a root leaf (the room's planes). */
+/* Pins a loaded record in registers: the compiler may not sink any part of the
+ * load below this point, so all 16-B loads of a node or triangle are issued
+ * together and paid as one memory round trip (without it, the leaf/count words
+ * are fetched first and the boxes only after the leaf branch: two trips). */
+__device__ __forceinline__ void pin(float4& v) { asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w)); }
+
 template <bool ANY>
 __device__ __forceinline__ bool leafTest(const float4* tri, uint32_t lf, uint32_t cnt, V3 o, V3 d, float& depth,
                                          float& hu, float& hv, uint32_t& hprim) {
+    bool any = false;
+    for (uint32_t k = 0; k < cnt; ++k) {
+        const float4* tp = tri + 3u * (lf + k);
+        float4 a = tp[0], b = tp[1], c = tp[2];
+        pin(a); pin(b); pin(c);
+        float u, v;
+        if (triHit(xyz(a), xyz(b), xyz(c), o, d, depth, u, v)) {
+            if (ANY) return true;
+            any = true;
+            hu = u; hv = v; hprim = f2u(a.w);
+        }
+    }
+    return any;
+}
+
+/* Scalar (wave-uniform) variant for a root leaf: no pinning, s_load path. */
+template <bool ANY>
+__device__ __forceinline__ bool leafTestUniform(const float4* tri, uint32_t lf, uint32_t cnt, V3 o, V3 d, float& depth,
+                                                float& hu, float& hv, uint32_t& hprim) {
     bool any = false;
     for (uint32_t k = 0; k < cnt; ++k) {
         const float4 a = tri[3u * (lf + k)], b = tri[3u * (lf + k) + 1u], c = tri[3u * (lf + k) + 2u];
@@ -132,54 +182,65 @@ __device__ __forceinline__ bool leafTest(const float4* tri, uint32_t lf, uint32_
     return any;
 }
 
-template <bool ANY>
-__device__ __forceinline__ bool blasTrace(const DevScene& S, uint32_t nodeOff, uint32_t idxOff, V3 o, V3 d, float& depth,
+template <bool FIN>
+__device__ __forceinline__ float boxDist(float4 lo, float4 hi, V3 o, V3 rd, float depth) {
+    return FIN ? slabFinite(lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, o, rd, depth)
+               : slab(lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, o, rd, depth);
+}
+
+/* FIN: o, rd and every box finite (slabFinite is exact); else the reference's
+ * ternary slab with its NaN behaviour. */
+template <bool ANY, bool FIN>
+__device__ __forceinline__ bool blasTrace(const DevScene& S, const TraceInst& I, V3 o, V3 d, V3 rd, float& depth,
                                           float& hu, float& hv, uint32_t& hprim,
                                           uint32_t* stk, uint32_t stride, uint32_t base) {
-    const V3 rd = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-    const float4* tri = S.tris + 3u * idxOff;
+    const uint32_t nodeOff = I.meta.x;
+    const float4* tri = S.tris + 3u * I.meta.y;
     /* root: never box-tested (bvh.cpp:131), only its children are */
-    const float4* rn = S.nodes + 4u * nodeOff;
-    const float4 r0 = rn[0], r1 = rn[1];
+    const float4 r0 = I.r0, r1 = I.r1;
     const uint32_t rlf = f2u(r0.w), rcnt = f2u(r1.w);
-    if (rcnt != 0u) return leafTest<ANY>(tri, rlf, rcnt, o, d, depth, hu, hv, hprim);
-    uint32_t sp = base;
+    if (rcnt != 0u) return leafTestUniform<ANY>(tri, rlf, rcnt, o, d, depth, hu, hv, hprim);
+    /* stack pointer walks in steps of `stride` words (lane-interleaved LDS) */
+    uint32_t* const bottom = stk + base * stride;
+    uint32_t* sp = bottom;
     uint32_t node;
     bool any = false;
     {
-        const float4 r2 = rn[2], r3 = rn[3];
-        float dn = slab(r0.x, r0.y, r0.z, r1.x, r1.y, r1.z, o, rd, depth);
-        float df = slab(r2.x, r2.y, r2.z, r3.x, r3.y, r3.z, o, rd, depth);
+        const float4 r2 = I.r2, r3 = I.r3;
+        float dn = boxDist<FIN>(r0, r1, o, rd, depth);
+        float df = boxDist<FIN>(r2, r3, o, rd, depth);
         uint32_t cn = nodeOff + rlf, cf = cn + 1u;
         if (dn > df) { const float t = dn; dn = df; df = t; const uint32_t c = cn; cn = cf; cf = c; }
         if (dn == kFarAway) return false;
         node = cn;
-        if (df != kFarAway) stk[(sp++) * stride] = cf;
+        if (df != kFarAway) { *sp = cf; sp += stride; }
     }
     for (;;) {
         const float4* nd = S.nodes + 4u * node;
-        const float4 q0 = nd[0], q1 = nd[1];
+        float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
+        pin(q0); pin(q1); pin(q2); pin(q3);
         const uint32_t lf = f2u(q0.w), cnt = f2u(q1.w);
         if (cnt != 0u) {
             if (leafTest<ANY>(tri, lf, cnt, o, d, depth, hu, hv, hprim)) {
                 if (ANY) return true;
                 any = true;
             }
-            if (sp == base) break;
-            node = stk[(--sp) * stride];
+            if (sp == bottom) break;
+            sp -= stride;
+            node = *sp;
             continue;
         }
-        const float4 q2 = nd[2], q3 = nd[3];
-        float dn = slab(q0.x, q0.y, q0.z, q1.x, q1.y, q1.z, o, rd, depth);
-        float df = slab(q2.x, q2.y, q2.z, q3.x, q3.y, q3.z, o, rd, depth);
+        float dn = boxDist<FIN>(q0, q1, o, rd, depth);
+        float df = boxDist<FIN>(q2, q3, o, rd, depth);
         uint32_t cn = nodeOff + lf, cf = cn + 1u;
         if (dn > df) { const float t = dn; dn = df; df = t; const uint32_t c = cn; cn = cf; cf = c; }
         if (dn == kFarAway) {
-            if (sp == base) break;
-            node = stk[(--sp) * stride];
+            if (sp == bottom) break;
+            sp -= stride;
+            node = *sp;
         } else {
             node = cn;
-            if (df != kFarAway) stk[(sp++) * stride] = cf;
+            if (df != kFarAway) { *sp = cf; sp += stride; }
         }
     }
     return any;
@@ -188,28 +249,62 @@ __device__ __forceinline__ bool blasTrace(const DevScene& S, uint32_t nodeOff, u
 /* Instance::intersect(Any) (bvh.cpp:481-513): origin (M^-1 (o,1)).xyz / w,
  * direction (M^-1 (d,0)).xyz (not renormalized: t is shared with world space).
  * For an affine M^-1 (row 3 = 0,0,0,1) w is exactly 1 for finite o and x/1 = x,
- * so the division is skipped without changing a bit. */
+ * so the division is skipped without changing a bit.  Row products keep glm's
+ * pairwise sum (m0 x + m1 y) + (m2 z + m3 w) (mrow). */
+__device__ __forceinline__ float rowDot(float4 r, float x, float y, float z, float w) {
+    const float a = r.x * x + r.y * y;
+    const float b = r.z * z + r.w * w;
+    return a + b;
+}
+
 template <bool ANY>
-__device__ __forceinline__ bool instanceTrace(const DevScene& S, const DevInstance& I, V3 o, V3 d, float& depth, float& hu,
+__device__ __forceinline__ bool instanceTrace(const DevScene& S, const TraceInst& I, V3 o, V3 d, float& depth, float& hu,
                                               float& hv, uint32_t& hprim, uint32_t* stk, uint32_t stride, uint32_t base) {
-    const float* m = I.Minv;
-    V3 oo = mk3(mrow(m, 0, o.x, o.y, o.z, 1.0f), mrow(m, 1, o.x, o.y, o.z, 1.0f), mrow(m, 2, o.x, o.y, o.z, 1.0f));
-    if (!I.affineInv) oo = divs(oo, mrow(m, 3, o.x, o.y, o.z, 1.0f));
-    const V3 dd = mk3(mrow(m, 0, d.x, d.y, d.z, 0.0f), mrow(m, 1, d.x, d.y, d.z, 0.0f), mrow(m, 2, d.x, d.y, d.z, 0.0f));
-    return blasTrace<ANY>(S, I.nodeOffset, I.idxOffset, oo, dd, depth, hu, hv, hprim, stk, stride, base);
+    V3 oo = mk3(rowDot(I.m0, o.x, o.y, o.z, 1.0f), rowDot(I.m1, o.x, o.y, o.z, 1.0f), rowDot(I.m2, o.x, o.y, o.z, 1.0f));
+    if (!I.meta.z) oo = divs(oo, rowDot(I.m3, o.x, o.y, o.z, 1.0f));
+    const V3 dd = mk3(rowDot(I.m0, d.x, d.y, d.z, 0.0f), rowDot(I.m1, d.x, d.y, d.z, 0.0f), rowDot(I.m2, d.x, d.y, d.z, 0.0f));
+    const V3 rd = mk3(1.0f / dd.x, 1.0f / dd.y, 1.0f / dd.z);
+    /* S.finiteBoxes: every BLAS box is finite (checked at upload) */
+    if (S.finiteBoxes && finite3(oo) && finite3(rd))
+        return blasTrace<ANY, true>(S, I, oo, dd, rd, depth, hu, hv, hprim, stk, stride, base);
+    return blasTrace<ANY, false>(S, I, oo, dd, rd, depth, hu, hv, hprim, stk, stride, base);
+}
+
+/* Instance tables a traversal reads: LDS copies (stageTrace) or global. */
+struct TraceTables {
+    const TraceInst* inst;    /* by instance id */
+    const uint32_t* order;    /* TLAS leaf index array (tlasIndices) */
+};
+
+/* Dynamic LDS layout of the traversal kernels: [stack: depth x blockDim u32]
+ * [TraceInst x nInst][tlasIdx x nInst].  Every thread of the block calls this. */
+__device__ __forceinline__ TraceTables stageTrace(const DevScene& S, uint32_t* lds, uint32_t stackWords) {
+    TraceInst* tab = reinterpret_cast<TraceInst*>(lds + stackWords);
+    uint32_t* order = reinterpret_cast<uint32_t*>(tab + S.nInst);
+    const uint32_t n16 = S.nInst * (uint32_t)(sizeof(TraceInst) / 16);
+    for (uint32_t k = threadIdx.x; k < n16; k += blockDim.x) reinterpret_cast<float4*>(tab)[k] = reinterpret_cast<const float4*>(S.tinst)[k];
+    for (uint32_t k = threadIdx.x; k < S.nInst; k += blockDim.x) order[k] = S.tlasIdx[k];
+    __syncthreads();
+    return TraceTables{tab, order};
+}
+
+template <bool LDS_INST>
+__device__ __forceinline__ TraceTables traceTables(const DevScene& S, uint32_t* lds, uint32_t stackWords) {
+    if (LDS_INST) return stageTrace(S, lds, stackWords);
+    return TraceTables{S.tinst, S.tlasIdx};
 }
 
 /* BvhTLAS::intersect / intersectAny (bvh.cpp:654-778). */
 template <bool ANY>
-__device__ __forceinline__ bool traceScene(const DevScene& S, V3 o, V3 d, float& depth, float& hu, float& hv,
+__device__ __forceinline__ bool traceScene(const DevScene& S, const TraceTables& Tt, V3 o, V3 d, float& depth, float& hu, float& hv,
                                            uint32_t& hinst, uint32_t& hprim, uint32_t* stk, uint32_t stride) {
     bool any = false;
     if (S.tlasLeafCount) {
         /* single-leaf TLAS (the bundled scene): every lane visits the same
-         * instances in the same order -> wave-uniform loop, scalar loads */
+         * instances in the same order -> wave-uniform loop over LDS records */
         for (uint32_t k = 0; k < S.tlasLeafCount; ++k) {
-            const uint32_t ii = S.tlasIdx[k];
-            if (instanceTrace<ANY>(S, S.inst[ii], o, d, depth, hu, hv, hprim, stk, stride, 0u)) {
+            const uint32_t ii = Tt.order[k];
+            if (instanceTrace<ANY>(S, Tt.inst[ii], o, d, depth, hu, hv, hprim, stk, stride, 0u)) {
                 if (ANY) return true;
                 any = true;
                 hinst = ii;
@@ -221,12 +316,13 @@ __device__ __forceinline__ bool traceScene(const DevScene& S, V3 o, V3 d, float&
     uint32_t sp = 0, node = 0;
     for (;;) {
         const float4* nd = S.tlasNodes + 4u * node;
-        const float4 q0 = nd[0], q1 = nd[1];
+        float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
+        pin(q0); pin(q1); pin(q2); pin(q3);
         const uint32_t lf = f2u(q0.w), cnt = f2u(q1.w);
         if (cnt != 0u) {
             for (uint32_t k = 0; k < cnt; ++k) {
-                const uint32_t ii = S.tlasIdx[lf + k];
-                if (instanceTrace<ANY>(S, S.inst[ii], o, d, depth, hu, hv, hprim, stk, stride, sp)) {
+                const uint32_t ii = Tt.order[lf + k];
+                if (instanceTrace<ANY>(S, Tt.inst[ii], o, d, depth, hu, hv, hprim, stk, stride, sp)) {
                     if (ANY) return true;
                     any = true;
                     hinst = ii;
@@ -236,7 +332,6 @@ __device__ __forceinline__ bool traceScene(const DevScene& S, V3 o, V3 d, float&
             node = stk[(--sp) * stride];
             continue;
         }
-        const float4 q2 = nd[2], q3 = nd[3];
         float dn = slab(q0.x, q0.y, q0.z, q1.x, q1.y, q1.z, o, rd, depth);
         float df = slab(q2.x, q2.y, q2.z, q3.x, q3.y, q3.z, o, rd, depth);
         uint32_t cn = lf, cf = lf + 1u;
@@ -268,10 +363,33 @@ __device__ __forceinline__ void waveCount(unsigned long long* ctr, unsigned long
     if (laneId() == 0 && v) atomicAdd(ctr, v);
 }
 
+/* Block-level event counts: one atomic per counter per workgroup (the counters
+ * are hot addresses shared by every wave of the launch).  vals are wave-uniform;
+ * every thread of the block must call this. */
+template <int N>
+__device__ __forceinline__ void blockCount(Counters* C, const int (&idx)[N], const unsigned long long (&vals)[N]) {
+    unsigned long long* ev = C->evS[blockIdx.x % kStripes];
+    __shared__ unsigned long long sEv[N][kBlock / 64];
+    const uint32_t w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    if (laneId() == 0)
+        for (int k = 0; k < N; ++k) sEv[k][w] = vals[k];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int k = 0; k < N; ++k) {
+            unsigned long long t = 0;
+            for (uint32_t j = 0; j < nw; ++j) t += sEv[k][j];
+            if (t) atomicAdd(&ev[idx[k]], t);
+        }
+    }
+}
+
 /* ------------------------------------------------------------------ kernels */
-__global__ __launch_bounds__(kBlock) void k_extend(DevScene S, Pool cur, float4* __restrict__ hitTUV,
-                                                   uint32_t* __restrict__ hitInst, const Counters* C, int par) {
+template <bool LDS>
+__global__ __launch_bounds__(kBlock, SURF_TRACE_WAVES) void k_extend(DevScene S, Pool cur, float4* __restrict__ hitTUV,
+                                                   uint32_t* __restrict__ hitInst, const Counters* C, int par, uint32_t stackWords) {
     extern __shared__ uint32_t lds[];
+    const TraceTables Tt = traceTables<LDS>(S, lds, stackWords);
     const uint32_t n = C->nIn[par];
     const uint32_t stride = blockDim.x;
     uint32_t* stk = lds + threadIdx.x;
@@ -279,7 +397,7 @@ __global__ __launch_bounds__(kBlock) void k_extend(DevScene S, Pool cur, float4*
         const float4 o = cur.o[i], d = cur.d[i];
         float depth = kFarAway, u = 0.0f, v = 0.0f;
         uint32_t inst = kUnset, prim = kUnset;
-        const bool hit = traceScene<false>(S, xyz(o), xyz(d), depth, u, v, inst, prim, stk, stride);
+        const bool hit = traceScene<false>(S, Tt, xyz(o), xyz(d), depth, u, v, inst, prim, stk, stride);
         hitTUV[i] = make_float4(depth, u, v, u2f(prim));
         hitInst[i] = hit ? inst : kUnset;
     }
@@ -498,10 +616,10 @@ __device__ __forceinline__ void frameDoneAdd(uint32_t* frameDone, bool done, uin
 }
 
 template <bool LDS_TABLES>
-__global__ __launch_bounds__(kBlock) void k_shade(DevScene S, Pool cur, Pool nxt, const float4* __restrict__ hitTUV,
+__global__ __launch_bounds__(kBlock, SURF_SHADE_WAVES) void k_shade(DevScene S, Pool cur, Pool nxt, const float4* __restrict__ hitTUV,
                                                   const uint32_t* __restrict__ hitInst, ShadowQ Q,
                                                   float4* __restrict__ rad, uint32_t* __restrict__ frameDone,
-                                                  uint32_t npx, Counters* C, int par) {
+                                                  uint32_t npx, uint32_t window, Counters* C, int par) {
     __shared__ DevInstance sInst[LDS_TABLES ? kLdsInst : 1];
     __shared__ DevMaterial sMat[LDS_TABLES ? kLdsMats : 1];
     __shared__ uint2 sLights[LDS_TABLES ? kLdsLights : 1];
@@ -510,11 +628,16 @@ __global__ __launch_bounds__(kBlock) void k_shade(DevScene S, Pool cur, Pool nxt
         stageTables(S, sInst, sMat, sLights);
         Tb = ShadeTables{sInst, sMat, sLights};
     }
+    /* block-level compaction: per iteration one packed 64-bit atomic reserves the
+     * block's continuation and shadow slots (LDS double-buffered by iteration) */
+    __shared__ uint32_t sWave[2][kBlock / 64][2];
+    __shared__ uint32_t sBase[2][2];
     const uint32_t n = C->nIn[par];
     const uint32_t maxSeg = C->maxSeg, zeroCutoff = C->zeroCutoff;
-    const int nx = par ^ 1;
+    const uint32_t wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    uint32_t it = 0;
     unsigned long long cHit = 0, cCont = 0, cSh = 0, cAcc = 0;
-    for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
+    for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x, it ^= 1u) {
         const uint32_t i = base + threadIdx.x;
         ShadeOut r;
         r.cont = r.shadow = r.hitGeom = r.accd = r.capped = false;
@@ -527,13 +650,24 @@ __global__ __launch_bounds__(kBlock) void k_shade(DevScene S, Pool cur, Pool nxt
             shadePath(S, Tb, o4, cur.d[i], cur.T[i], hitTUV[i], hitInst[i], rad, maxSeg, zeroCutoff, r);
         }
         const unsigned long long mCont = __ballot(r.cont), mSh = __ballot(r.shadow);
-        const uint32_t jc = waveAppend(&C->nApp[nx], mCont);
-        const uint32_t js = waveAppend(&C->nSh[par], mSh);
+        if (laneId() == 0) { sWave[it][wv][0] = (uint32_t)__popcll(mCont); sWave[it][wv][1] = (uint32_t)__popcll(mSh); }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned long long tc = 0, ts = 0;
+            for (uint32_t k = 0; k < nw; ++k) { tc += sWave[it][k][0]; ts += sWave[it][k][1]; }
+            const unsigned long long old = (tc | ts) ? atomicAdd(&C->app[par], (ts << 32) | tc) : 0ull;
+            sBase[it][0] = (uint32_t)old; sBase[it][1] = (uint32_t)(old >> 32);
+        }
+        __syncthreads();
+        uint32_t jc = sBase[it][0], js = sBase[it][1];
+        for (uint32_t k = 0; k < wv; ++k) { jc += sWave[it][k][0]; js += sWave[it][k][1]; }
+        jc += rankBelow(mCont);
+        js += rankBelow(mSh);
         if (r.cont) { nxt.o[jc] = r.o; nxt.d[jc] = r.d; nxt.T[jc] = r.T; }
         if (r.shadow) { Q.o[js] = r.so; Q.d[js] = r.sd; Q.c[js] = r.sc; }
         /* a path that ends here may still have this phase's shadow ray pending:
          * connect runs before the host reads frameDone (end of the phase). */
-        frameDoneAdd(frameDone, active && !r.cont, slot);
+        frameDoneAdd(frameDone + (blockIdx.x % kStripes) * window, active && !r.cont, slot);
         if (active && !r.cont && r.seg > 32u) atomicMax(&C->segMax, r.seg);   /* rare: RR ends most paths early */
         if (r.capped) {
             const unsigned long long k = atomicAdd(&C->ev[7], 1ull);
@@ -544,15 +678,15 @@ __global__ __launch_bounds__(kBlock) void k_shade(DevScene S, Pool cur, Pool nxt
         cSh += (unsigned long long)__popcll(mSh);
         cAcc += (unsigned long long)__popcll(__ballot(r.accd));
     }
-    waveCount(&C->ev[1], cHit);
-    waveCount(&C->ev[2], cCont);
-    waveCount(&C->ev[3], cSh);
-    waveCount(&C->ev[4], cAcc);
+    blockCount<4>(C, {1, 2, 3, 4}, {cHit, cCont, cSh, cAcc});
 }
 
-__global__ __launch_bounds__(kBlock) void k_connect(DevScene S, ShadowQ Q, float4* __restrict__ rad, Counters* C, int par) {
+template <bool LDS>
+__global__ __launch_bounds__(kBlock, SURF_TRACE_WAVES) void k_connect(DevScene S, ShadowQ Q, float4* __restrict__ rad, Counters* C, int par,
+                                                    uint32_t stackWords) {
     extern __shared__ uint32_t lds[];
-    const uint32_t n = C->nSh[par];
+    const TraceTables Tt = traceTables<LDS>(S, lds, stackWords);
+    const uint32_t n = (uint32_t)(C->app[par] >> 32);
     const uint32_t stride = blockDim.x;
     uint32_t* stk = lds + threadIdx.x;
     unsigned long long cUn = 0;
@@ -563,7 +697,7 @@ __global__ __launch_bounds__(kBlock) void k_connect(DevScene S, ShadowQ Q, float
             const float4 o = Q.o[i], d = Q.d[i];
             float depth = o.w, u = 0.0f, v = 0.0f;
             uint32_t inst = kUnset, prim = kUnset;
-            const bool occ = traceScene<true>(S, xyz(o), xyz(d), depth, u, v, inst, prim, stk, stride);
+            const bool occ = traceScene<true>(S, Tt, xyz(o), xyz(d), depth, u, v, inst, prim, stk, stride);
             if (!occ) {
                 const float4 c = Q.c[i];
                 addRadiance(rad, f2u(d.w), xyz(c));
@@ -572,8 +706,7 @@ __global__ __launch_bounds__(kBlock) void k_connect(DevScene S, ShadowQ Q, float
         }
         cUn += (unsigned long long)__popcll(__ballot(unocc));
     }
-    waveCount(&C->ev[5], cUn);
-    waveCount(&C->ev[4], cUn);
+    blockCount<2>(C, {5, 4}, {cUn, cUn});
 }
 
 /* Camera::getPrimaryRay + sampleDefocusDisk (camera.h:59-87), jitter of
@@ -582,7 +715,7 @@ __global__ __launch_bounds__(kBlock) void k_connect(DevScene S, ShadowQ Q, float
 __global__ __launch_bounds__(kBlock) void k_regen(DevCamera cam, Pool nxt, float4* __restrict__ rad, Counters* C, int par,
                                                   uint32_t capacity, StreamGeom G) {
     const int nx = par ^ 1;
-    const uint32_t cont = C->nApp[nx];
+    const uint32_t cont = (uint32_t)C->app[par];
     const unsigned long long iss = C->issued[par];
     const unsigned long long lim = C->limit;
     const unsigned long long base = C->baseFrame;
@@ -628,8 +761,7 @@ __global__ __launch_bounds__(kBlock) void k_regen(DevCamera cam, Pool nxt, float
     if (gid == 0) {
         C->nIn[nx] = cont + nnew;
         C->issued[nx] = iss + nnew;
-        C->nApp[par] = 0;
-        C->nSh[nx] = 0;
+        C->app[nx] = 0ull;             /* next phase's append cursors */
         C->ev[0] += cont + nnew;     /* extension rays of the next phase */
     }
 }
@@ -640,8 +772,10 @@ __global__ __launch_bounds__(kBlock) void k_regen(DevCamera cam, Pool nxt, float
  * the wavefront kernels: identical results.  lanes < lpw of each wave work. */
 template <bool LDS_TABLES>
 __global__ __launch_bounds__(64) void k_tail(DevScene S, Pool cur, uint32_t n, uint32_t lpw, float4* __restrict__ rad,
-                                             uint32_t* __restrict__ frameDone, uint32_t npx, Counters* C) {
+                                             uint32_t* __restrict__ frameDone, uint32_t npx, uint32_t window, Counters* C,
+                                             uint32_t stackWords) {
     extern __shared__ uint32_t lds[];
+    const TraceTables Tt = traceTables<LDS_TABLES>(S, lds, stackWords);
     __shared__ DevInstance sInst[LDS_TABLES ? kLdsInst : 1];
     __shared__ DevMaterial sMat[LDS_TABLES ? kLdsMats : 1];
     __shared__ uint2 sLights[LDS_TABLES ? kLdsLights : 1];
@@ -662,7 +796,7 @@ __global__ __launch_bounds__(64) void k_tail(DevScene S, Pool cur, uint32_t n, u
     for (;;) {
         float depth = kFarAway, u = 0.0f, v = 0.0f;
         uint32_t inst = kUnset, prim = kUnset;
-        const bool hit = traceScene<false>(S, xyz(o4), xyz(d4), depth, u, v, inst, prim, stk, stride);
+        const bool hit = traceScene<false>(S, Tt, xyz(o4), xyz(d4), depth, u, v, inst, prim, stk, stride);
         ++nExt;
         ShadeOut r;
         shadePath(S, Tb, o4, d4, T4, make_float4(depth, u, v, u2f(prim)), hit ? inst : kUnset, rad, maxSeg, zeroCutoff, r);
@@ -671,7 +805,7 @@ __global__ __launch_bounds__(64) void k_tail(DevScene S, Pool cur, uint32_t n, u
             ++nSh;
             float sdep = r.so.w, su = 0.0f, sv = 0.0f;
             uint32_t si = kUnset, sp = kUnset;
-            if (!traceScene<true>(S, xyz(r.so), xyz(r.sd), sdep, su, sv, si, sp, stk, stride)) {
+            if (!traceScene<true>(S, Tt, xyz(r.so), xyz(r.sd), sdep, su, sv, si, sp, stk, stride)) {
                 addRadiance(rad, f2u(r.sd.w), xyz(r.sc));
                 ++nUn; ++nAcc;
             }
@@ -684,10 +818,12 @@ __global__ __launch_bounds__(64) void k_tail(DevScene S, Pool cur, uint32_t n, u
         ++nCont;
         o4 = r.o; d4 = r.d; T4 = r.T;
     }
-    atomicAdd(&frameDone[slot], 1u);
-    atomicAdd(&C->ev[0], nExt - 1ull); atomicAdd(&C->ev[1], nHit); atomicAdd(&C->ev[2], nCont);
-    atomicAdd(&C->ev[3], nSh); atomicAdd(&C->ev[4], nAcc); atomicAdd(&C->ev[5], nUn);
-    atomicAdd(&C->ev[6], 1ull);
+    const uint32_t st = blockIdx.x % kStripes;
+    unsigned long long* ev = C->evS[st];
+    atomicAdd(&frameDone[st * window + slot], 1u);
+    atomicAdd(&ev[0], nExt - 1ull); atomicAdd(&ev[1], nHit); atomicAdd(&ev[2], nCont);
+    atomicAdd(&ev[3], nSh); atomicAdd(&ev[4], nAcc); atomicAdd(&ev[5], nUn);
+    atomicAdd(&ev[6], 1ull);
 }
 
 /* acc[p] += (radiance, 1) for frames [f0, f0+count) of the stream, in frame
@@ -721,26 +857,32 @@ __global__ __launch_bounds__(kBlock) void k_finalize(const float4* __restrict__ 
 }
 
 /* Traversal entry points for kernel-level parity tests. */
+template <bool LDS>
 __global__ __launch_bounds__(kBlock) void k_trace_closest(DevScene S, const float* __restrict__ o, const float* __restrict__ d,
-                                                          uint32_t n, float4* __restrict__ tuv, uint2* __restrict__ ip) {
+                                                          uint32_t n, float4* __restrict__ tuv, uint2* __restrict__ ip,
+                                                          uint32_t stackWords) {
     extern __shared__ uint32_t lds[];
+    const TraceTables Tt = traceTables<LDS>(S, lds, stackWords);
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     float depth = kFarAway, u = 0.0f, v = 0.0f;
     uint32_t inst = kUnset, prim = kUnset;
-    const bool hit = traceScene<false>(S, mk3(o[3 * i], o[3 * i + 1], o[3 * i + 2]), mk3(d[3 * i], d[3 * i + 1], d[3 * i + 2]),
+    const bool hit = traceScene<false>(S, Tt, mk3(o[3 * i], o[3 * i + 1], o[3 * i + 2]), mk3(d[3 * i], d[3 * i + 1], d[3 * i + 2]),
                                        depth, u, v, inst, prim, lds + threadIdx.x, blockDim.x);
     tuv[i] = make_float4(depth, hit ? u : 0.0f, hit ? v : 0.0f, 0.0f);
     ip[i] = make_uint2(hit ? inst : kUnset, hit ? prim : kUnset);
 }
+template <bool LDS>
 __global__ __launch_bounds__(kBlock) void k_trace_any(DevScene S, const float* __restrict__ o, const float* __restrict__ d,
-                                                      const float* __restrict__ tmaxv, uint32_t n, uint8_t* __restrict__ occ) {
+                                                      const float* __restrict__ tmaxv, uint32_t n, uint8_t* __restrict__ occ,
+                                                      uint32_t stackWords) {
     extern __shared__ uint32_t lds[];
+    const TraceTables Tt = traceTables<LDS>(S, lds, stackWords);
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     float depth = tmaxv[i], u = 0.0f, v = 0.0f;
     uint32_t inst = kUnset, prim = kUnset;
-    occ[i] = traceScene<true>(S, mk3(o[3 * i], o[3 * i + 1], o[3 * i + 2]), mk3(d[3 * i], d[3 * i + 1], d[3 * i + 2]),
+    occ[i] = traceScene<true>(S, Tt, mk3(o[3 * i], o[3 * i + 1], o[3 * i + 2]), mk3(d[3 * i], d[3 * i + 1], d[3 * i + 2]),
                               depth, u, v, inst, prim, lds + threadIdx.x, blockDim.x) ? 1 : 0;
 }
 

@@ -13,6 +13,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <cfloat>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -76,7 +77,7 @@ struct surf_ctx {
     uint32_t* dRows = nullptr;
     Counters* ctr = nullptr;
     Counters* hctr = nullptr;      /* pinned */
-    uint32_t* frameDone = nullptr; /* [window] */
+    uint32_t* frameDone = nullptr; /* [kStripes][window] completions per frame slot */
     uint32_t* hFrameDone = nullptr;/* pinned */
     uint32_t* dOutRGBA = nullptr;
     std::vector<void*> wfAllocs;
@@ -148,7 +149,14 @@ void destroyGraph(surf_ctx* c) {
     c->graph = nullptr;
 }
 
-size_t stackBytes(const surf_ctx* c) { return (size_t)c->stackDepth * kBlock * sizeof(uint32_t); }
+/* Dynamic LDS of a traversal kernel with `block` threads: the per-lane stack,
+ * then (LDS tables) the TraceInst table and the TLAS index array. */
+uint32_t stackWords(const surf_ctx* c, uint32_t block) { return c->stackDepth * block; }
+size_t traversalLds(const surf_ctx* c, uint32_t block) {
+    size_t b = (size_t)stackWords(c, block) * sizeof(uint32_t);
+    if (c->ldsTables) b += (size_t)c->nInstances * (sizeof(TraceInst) + sizeof(uint32_t));
+    return b;
+}
 
 /* ----------------------------------------------------------- scene upload
  * Walks every BLAS/TLAS from its root: validates indices (no kernel can
@@ -231,10 +239,10 @@ int allocWavefront(surf_ctx* c) {
     if ((rc = devAlloc(c, c->wfAllocs, &c->Q.c, cap))) return rc;
     if ((rc = devAlloc(c, c->wfAllocs, &c->rad, (size_t)c->npx * c->window))) return rc;
     if ((rc = devAlloc(c, c->wfAllocs, &c->ctr, 1))) return rc;
-    if ((rc = devAlloc(c, c->wfAllocs, &c->frameDone, c->window))) return rc;
+    if ((rc = devAlloc(c, c->wfAllocs, &c->frameDone, (size_t)kStripes * c->window))) return rc;
     if ((rc = devAlloc(c, c->wfAllocs, &c->dOutRGBA, c->npx))) return rc;
     if (hipHostMalloc((void**)&c->hctr, sizeof(Counters), hipHostMallocDefault) != hipSuccess ||
-        hipHostMalloc((void**)&c->hFrameDone, c->window * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess)
+        hipHostMalloc((void**)&c->hFrameDone, (size_t)kStripes * c->window * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess)
         return fail(c, SURF_ERR_OOM, "hipHostMalloc of the counter block failed");
     for (auto& e : c->pev) SURF_CHECK(c, hipEventCreate(&e));
     /* grid: 8 workgroups of 256 per CU saturate the 256-CU chip; grid-stride beyond */
@@ -253,19 +261,27 @@ StreamGeom geom(const surf_ctx* c) { return StreamGeom{c->dRows, c->width, c->np
 /* One wavefront phase: extend -> shade -> connect -> regen.  With ev != null,
  * an event is recorded before each kernel and after the last (profiling). */
 void launchPhase(surf_ctx* c, int par, hipEvent_t* ev) {
-    const size_t lds = stackBytes(c);
+    const size_t lds = traversalLds(c, kBlock);
+    const uint32_t sw = stackWords(c, kBlock);
     if (ev) (void)hipEventRecord(ev[0], c->stream);
-    hipLaunchKernelGGL(k_extend, dim3(c->gridWork), dim3(kBlock), lds, c->stream, c->S, c->pool[par], c->hitTUV, c->hitInst,
-                       (const Counters*)c->ctr, par);
+    if (c->ldsTables)
+        hipLaunchKernelGGL(k_extend<true>, dim3(c->gridWork), dim3(kBlock), lds, c->stream, c->S, c->pool[par], c->hitTUV,
+                           c->hitInst, (const Counters*)c->ctr, par, sw);
+    else
+        hipLaunchKernelGGL(k_extend<false>, dim3(c->gridWork), dim3(kBlock), lds, c->stream, c->S, c->pool[par], c->hitTUV,
+                           c->hitInst, (const Counters*)c->ctr, par, sw);
     if (ev) (void)hipEventRecord(ev[1], c->stream);
     if (c->ldsTables)
         hipLaunchKernelGGL(k_shade<true>, dim3(c->gridWork), dim3(kBlock), 0, c->stream, c->S, c->pool[par], c->pool[par ^ 1],
-                           c->hitTUV, (const uint32_t*)c->hitInst, c->Q, c->rad, c->frameDone, c->npx, c->ctr, par);
+                           c->hitTUV, (const uint32_t*)c->hitInst, c->Q, c->rad, c->frameDone, c->npx, c->window, c->ctr, par);
     else
         hipLaunchKernelGGL(k_shade<false>, dim3(c->gridWork), dim3(kBlock), 0, c->stream, c->S, c->pool[par], c->pool[par ^ 1],
-                           c->hitTUV, (const uint32_t*)c->hitInst, c->Q, c->rad, c->frameDone, c->npx, c->ctr, par);
+                           c->hitTUV, (const uint32_t*)c->hitInst, c->Q, c->rad, c->frameDone, c->npx, c->window, c->ctr, par);
     if (ev) (void)hipEventRecord(ev[2], c->stream);
-    hipLaunchKernelGGL(k_connect, dim3(c->gridWork), dim3(kBlock), lds, c->stream, c->S, c->Q, c->rad, c->ctr, par);
+    if (c->ldsTables)
+        hipLaunchKernelGGL(k_connect<true>, dim3(c->gridWork), dim3(kBlock), lds, c->stream, c->S, c->Q, c->rad, c->ctr, par, sw);
+    else
+        hipLaunchKernelGGL(k_connect<false>, dim3(c->gridWork), dim3(kBlock), lds, c->stream, c->S, c->Q, c->rad, c->ctr, par, sw);
     if (ev) (void)hipEventRecord(ev[3], c->stream);
     hipLaunchKernelGGL(k_regen, dim3(c->gridRegen), dim3(kBlock), 0, c->stream, c->cam, c->pool[par ^ 1], c->rad, c->ctr, par,
                        c->capacity, geom(c));
@@ -290,7 +306,7 @@ int startStream(surf_ctx* c, uint64_t baseFrame, uint32_t maxSeg) {
     h.baseFrame = baseFrame;
     *c->hctr = h;
     SURF_CHECK(c, hipMemcpyAsync(c->ctr, c->hctr, sizeof(Counters), hipMemcpyHostToDevice, c->stream));
-    SURF_CHECK(c, hipMemsetAsync(c->frameDone, 0, c->window * sizeof(uint32_t), c->stream));
+    SURF_CHECK(c, hipMemsetAsync(c->frameDone, 0, (size_t)kStripes * c->window * sizeof(uint32_t), c->stream));
     c->streamActive = true;
     c->baseFrame = baseFrame;
     c->targetFrames = 0;
@@ -313,25 +329,41 @@ int pushLimit(surf_ctx* c) {
     return SURF_OK;
 }
 
+/* Finished paths of a frame slot: sum over the completion stripes. */
+uint64_t framePaths(const surf_ctx* c, uint32_t slot) {
+    uint64_t n = 0;
+    for (uint32_t k = 0; k < kStripes; ++k) n += c->hFrameDone[(size_t)k * c->window + slot];
+    return n;
+}
+
+/* Event totals of the current stream: plain counters + the block stripes. */
+void streamEvents(const Counters& h, unsigned long long out[8]) {
+    for (int k = 0; k < 8; ++k) {
+        out[k] = h.ev[k];
+        for (uint32_t s = 0; s < kStripes; ++s) out[k] += h.evS[s][k];
+    }
+}
+
 /* Reads counters + per-frame completion (one sync) and accumulates, in frame
  * order, every leading frame whose samples have all finished. */
 int syncAndAccumulate(surf_ctx* c) {
     SURF_CHECK(c, hipMemcpyAsync(c->hctr, c->ctr, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
-    SURF_CHECK(c, hipMemcpyAsync(c->hFrameDone, c->frameDone, c->window * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+    SURF_CHECK(c, hipMemcpyAsync(c->hFrameDone, c->frameDone, (size_t)kStripes * c->window * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
     SURF_CHECK(c, hipStreamSynchronize(c->stream));
     /* a frame is complete when all its samples were issued and all finished; a
      * slot is reused only after its frame is accumulated, so frames beyond the
      * issued range must not be tested (their slot may still count an older frame) */
     uint64_t f = c->accFrames;
     const uint64_t issuedFrames = c->hctr->issued[0] / c->npx;
-    while (f < c->targetFrames && f < issuedFrames && c->hFrameDone[f % c->window] == c->npx) ++f;
+    while (f < c->targetFrames && f < issuedFrames && framePaths(c, f % c->window) == c->npx) ++f;
     if (f == c->accFrames) return SURF_OK;
     const uint32_t count = (uint32_t)(f - c->accFrames);
     hipLaunchKernelGGL(k_accumulate, dim3((c->npx + kBlock - 1) / kBlock), dim3(kBlock), 0, c->stream, (const float4*)c->rad,
                        c->acc, c->npx, (unsigned long long)c->accFrames, count, c->window);
     SURF_CHECK(c, hipGetLastError());
-    for (uint64_t g = c->accFrames; g < f; ++g) c->hFrameDone[g % c->window] = 0;
-    SURF_CHECK(c, hipMemcpyAsync(c->frameDone, c->hFrameDone, c->window * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+    for (uint64_t g = c->accFrames; g < f; ++g)
+        for (uint32_t k = 0; k < kStripes; ++k) c->hFrameDone[(size_t)k * c->window + g % c->window] = 0;
+    SURF_CHECK(c, hipMemcpyAsync(c->frameDone, c->hFrameDone, (size_t)kStripes * c->window * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
     c->accFrames = f;
     return pushLimit(c);
 }
@@ -367,13 +399,13 @@ int runTail(surf_ctx* c) {
                                       : std::min<uint32_t>(64u, std::max<uint32_t>(1u, (n + 4095u) / 4096u));
     const uint32_t blocks = (n + lpw - 1) / lpw;
     if (c->profiling) SURF_CHECK(c, hipEventRecord(c->pev[0], c->stream));
-    const size_t lds = (size_t)c->stackDepth * 64 * sizeof(uint32_t);
+    const size_t lds = traversalLds(c, 64);
     if (c->ldsTables)
         hipLaunchKernelGGL(k_tail<true>, dim3(blocks), dim3(64), lds, c->stream, c->S, c->pool[0], n, lpw, c->rad, c->frameDone,
-                           c->npx, c->ctr);
+                           c->npx, c->window, c->ctr, stackWords(c, 64));
     else
         hipLaunchKernelGGL(k_tail<false>, dim3(blocks), dim3(64), lds, c->stream, c->S, c->pool[0], n, lpw, c->rad, c->frameDone,
-                           c->npx, c->ctr);
+                           c->npx, c->window, c->ctr, stackWords(c, 64));
     SURF_CHECK(c, hipGetLastError());
     if (c->profiling) {
         SURF_CHECK(c, hipEventRecord(c->pev[1], c->stream));
@@ -440,7 +472,9 @@ int endStream(surf_ctx* c) {
     int rc = ensureDrained(c);
     if (rc) return rc;
     if (c->streamActive) {
-        for (int k = 0; k < 8; ++k) c->evBase[k] += c->hctr->ev[k];
+        unsigned long long e[8];
+        streamEvents(*c->hctr, e);
+        for (int k = 0; k < 8; ++k) c->evBase[k] += e[k];
         c->segMaxBase = std::max(c->segMaxBase, c->hctr->segMax);
     }
     c->streamActive = false;
@@ -687,6 +721,19 @@ int surf_upload_scene(surf_ctx* c, const surf_scene_desc* d) {
             return fail(c, SURF_ERR_INVALID, "light " + std::to_string(l) + " out of range");
         lights[l] = make_uint2(L.light_instance_idx, L.primitive_count);
     }
+    /* traversal records: M^-1 rows, offsets, BLAS root record (TraceInst) */
+    std::vector<TraceInst> tinst(d->instance_count);
+    for (uint32_t i = 0; i < d->instance_count; ++i) {
+        const float* m = inst[i].Minv;
+        TraceInst& T = tinst[i];
+        T.m0 = make_float4(m[0], m[4], m[8], m[12]);
+        T.m1 = make_float4(m[1], m[5], m[9], m[13]);
+        T.m2 = make_float4(m[2], m[6], m[10], m[14]);
+        T.m3 = make_float4(m[3], m[7], m[11], m[15]);
+        T.meta = make_uint4(inst[i].nodeOffset, inst[i].idxOffset, inst[i].affineInv, i);
+        const size_t r = 4 * (size_t)inst[i].nodeOffset;
+        T.r0 = nodes[r]; T.r1 = nodes[r + 1]; T.r2 = nodes[r + 2]; T.r3 = nodes[r + 3];
+    }
     std::vector<DevMaterial> mats(d->material_count);
     std::memcpy(mats.data(), d->materials, d->material_count * sizeof(DevMaterial));
 
@@ -702,11 +749,15 @@ int surf_upload_scene(surf_ctx* c, const surf_scene_desc* d) {
     if ((rc = upload(c, tnodes, &S.tlasNodes))) return rc;
     if ((rc = upload(c, tidx, &S.tlasIdx))) return rc;
     if ((rc = upload(c, inst, &S.inst))) return rc;
+    if ((rc = upload(c, tinst, &S.tinst))) return rc;
     if ((rc = upload(c, mats, &S.mats))) return rc;
     if ((rc = upload(c, lights, &S.lights))) return rc;
     S.nLights = d->light_count;
     S.nInst = d->instance_count;
     S.nMats = d->material_count;
+    S.finiteBoxes = 1u;
+    for (const float4& q : nodes)
+        if (!(std::fabs(q.x) <= FLT_MAX && std::fabs(q.y) <= FLT_MAX && std::fabs(q.z) <= FLT_MAX)) { S.finiteBoxes = 0u; break; }
     S.tlasLeafCount = d->tlas_nodes[0].count;   /* root leaf: wave-uniform instance loop */
     if (S.tlasLeafCount && d->tlas_nodes[0].left_first != 0) S.tlasLeafCount = 0;   /* general path unless indices start at 0 */
     const surf_background& bg = *d->background;
@@ -715,7 +766,8 @@ int surf_upload_scene(surf_ctx* c, const surf_scene_desc* d) {
     S.bgA[0] = bg.gradient_a.x; S.bgA[1] = bg.gradient_a.y; S.bgA[2] = bg.gradient_a.z;
     S.bgB[0] = bg.gradient_b.x; S.bgB[1] = bg.gradient_b.y; S.bgB[2] = bg.gradient_b.z;
     c->S = S;
-    c->ldsTables = d->instance_count <= kLdsInst && d->material_count <= kLdsMats && d->light_count <= kLdsLights;
+    c->ldsTables = d->instance_count <= kLdsInst && d->instance_count <= kLdsTraceInst && d->material_count <= kLdsMats &&
+                   d->light_count <= kLdsLights;
     c->stackDepth = depth;
     c->nInstances = d->instance_count;
     c->nTriangles = d->triangle_count;
@@ -842,7 +894,9 @@ int surf_get_stats(surf_ctx* c, surf_stats* out) {
     if (rc) return rc;
     surf_stats s = c->stats;
     unsigned long long ev[8];
-    for (int k = 0; k < 8; ++k) ev[k] = c->evBase[k] + ((c->streamActive && c->hctr) ? c->hctr->ev[k] : 0ull);
+    unsigned long long cur[8] = {};
+    if (c->streamActive && c->hctr) streamEvents(*c->hctr, cur);
+    for (int k = 0; k < 8; ++k) ev[k] = c->evBase[k] + cur[k];
     s.n_ext = ev[0]; s.n_hit = ev[1]; s.n_cont = ev[2]; s.n_shadow = ev[3]; s.n_acc = ev[4]; s.n_unocc = ev[5];
     s.tail_paths = ev[6];
     s.max_segments = std::max(c->segMaxBase, (c->streamActive && c->hctr) ? c->hctr->segMax : 0u);
@@ -883,8 +937,12 @@ int surf_trace_closest(surf_ctx* c, uint32_t n, const float* o, const float* d, 
         (rc = devAlloc(c, tmp, &dT, n)) || (rc = devAlloc(c, tmp, &dI, n))) { freeList(tmp); return rc; }
     (void)hipMemcpyAsync(dO, o, 12 * (size_t)n, hipMemcpyHostToDevice, c->stream);
     (void)hipMemcpyAsync(dD, d, 12 * (size_t)n, hipMemcpyHostToDevice, c->stream);
-    hipLaunchKernelGGL(k_trace_closest, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), stackBytes(c), c->stream, c->S,
-                       (const float*)dO, (const float*)dD, n, dT, dI);
+    if (c->ldsTables)
+        hipLaunchKernelGGL(k_trace_closest<true>, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), traversalLds(c, kBlock), c->stream,
+                           c->S, (const float*)dO, (const float*)dD, n, dT, dI, stackWords(c, kBlock));
+    else
+        hipLaunchKernelGGL(k_trace_closest<false>, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), traversalLds(c, kBlock), c->stream,
+                           c->S, (const float*)dO, (const float*)dD, n, dT, dI, stackWords(c, kBlock));
     std::vector<float4> t(n);
     std::vector<uint2> ip(n);
     (void)hipMemcpyAsync(t.data(), dT, 16 * (size_t)n, hipMemcpyDeviceToHost, c->stream);
@@ -909,8 +967,12 @@ int surf_trace_any(surf_ctx* c, uint32_t n, const float* o, const float* d, cons
     (void)hipMemcpyAsync(dO, o, 12 * (size_t)n, hipMemcpyHostToDevice, c->stream);
     (void)hipMemcpyAsync(dD, d, 12 * (size_t)n, hipMemcpyHostToDevice, c->stream);
     (void)hipMemcpyAsync(dM, tm, 4 * (size_t)n, hipMemcpyHostToDevice, c->stream);
-    hipLaunchKernelGGL(k_trace_any, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), stackBytes(c), c->stream, c->S,
-                       (const float*)dO, (const float*)dD, (const float*)dM, n, dR);
+    if (c->ldsTables)
+        hipLaunchKernelGGL(k_trace_any<true>, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), traversalLds(c, kBlock), c->stream,
+                           c->S, (const float*)dO, (const float*)dD, (const float*)dM, n, dR, stackWords(c, kBlock));
+    else
+        hipLaunchKernelGGL(k_trace_any<false>, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), traversalLds(c, kBlock), c->stream,
+                           c->S, (const float*)dO, (const float*)dD, (const float*)dM, n, dR, stackWords(c, kBlock));
     (void)hipMemcpyAsync(occ, dR, n, hipMemcpyDeviceToHost, c->stream);
     hipError_t e = hipStreamSynchronize(c->stream);
     freeList(tmp);

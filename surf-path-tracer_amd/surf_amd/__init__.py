@@ -84,9 +84,10 @@ def load() -> C.CDLL:
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.exists(LIB_PATH):
-        raise FileNotFoundError(f"{LIB_PATH} not built: run `make -C surf-path-tracer_amd` or __graft_entry__.build()")
-    lib = C.CDLL(LIB_PATH)
+    path = os.environ.get("SURF_HIP_LIB", LIB_PATH)   # tuning builds (make variants); still the HIP library
+    if not os.path.exists(path):
+        raise FileNotFoundError(f"{path} not built: run `make -C surf-path-tracer_amd` or __graft_entry__.build()")
+    lib = C.CDLL(path)
     P, U32, I32, F = C.c_void_p, C.c_uint32, C.c_int, C.c_float
     sig = {
         "surf_abi_version": ([], I32), "surf_device_count": ([C.POINTER(I32)], I32),
