@@ -127,6 +127,7 @@ typedef struct {
     uint32_t pool_capacity;    /* paths in flight */
     float    energy;           /* sum of acc.rgb / samples over the shard ("Lumen", renderer.cpp:191-201) */
     uint32_t max_segments;     /* longest path seen (extension rays), diagnostics */
+    uint64_t tail_survivors;   /* drain paths still alive after the tail's first stage */
 } surf_stats;
 
 typedef struct surf_ctx surf_ctx;       /* one per HIP device */
@@ -167,9 +168,12 @@ int surf_set_frame_batch(surf_ctx* ctx, uint32_t frames);
  * traces for up to millions of segments. */
 int surf_set_zero_cutoff(surf_ctx* ctx, int enabled);
 /* Drain policy: when no new sample may be issued and at most `threshold_paths`
- * paths are in flight, one k_tail launch finishes them, `lanes_per_wave`
- * paths per 64-lane wave (0 = automatic for either). */
-int surf_set_tail_policy(surf_ctx* ctx, uint32_t threshold_paths, uint32_t lanes_per_wave);
+ * paths are in flight, the tail kernel finishes them: stage 1 runs
+ * `lanes_per_wave` paths per 64-lane wave for up to `stage_segments` segments
+ * each (0 = automatic for the first two; stage_segments 0 = no second stage),
+ * stage 2 runs the survivors one per wave.  Results do not depend on the
+ * policy.  Drains the context first. */
+int surf_set_tail_policy(surf_ctx* ctx, uint32_t threshold_paths, uint32_t lanes_per_wave, uint32_t stage_segments);
 /* Diagnostics: how many paths the segment cap ended in the current sample
  * stream, and the sample ids (frame slot * shard pixels + pixel) of the first
  * min(count, 64, max). */

@@ -107,6 +107,8 @@ struct Counters {
     uint32_t maxSeg;                 /* 0 = unbounded */
     uint32_t zeroCutoff;             /* end paths whose throughput is exactly 0 (radiance-neutral) */
     uint32_t segMax;                 /* longest finished path (extension rays), diagnostics */
+    uint32_t survN;                  /* k_tail survivors appended (may exceed survCap) */
+    uint32_t survCap;
     uint32_t _pad;
     unsigned long long issued[2];    /* stream samples issued, per parity */
     unsigned long long limit;        /* host-written issue limit (frame window) */
@@ -767,13 +769,18 @@ __global__ __launch_bounds__(kBlock) void k_regen(DevCamera cam, Pool nxt, float
 }
 
 /* Finishes the last paths of the stream: one kernel, each active lane runs its
- * path to termination (extend -> shade -> connect per segment), so the long
- * Russian-roulette tail pays no per-bounce launch.  Same device functions as
- * the wavefront kernels: identical results.  lanes < lpw of each wave work. */
+ * path (extend -> shade -> connect per segment), so the long Russian-roulette
+ * tail pays no per-bounce launch.  Same device functions as the wavefront
+ * kernels: identical results.  lanes < lpw of each wave work.
+ * Two stages (runTail): pool 0 with a segment budget -- a path still alive
+ * after `budget` segments is appended to `surv` instead of holding its wave --
+ * then the survivors (lens TIR orbits run thousands of segments) one per wave,
+ * so no long path shares a wave.  firstCounted: the first extension ray of
+ * each input path is already in the event counts (regen counted it). */
 template <bool LDS_TABLES>
 __global__ __launch_bounds__(64) void k_tail(DevScene S, Pool cur, uint32_t n, uint32_t lpw, float4* __restrict__ rad,
                                              uint32_t* __restrict__ frameDone, uint32_t npx, uint32_t window, Counters* C,
-                                             uint32_t stackWords) {
+                                             uint32_t stackWords, uint32_t firstCounted, uint32_t budget, Pool surv) {
     extern __shared__ uint32_t lds[];
     const TraceTables Tt = traceTables<LDS_TABLES>(S, lds, stackWords);
     __shared__ DevInstance sInst[LDS_TABLES ? kLdsInst : 1];
@@ -793,6 +800,7 @@ __global__ __launch_bounds__(64) void k_tail(DevScene S, Pool cur, uint32_t n, u
     float4 o4 = cur.o[i], d4 = cur.d[i], T4 = cur.T[i];
     const uint32_t slot = f2u(o4.w) / npx;
     unsigned long long nExt = 0, nHit = 0, nCont = 0, nSh = 0, nAcc = 0, nUn = 0;
+    bool done = true;
     for (;;) {
         float depth = kFarAway, u = 0.0f, v = 0.0f;
         uint32_t inst = kUnset, prim = kUnset;
@@ -816,21 +824,35 @@ __global__ __launch_bounds__(64) void k_tail(DevScene S, Pool cur, uint32_t n, u
         }
         if (!r.cont) { atomicMax(&C->segMax, r.seg); break; }
         ++nCont;
+        if (budget != 0u && nExt >= budget) {
+            /* survivor: hand the continuation to the one-path-per-wave stage */
+            const uint32_t k = atomicAdd(&C->survN, 1u);
+            if (k < C->survCap) {
+                surv.o[k] = r.o; surv.d[k] = r.d; surv.T[k] = r.T;
+                done = false;
+                break;
+            }
+        }
         o4 = r.o; d4 = r.d; T4 = r.T;
     }
     const uint32_t st = blockIdx.x % kStripes;
     unsigned long long* ev = C->evS[st];
-    atomicAdd(&frameDone[st * window + slot], 1u);
-    atomicAdd(&ev[0], nExt - 1ull); atomicAdd(&ev[1], nHit); atomicAdd(&ev[2], nCont);
+    if (done) atomicAdd(&frameDone[st * window + slot], 1u);
+    atomicAdd(&ev[0], nExt - (unsigned long long)firstCounted); atomicAdd(&ev[1], nHit); atomicAdd(&ev[2], nCont);
     atomicAdd(&ev[3], nSh); atomicAdd(&ev[4], nAcc); atomicAdd(&ev[5], nUn);
-    atomicAdd(&ev[6], 1ull);
+    if (done) atomicAdd(&ev[6], 1ull);
 }
 
 /* acc[p] += (radiance, 1) for frames [f0, f0+count) of the stream, in frame
  * order (renderer.cpp:180); frame f's radiance lives in slot f % window. */
 __global__ __launch_bounds__(kBlock) void k_accumulate(const float4* __restrict__ rad, float4* __restrict__ acc,
-                                                       uint32_t npx, unsigned long long f0, uint32_t count, uint32_t window) {
+                                                       uint32_t npx, unsigned long long f0, uint32_t count, uint32_t window,
+                                                       uint32_t* __restrict__ frameDone) {
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    /* the accumulated frames' slots are free again: reset their completion
+     * stripes here, on the render stream (the escape worker may be updating
+     * other slots concurrently, so the host never rewrites the whole array) */
+    if (p < count * kStripes) frameDone[(p % kStripes) * window + (uint32_t)((f0 + p / kStripes) % window)] = 0u;
     if (p >= npx) return;
     float4 a = acc[p];
     for (uint32_t k = 0; k < count; ++k) {

@@ -92,6 +92,9 @@ struct surf_ctx {
     bool zeroCutoff = true;        /* radiance-neutral early end of T == 0 paths */
     uint64_t pushedLimit = 0;
     uint32_t tailPaths = 0;        /* drain policy (surf_set_tail_policy), 0 = automatic */
+    uint32_t tailBudget = 0;       /* stage-1 segment budget of the drain tail (0 = one stage) */
+    Pool surv{};                   /* drain survivors (stage 2 input) */
+    uint32_t survCap = 0;
     uint32_t tailLanes = 0;
     uint32_t segMaxBase = 0;       /* longest path of finished streams */
 
@@ -232,6 +235,10 @@ int allocWavefront(surf_ctx* c) {
         if ((rc = devAlloc(c, c->wfAllocs, &c->pool[p].d, cap))) return rc;
         if ((rc = devAlloc(c, c->wfAllocs, &c->pool[p].T, cap))) return rc;
     }
+    c->survCap = (uint32_t)std::min<size_t>(std::max<size_t>(cap / 16, 4096), 1u << 18);
+    if ((rc = devAlloc(c, c->wfAllocs, &c->surv.o, c->survCap))) return rc;
+    if ((rc = devAlloc(c, c->wfAllocs, &c->surv.d, c->survCap))) return rc;
+    if ((rc = devAlloc(c, c->wfAllocs, &c->surv.T, c->survCap))) return rc;
     if ((rc = devAlloc(c, c->wfAllocs, &c->hitTUV, cap))) return rc;
     if ((rc = devAlloc(c, c->wfAllocs, &c->hitInst, cap))) return rc;
     if ((rc = devAlloc(c, c->wfAllocs, &c->Q.o, cap))) return rc;
@@ -304,6 +311,7 @@ int startStream(surf_ctx* c, uint64_t baseFrame, uint32_t maxSeg) {
     h.maxSeg = maxSeg;
     h.zeroCutoff = c->zeroCutoff ? 1u : 0u;
     h.baseFrame = baseFrame;
+    h.survCap = c->survCap;
     *c->hctr = h;
     SURF_CHECK(c, hipMemcpyAsync(c->ctr, c->hctr, sizeof(Counters), hipMemcpyHostToDevice, c->stream));
     SURF_CHECK(c, hipMemsetAsync(c->frameDone, 0, (size_t)kStripes * c->window * sizeof(uint32_t), c->stream));
@@ -358,12 +366,10 @@ int syncAndAccumulate(surf_ctx* c) {
     while (f < c->targetFrames && f < issuedFrames && framePaths(c, f % c->window) == c->npx) ++f;
     if (f == c->accFrames) return SURF_OK;
     const uint32_t count = (uint32_t)(f - c->accFrames);
-    hipLaunchKernelGGL(k_accumulate, dim3((c->npx + kBlock - 1) / kBlock), dim3(kBlock), 0, c->stream, (const float4*)c->rad,
-                       c->acc, c->npx, (unsigned long long)c->accFrames, count, c->window);
+    const uint32_t threads = std::max<uint32_t>(c->npx, count * kStripes);
+    hipLaunchKernelGGL(k_accumulate, dim3((threads + kBlock - 1) / kBlock), dim3(kBlock), 0, c->stream, (const float4*)c->rad,
+                       c->acc, c->npx, (unsigned long long)c->accFrames, count, c->window, c->frameDone);
     SURF_CHECK(c, hipGetLastError());
-    for (uint64_t g = c->accFrames; g < f; ++g)
-        for (uint32_t k = 0; k < kStripes; ++k) c->hFrameDone[(size_t)k * c->window + g % c->window] = 0;
-    SURF_CHECK(c, hipMemcpyAsync(c->frameDone, c->hFrameDone, (size_t)kStripes * c->window * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
     c->accFrames = f;
     return pushLimit(c);
 }
@@ -392,31 +398,50 @@ int advance(surf_ctx* c) {
 
 /* Finishes every path of pool 0 in one k_tail launch (counters at an even
  * phase boundary: pool 0 is the next to be extended, nothing else pending). */
+void launchTail(surf_ctx* c, Pool in, uint32_t n, uint32_t lpw, uint32_t firstCounted, uint32_t budget) {
+    const uint32_t blocks = (n + lpw - 1) / lpw;
+    const size_t lds = traversalLds(c, 64);
+    if (c->ldsTables)
+        hipLaunchKernelGGL(k_tail<true>, dim3(blocks), dim3(64), lds, c->stream, c->S, in, n, lpw, c->rad, c->frameDone,
+                           c->npx, c->window, c->ctr, stackWords(c, 64), firstCounted, budget, c->surv);
+    else
+        hipLaunchKernelGGL(k_tail<false>, dim3(blocks), dim3(64), lds, c->stream, c->S, in, n, lpw, c->rad, c->frameDone,
+                           c->npx, c->window, c->ctr, stackWords(c, 64), firstCounted, budget, c->surv);
+}
+
+/* Finishes every path of pool 0 (counters at an even phase boundary: pool 0 is
+ * the next to be extended, nothing else pending).  Stage 1 runs each path up
+ * to tailBudget segments, many paths per wave; the few still alive (lens TIR
+ * orbits: thousands of segments) go to stage 2, one path per wave, so a long
+ * path never drags a wave of finished lanes and never shares one. */
 int runTail(surf_ctx* c) {
     const uint32_t n = c->hctr->nIn[0];
     if (n == 0) return SURF_OK;
     const uint32_t lpw = c->tailLanes ? std::min<uint32_t>(64u, c->tailLanes)
                                       : std::min<uint32_t>(64u, std::max<uint32_t>(1u, (n + 4095u) / 4096u));
-    const uint32_t blocks = (n + lpw - 1) / lpw;
     if (c->profiling) SURF_CHECK(c, hipEventRecord(c->pev[0], c->stream));
-    const size_t lds = traversalLds(c, 64);
-    if (c->ldsTables)
-        hipLaunchKernelGGL(k_tail<true>, dim3(blocks), dim3(64), lds, c->stream, c->S, c->pool[0], n, lpw, c->rad, c->frameDone,
-                           c->npx, c->window, c->ctr, stackWords(c, 64));
-    else
-        hipLaunchKernelGGL(k_tail<false>, dim3(blocks), dim3(64), lds, c->stream, c->S, c->pool[0], n, lpw, c->rad, c->frameDone,
-                           c->npx, c->window, c->ctr, stackWords(c, 64));
+    c->hctr->survN = 0;
+    SURF_CHECK(c, hipMemcpyAsync(&c->ctr->survN, &c->hctr->survN, sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+    launchTail(c, c->pool[0], n, lpw, 1u, c->tailBudget);
     SURF_CHECK(c, hipGetLastError());
+    SURF_CHECK(c, hipMemcpyAsync(&c->hctr->survN, &c->ctr->survN, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+    SURF_CHECK(c, hipStreamSynchronize(c->stream));
+    const uint32_t m = std::min(c->hctr->survN, c->survCap);
+    if (m) {
+        const uint32_t lpw2 = std::min<uint32_t>(64u, std::max<uint32_t>(1u, (m + 2047u) / 2048u));
+        launchTail(c, c->surv, m, lpw2, 0u, 0u);
+        SURF_CHECK(c, hipGetLastError());
+    }
     if (c->profiling) {
         SURF_CHECK(c, hipEventRecord(c->pev[1], c->stream));
         SURF_CHECK(c, hipEventSynchronize(c->pev[1]));
         float t; (void)hipEventElapsedTime(&t, c->pev[0], c->pev[1]);
         c->stats.ms_tail += t;
     }
+    c->stats.tail_survivors += m;
     /* pool 0 is now empty: the next phase starts from regen's refill */
-    const uint32_t zero = 0;
     c->hctr->nIn[0] = 0;
-    SURF_CHECK(c, hipMemcpyAsync(&c->ctr->nIn[0], &zero, sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+    SURF_CHECK(c, hipMemcpyAsync(&c->ctr->nIn[0], &c->hctr->nIn[0], sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
     SURF_CHECK(c, hipStreamSynchronize(c->stream));
     return SURF_OK;
 }
@@ -611,11 +636,15 @@ int surf_debug_capped(surf_ctx* c, uint32_t* sids, uint32_t max, uint64_t* count
     return SURF_OK;
 }
 
-int surf_set_tail_policy(surf_ctx* c, uint32_t threshold_paths, uint32_t lanes_per_wave) {
+int surf_set_tail_policy(surf_ctx* c, uint32_t threshold_paths, uint32_t lanes_per_wave, uint32_t stage_segments) {
     if (!c) return fail(nullptr, SURF_ERR_INVALID, "ctx is NULL");
     if (lanes_per_wave > 64) return fail(c, SURF_ERR_INVALID, "lanes_per_wave must be <= 64");
+    SURF_CHECK(c, hipSetDevice(c->device));
+    const int rc = endStream(c);
+    if (rc) return rc;
     c->tailPaths = threshold_paths;
     c->tailLanes = lanes_per_wave;
+    c->tailBudget = stage_segments;
     return SURF_OK;
 }
 

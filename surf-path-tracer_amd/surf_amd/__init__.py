@@ -63,7 +63,7 @@ class Stats(C.Structure):
         ("ms_regen", C.c_double), ("ms_tail", C.c_double), ("ms_accum", C.c_double),
         ("launches_extend", C.c_uint64),
         ("stack_depth", C.c_uint32), ("pool_capacity", C.c_uint32),
-        ("energy", C.c_float), ("max_segments", C.c_uint32),
+        ("energy", C.c_float), ("max_segments", C.c_uint32), ("tail_survivors", C.c_uint64),
     ]
 
     def as_dict(self) -> dict:
@@ -96,7 +96,7 @@ def load() -> C.CDLL:
         "surf_destroy": ([P], None), "surf_last_error": ([P], C.c_char_p),
         "surf_shard_rows": ([P, P, C.POINTER(U32)], I32),
         "surf_set_pool_capacity": ([P, U32], I32), "surf_set_frame_batch": ([P, U32], I32),
-        "surf_set_profiling": ([P, I32], I32), "surf_set_zero_cutoff": ([P, I32], I32), "surf_set_tail_policy": ([P, U32, U32], I32),
+        "surf_set_profiling": ([P, I32], I32), "surf_set_zero_cutoff": ([P, I32], I32), "surf_set_tail_policy": ([P, U32, U32, U32], I32),
         "surf_debug_capped": ([P, P, U32, C.POINTER(C.c_uint64)], I32),
         "surf_upload_scene": ([P, C.POINTER(SceneDesc)], I32),
         "surf_set_camera": ([P, P], I32),
@@ -259,9 +259,11 @@ class Renderer:
     def set_zero_cutoff(self, on: bool):
         _check(load().surf_set_zero_cutoff(self._h, 1 if on else 0), "surf_set_zero_cutoff", self._h)
 
-    def set_tail_policy(self, threshold_paths: int = 0, lanes_per_wave: int = 0):
-        """Drain policy of the tail kernel (0 = automatic)."""
-        _check(load().surf_set_tail_policy(self._h, threshold_paths, lanes_per_wave), "surf_set_tail_policy", self._h)
+    def set_tail_policy(self, threshold_paths: int = 0, lanes_per_wave: int = 0, stage_segments: int = 0):
+        """Drain policy of the tail kernel (0 = automatic); stage_segments is the
+        first stage's per-path budget before survivors run one per wave (0 = one stage)."""
+        _check(load().surf_set_tail_policy(self._h, threshold_paths, lanes_per_wave, stage_segments), "surf_set_tail_policy",
+               self._h)
 
     def set_profiling(self, on: bool):
         _check(load().surf_set_profiling(self._h, 1 if on else 0), "surf_set_profiling", self._h)
