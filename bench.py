@@ -31,6 +31,9 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 # Algorithmic HBM bytes per extension ray of k_extend (DESIGN.md "Roofline"):
 # read ray o (16 B) + d (16 B), write hit (t,u,v,prim 16 B + inst 4 B).
 EXTEND_BYTES_PER_RAY = 52
+# rocprofv3 PMC summary of this bench command (tools/profile_round.sh + tools/summarize_profile.py):
+# HBM bytes per k_extend launch, FETCH_SIZE x2 + WRITE_SIZE (MI355X_MICROARCH.md, HBM/rocprofv3 section).
+PMC_SUMMARY = os.path.join(REPO, "profiles", "r1_final", "summary.json")
 
 
 def parse():
@@ -46,7 +49,8 @@ def parse():
     ap.add_argument("--cpu-frames", type=int, default=48, help="frames of the CPU baseline sample (full frame)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--profile-pass", type=int, default=2, help="steps re-run with per-kernel HIP events (roofline)")
+    ap.add_argument("--profile-pass", type=int, default=-1,
+                    help="steps re-run with per-kernel HIP events for the roofline (-1 = --steps, same composition as the timed run)")
     return ap.parse_args()
 
 
@@ -134,6 +138,8 @@ def main():
     # ---- roofline of the dominant kernel (k_extend), HIP events on the render stream ----
     roof = None
     kernel_ms = None
+    if args.profile_pass < 0:
+        args.profile_pass = args.steps
     if args.profile_pass > 0:
         r.set_profiling(True)
         r.clear_accumulator()
@@ -145,11 +151,18 @@ def main():
         bytes_per_launch = EXTEND_BYTES_PER_RAY * pe["n_ext"] / launches
         avg_ms = pe["ms_extend"] / launches
         achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
+        traffic, traffic_src = None, None
+        if os.path.exists(PMC_SUMMARY):
+            pmc = json.load(open(PMC_SUMMARY)).get("k_extend_pmc", {})
+            traffic = pmc.get("hbm_bytes_per_launch_corrected")
+            traffic_src = os.path.relpath(PMC_SUMMARY, REPO)
         roof = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
+                "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": round(traffic) if traffic else None,
+                "traffic_source": traffic_src,
                 "kernel": "k_extend", "avg_launch_ms": round(avg_ms, 5), "launches": int(pe["launches_extend"]),
                 "algorithmic_bytes_per_launch": round(bytes_per_launch, 1)}
         kernel_ms = {k: round(pe[k], 3) for k in ("ms_extend", "ms_shade", "ms_connect", "ms_regen", "ms_tail", "ms_total")}
+        kernel_ms["steps"] = args.profile_pass
         kernel_ms["tail_paths"] = int(pe["tail_paths"])
         if dist_on:
             t = torch.tensor([achieved], dtype=torch.float64, device=dev)

@@ -52,6 +52,7 @@ def load():
         "orc_trace_any": ([P, U32, P, P, P, P], None),
         "orc_trace_brute": ([P, U32, P, P, P, P, P], None),
         "orc_trace_visits": ([P, U32, P, P, P, P], None),
+        "orc_path_lengths": ([P, U32, U32, U32, P], None),
         "orc_record_rays": ([P, U32, U32, U32, U32, U32, U32, P, P, P, U32, P, P, P, P], None),
         "orc_bvh_depths": ([P, C.POINTER(U32), C.POINTER(U32)], None),
         "orc_init_seed": ([U32], U32), "orc_random_u32": ([C.POINTER(U32)], U32),
@@ -150,6 +151,12 @@ class OracleScene:
         nodes, tris = np.zeros((len(o), ni), np.uint32), np.zeros((len(o), ni), np.uint32)
         load().orc_trace_visits(self._h, len(o), _p(o), _p(d), _p(nodes), _p(tris))
         return nodes, tris
+
+    def path_lengths(self, width, height, frame):
+        """Extension rays per pixel path of one frame (diagnostics)."""
+        out = np.zeros(width * height, np.uint32)
+        load().orc_path_lengths(self._h, width, height, frame, _p(out))
+        return out.reshape(height, width)
 
     def record_rays(self, width, height, frame, pix_begin, pix_end, max_ext=1 << 20, max_shadow=1 << 20):
         eo, ed = np.zeros((max_ext, 3), np.float32), np.zeros((max_ext, 3), np.float32)

@@ -947,6 +947,26 @@ double orc_render(orc_scene* h, uint32_t W, uint32_t H, uint32_t r0, uint32_t r1
     return std::chrono::duration<double>(t1 - t0).count();
 }
 
+void orc_path_lengths(orc_scene* h, uint32_t W, uint32_t H, uint32_t frame, uint32_t* out) {
+    Scene& S = *h->s;
+    if (S.scrW != (float)W || S.scrH != (float)H) setCamera(S, W, H);
+    #pragma omp parallel for schedule(dynamic)
+    for (int64_t y = 0; y < (int64_t)H; ++y) {
+        Counters C; uint32_t sm = 0;
+        for (uint32_t x = 0; x < W; ++x) {
+            const uint64_t p = (uint64_t)x + (uint64_t)y * W;
+            uint32_t seed = seedOf((uint32_t)(p + (uint64_t)frame * 1799u));
+            float jy = rndRange(seed, -0.5f, 0.5f);
+            float jx = rndRange(seed, -0.5f, 0.5f);
+            V3 o, d;
+            primaryRay(S, seed, (float)x + jx, (float)y + jy, o, d);
+            const uint64_t e0 = C.ext;
+            trace(S, seed, o, d, 0, C, nullptr, sm);
+            out[p] = (uint32_t)(C.ext - e0);
+        }
+    }
+}
+
 void orc_trace_closest(const orc_scene* h, uint32_t n, const float* o, const float* d,
                        float* ot, float* ou, float* ov, uint32_t* oi, uint32_t* op) {
     const Scene& S = *h->s;

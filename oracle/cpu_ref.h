@@ -94,6 +94,9 @@ void orc_record_rays(orc_scene*, uint32_t width, uint32_t height, uint32_t frame
                      uint32_t max_shadow, float* sh_o, float* sh_d, float* sh_tmax,
                      uint32_t* n_shadow);
 
+/* Extension rays of every pixel's path of one whole frame (W x H, row-major). Diagnostics. */
+void orc_path_lengths(orc_scene*, uint32_t width, uint32_t height, uint32_t frame, uint32_t* out);
+
 /* Deepest root-to-leaf edge count of the TLAS and of every BLAS. */
 void orc_bvh_depths(const orc_scene*, uint32_t* tlas_depth, uint32_t* max_blas_depth);
 

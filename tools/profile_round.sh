@@ -12,7 +12,7 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
     python3 bench.py --steps "$STEPS" --warmup 1 --no-cpu > "$OUT/bench_traced.json" 2> "$OUT/trace.err"
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- \
-    python3 bench.py --steps 2 --warmup 0 --no-cpu --profile-pass 0 > "$OUT/bench_fetch.json" 2> "$OUT/fetch.err"
+    python3 bench.py --steps "$STEPS" --warmup 1 --no-cpu --profile-pass 0 > "$OUT/bench_fetch.json" 2> "$OUT/fetch.err"
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- \
-    python3 bench.py --steps 2 --warmup 0 --no-cpu --profile-pass 0 > "$OUT/bench_write.json" 2> "$OUT/write.err"
+    python3 bench.py --steps "$STEPS" --warmup 1 --no-cpu --profile-pass 0 > "$OUT/bench_write.json" 2> "$OUT/write.err"
 echo done

@@ -26,9 +26,12 @@ def kernel_stats(path):
 
 
 def counter(path, kernel, name):
-    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
-            if short(r["Kernel_Name"]) == kernel and r["Counter_Name"] == name]
-    return vals
+    """Per-dispatch values of one counter for kernels whose short name starts with `kernel`."""
+    per = {}
+    for r in csv.DictReader(open(path)):
+        if short(r["Kernel_Name"]).startswith(kernel) and r["Counter_Name"] == name:
+            per[r["Dispatch_Id"]] = per.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
+    return list(per.values())
 
 
 def main():
@@ -38,7 +41,8 @@ def main():
     write = counter(f"{d}/write/run_counter_collection.csv", "k_extend", "WRITE_SIZE")
     bench = json.loads(open(f"{d}/bench_traced.json").read().strip().splitlines()[-1])
     res = {
-        "command": "python3 bench.py --steps 16 --warmup 1 --no-cpu  (under rocprofv3 --kernel-trace --stats)",
+        "command": "python3 bench.py --steps 16 --warmup 1 --no-cpu  (under rocprofv3 --kernel-trace --stats); "
+                   "PMC passes: same command with --profile-pass 0, one counter per pass",
         "kernels": ks,
         "bench_value_traced": bench["value"],
         "k_extend_pmc": {
