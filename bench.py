@@ -96,16 +96,16 @@ def main():
     r = surf_amd.Renderer(scene, W, H, device=local, shard=spec)
     rows = len(r.rows)
     acc_dev = torch.empty((rows, W, 4), dtype=torch.float32, device=dev)
-    max_rows = -(-H // (world * args.row_block)) * args.row_block if world > 1 else H
-    gather_buf = [torch.empty((max_rows, W, 4), dtype=torch.float32, device=dev) for _ in range(world)] if (dist_on and rank == 0) else None
-    send_buf = torch.zeros((max_rows, W, 4), dtype=torch.float32, device=dev) if dist_on else None
+    gather = None
+    if dist_on:
+        from surf_amd.dist import RowGather
+        gather = RowGather(W, H, world, rank, args.row_block, dev)
 
     def step(i):
         r.render(F, i * F, args.max_segments)
         if dist_on:                       # one RCCL gather of the accumulator per step
             r.copy_accumulator_to(acc_dev.data_ptr())
-            send_buf[:rows].copy_(acc_dev)
-            dist.gather(send_buf, gather_buf, dst=0)
+            gather.gather(acc_dev)
 
     for w in range(args.warmup):
         step(w)

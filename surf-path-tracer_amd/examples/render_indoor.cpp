@@ -1,0 +1,104 @@
+/*
+ * render_indoor.cpp -- headless equivalent of the reference's main.cpp GPU loop
+ * (sources/main.cpp:141-149 camera, :161-346 scene, :360-442 render loop),
+ * written against the drop-in C++ API (include/surf/surf_host.hpp): the scene,
+ * BVHs, camera and WaveFrontRenderer are built exactly as the reference's
+ * application builds them, with RenderContext holding a HIP device instead of
+ * a Vulkan context and no UIManager.
+ *
+ * usage: render_indoor ASSETS_DIR WIDTH HEIGHT FRAMES OUT.ppm
+ * Prints the reference's per-frame line (ms, Mrays/s, samples, Lumen) and
+ * writes the image as the reference presents it: acc / samples, then sqrt
+ * (fs_quad.frag:12-13, gamma 2), 8 bits per channel.
+ */
+#include "surf/surf_host.hpp"
+
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <memory>
+#include <string>
+#include <vector>
+
+using namespace surf;
+
+int main(int argc, char** argv) {
+    if (argc < 6) {
+        std::fprintf(stderr, "usage: %s ASSETS_DIR WIDTH HEIGHT FRAMES OUT.ppm\n", argv[0]);
+        return 2;
+    }
+    const std::string dir = argv[1];
+    const U32 W = (U32)std::atoi(argv[2]), H = (U32)std::atoi(argv[3]), frames = (U32)std::atoi(argv[4]);
+    try {
+        RenderContext context;            /* HIP device 0 */
+        Camera worldCam(Float3(0.0f, 0.0f, -7.0f), Float3(0.0f, 0.0f, 0.0f), W, H, 70.0f, 7.0f, 0.5f);
+
+        /* main.cpp:161-346 */
+        Mesh susanneMesh(dir + "/susanne.obj"), cubeMesh(dir + "/cube.obj"), lensMesh(dir + "/lens.obj"), planeMesh(dir + "/plane.obj");
+        BvhBLAS susanneBlas(&susanneMesh), cubeBlas(&cubeMesh), lensBlas(&lensMesh), planeBlas(&planeMesh);
+
+        Material floorMat; floorMat.albedo = Float3(0.8f); floorMat.reflectivity = 0.01f;
+        Material wallRed; wallRed.albedo = Float3(1.0f, 0.0f, 0.0f);
+        Material wallGreen; wallGreen.albedo = Float3(0.0f, 1.0f, 0.0f);
+        Material diffuseMat; diffuseMat.albedo = Float3(1.0f, 0.0f, 0.0f);
+        Material dielectricMat; dielectricMat.albedo = Float3(0.7f, 0.7f, 0.2f); dielectricMat.absorption = Float3(0.03f, 0.04f, 0.03f);
+        dielectricMat.refractivity = 1.0f; dielectricMat.indexOfRefraction = 1.42f;
+        Material specularMat; specularMat.albedo = Float3(0.2f, 0.9f, 1.0f); specularMat.reflectivity = 0.8f;
+        Material softLight; softLight.emissionColor = Float3(1.0f, 0.8f, 0.6f); softLight.emissionStrength = 5.0f;
+        Material redLight; redLight.emissionColor = Float3(1.0f, 0.5f, 0.2f); redLight.emissionStrength = 5.0f;
+
+        const Mat4 I(1.0f);
+        std::vector<Instance> instances;
+        instances.emplace_back(&planeBlas, &floorMat, scale(translate(I, Float3(0.0f, -1.0f, 0.0f)), Float3(10.0f, 10.0f, 10.0f)));
+        instances.emplace_back(&cubeBlas, &softLight, scale(translate(I, Float3(-8.0f, 7.0f, 5.0f)), Float3(0.5f, 0.5f, 0.5f)));
+        instances.emplace_back(&cubeBlas, &redLight, scale(translate(I, Float3(9.0f, 5.0f, -5.0f)), Float3(1.0f, 1.0f, 1.0f)));
+        instances.emplace_back(&susanneBlas, &diffuseMat, translate(I, Float3(0.0f, 0.0f, -1.0f)));
+        instances.emplace_back(&susanneBlas, &specularMat, translate(I, Float3(3.0f, 0.0f, -1.0f)));
+        instances.emplace_back(&lensBlas, &dielectricMat, translate(I, Float3(-3.0f, 0.0f, -1.0f)));
+        instances.emplace_back(&planeBlas, &wallRed, scale(rotate(translate(I, Float3(-10.0f, 4.0f, 0.0f)), radians(90.0f), WORLD_FORWARD), Float3(5.0f, 10.0f, 10.0f)));
+        instances.emplace_back(&planeBlas, &wallGreen, scale(rotate(translate(I, Float3(10.0f, 4.0f, 0.0f)), radians(90.0f), WORLD_FORWARD), Float3(5.0f, 10.0f, 10.0f)));
+        instances.emplace_back(&planeBlas, &floorMat, scale(translate(I, Float3(0.0f, 9.0f, 0.0f)), Float3(10.0f, 10.0f, 10.0f)));
+        instances.emplace_back(&planeBlas, &floorMat, scale(rotate(translate(I, Float3(0.0f, 4.0f, -10.0f)), radians(90.0f), WORLD_RIGHT), Float3(10.0f, 10.0f, 5.0f)));
+        instances.emplace_back(&planeBlas, &floorMat, scale(rotate(translate(I, Float3(0.0f, 4.0f, 10.0f)), radians(90.0f), WORLD_RIGHT), Float3(10.0f, 10.0f, 5.0f)));
+
+        SceneBackground background;
+        background.type = BackgroundType::ColorGradient;
+        background.gradient.colorA = Float3(0.8f, 0.8f, 0.8f);
+        background.gradient.colorB = Float3(0.1f, 0.4f, 0.6f);
+        GPUScene scene(&context, background, instances);
+
+        RendererConfig config;            /* samplesPerFrame 1 (ui_manager.h:26), unbounded + RR */
+        WaveFrontRenderer renderer(&context, nullptr, config, FramebufferSize{W, H}, worldCam, scene);
+
+        for (U32 f = 0; f < frames; ++f) {
+            const auto t0 = std::chrono::steady_clock::now();
+            renderer.render(0.0f);        /* frameInfo() reads the accumulator: the frame is complete */
+            const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+            const FrameInstrumentationData& info = renderer.frameInfo();
+            /* main.cpp:431-442 */
+            std::printf("%08.2fms (%05.1f fps) - %08.2fMrays/s - %05u samples (%u spp) - %010.2f Lumen\n", ms, 1000.0 / ms,
+                        (double)W * H * renderer.config().samplesPerFrame / ms / 1000.0, info.totalSamples,
+                        renderer.config().samplesPerFrame, info.energy);
+        }
+
+        const std::vector<F32> acc = renderer.readAccumulator();
+        FILE* out = std::fopen(argv[5], "wb");
+        if (!out) { std::perror(argv[5]); return 1; }
+        std::fprintf(out, "P6\n%u %u\n255\n", W, H);
+        std::vector<unsigned char> row((size_t)W * 3);
+        for (U32 y = 0; y < H; ++y) {
+            for (U32 x = 0; x < W; ++x)
+                for (int c = 0; c < 3; ++c) {
+                    const float v = std::sqrt(acc[4 * ((size_t)y * W + x) + c] / (float)frames);
+                    row[3 * (size_t)x + c] = (unsigned char)(v >= 1.0f ? 255 : (v <= 0.0f ? 0 : (int)(v * 255.0f + 0.5f)));
+                }
+            std::fwrite(row.data(), 1, row.size(), out);
+        }
+        std::fclose(out);
+    } catch (const std::exception& e) {
+        std::fprintf(stderr, "render_indoor: %s\n", e.what());
+        return 1;
+    }
+    return 0;
+}
