@@ -168,10 +168,11 @@ int surf_set_frame_batch(surf_ctx* ctx, uint32_t frames);
  * traces for up to millions of segments. */
 int surf_set_zero_cutoff(surf_ctx* ctx, int enabled);
 /* Drain policy: when no new sample may be issued and at most `threshold_paths`
- * paths are in flight, the tail kernel finishes them: stage 1 runs
- * `lanes_per_wave` paths per 64-lane wave for up to `stage_segments` segments
- * each (0 = automatic for the first two; stage_segments 0 = no second stage),
- * stage 2 runs the survivors one per wave.  Results do not depend on the
+ * paths are in flight, the tail kernel finishes them in stages: each stage
+ * runs `lanes_per_wave` paths per 64-lane wave for up to `stage_segments`
+ * segments; once few paths remain, the cooperative tail runs each on a whole
+ * wave (0 = automatic for the first two; stage_segments 0 = a single stage
+ * that runs every path to its end; default 64).  Results do not depend on the
  * policy.  Drains the context first. */
 int surf_set_tail_policy(surf_ctx* ctx, uint32_t threshold_paths, uint32_t lanes_per_wave, uint32_t stage_segments);
 /* Diagnostics: how many paths the segment cap ended in the current sample
@@ -221,6 +222,11 @@ int surf_trace_closest(surf_ctx* ctx, uint32_t n, const float* o, const float* d
                        float* out_t, float* out_u, float* out_v, uint32_t* out_inst, uint32_t* out_prim);
 int surf_trace_any(surf_ctx* ctx, uint32_t n, const float* o, const float* d, const float* tmax,
                    uint8_t* occluded);
+/* 0: one ray per lane (the wavefront kernels' traversal); 1: one ray per
+ * 64-lane wave with the instances traced in parallel (the cooperative tail's
+ * traversal; needs a scene uploaded with a single-leaf TLAS of <= 64
+ * instances).  Results are identical; selects what surf_trace_* run. */
+int surf_set_trace_mode(surf_ctx* ctx, int mode);
 
 /* ---- host scene build (the reference's main.cpp scene, OBJ assets) ----
  * variant 0: bundled indoor scene; 1: C5 deep scene (+648 Suzannes in one mesh). */

@@ -148,6 +148,7 @@ SURF_HD V3 xyz(float4 v) { return mk3(v.x, v.y, v.z); }
  * together and paid as one memory round trip (without it, the leaf/count words
  * are fetched first and the boxes only after the leaf branch: two trips). */
 __device__ __forceinline__ void pin(float4& v) { asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w)); }
+__device__ __forceinline__ uint32_t laneIdx() { return __lane_id(); }
 
 template <bool ANY>
 __device__ __forceinline__ bool leafTest(const float4* tri, uint32_t lf, uint32_t cnt, V3 o, V3 d, float& depth,
@@ -243,6 +244,71 @@ __device__ __forceinline__ bool blasTrace(const DevScene& S, const TraceInst& I,
         } else {
             node = cn;
             if (df != kFarAway) { *sp = cf; sp += stride; }
+        }
+    }
+    return any;
+}
+
+/* Closest hit of one BLAS with depth starting at kFarAway, for the
+ * instance-parallel merge (traceSceneCoop).  Same traversal as blasTrace; in
+ * addition it carries A = the largest box entry distance on the path to the
+ * current node (a second LDS stack) and flags `patho` when a hit is accepted at
+ * t < A -- a triangle reported in front of a box that contains it (rounding).
+ * Without such a hit, the traversal with any starting depth D returns exactly
+ * this result when t < D and a miss otherwise: a box the depth-D traversal
+ * prunes (entry >= its depth) could only have contributed a hit below that
+ * entry by exactly this rounding effect, so both traversals accept the same
+ * hits below D in the same order ("Cooperative tail"). */
+template <bool FIN>
+__device__ __forceinline__ bool blasTraceTrack(const DevScene& S, const TraceInst& I, V3 o, V3 d, V3 rd, float& depth,
+                                               float& hu, float& hv, uint32_t& hprim, uint32_t* stk, float* astk,
+                                               uint32_t stride, bool& patho) {
+    const uint32_t nodeOff = I.meta.x;
+    const float4* tri = S.tris + 3u * I.meta.y;
+    const float4 r0 = I.r0, r1 = I.r1;
+    const uint32_t rlf = f2u(r0.w), rcnt = f2u(r1.w);
+    if (rcnt != 0u) return leafTestUniform<false>(tri, rlf, rcnt, o, d, depth, hu, hv, hprim);   /* no boxes: exact for any D */
+    uint32_t* sp = stk;
+    float* ap = astk;
+    uint32_t node;
+    float A;
+    bool any = false;
+    {
+        float dn = boxDist<FIN>(r0, r1, o, rd, depth);
+        float df = boxDist<FIN>(I.r2, I.r3, o, rd, depth);
+        uint32_t cn = nodeOff + rlf, cf = cn + 1u;
+        if (dn > df) { const float t = dn; dn = df; df = t; const uint32_t c = cn; cn = cf; cf = c; }
+        if (dn == kFarAway) return false;
+        node = cn; A = dn;
+        if (df != kFarAway) { *sp = cf; *ap = df; sp += stride; ap += stride; }
+    }
+    for (;;) {
+        const float4* nd = S.nodes + 4u * node;
+        float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
+        pin(q0); pin(q1); pin(q2); pin(q3);
+        const uint32_t lf = f2u(q0.w), cnt = f2u(q1.w);
+        if (cnt != 0u) {
+            if (leafTest<false>(tri, lf, cnt, o, d, depth, hu, hv, hprim)) {
+                any = true;
+                if (depth < A) patho = true;
+            }
+            if (sp == stk) break;
+            sp -= stride; ap -= stride;
+            node = *sp; A = *ap;
+            continue;
+        }
+        float dn = boxDist<FIN>(q0, q1, o, rd, depth);
+        float df = boxDist<FIN>(q2, q3, o, rd, depth);
+        uint32_t cn = nodeOff + lf, cf = cn + 1u;
+        if (dn > df) { const float t = dn; dn = df; df = t; const uint32_t c = cn; cn = cf; cf = c; }
+        if (dn == kFarAway) {
+            if (sp == stk) break;
+            sp -= stride; ap -= stride;
+            node = *sp; A = *ap;
+        } else {
+            node = cn;
+            if (df != kFarAway) { *sp = cf; *ap = fmaxf(A, df); sp += stride; ap += stride; }
+            A = fmaxf(A, dn);
         }
     }
     return any;
@@ -349,6 +415,84 @@ __device__ __forceinline__ bool traceScene(const DevScene& S, const TraceTables&
     return any;
 }
 
+/* Object-space ray of instance I (Instance::intersect, bvh.cpp:481-513). */
+__device__ __forceinline__ void instanceRay(const TraceInst& I, V3 o, V3 d, V3& oo, V3& dd) {
+    oo = mk3(rowDot(I.m0, o.x, o.y, o.z, 1.0f), rowDot(I.m1, o.x, o.y, o.z, 1.0f), rowDot(I.m2, o.x, o.y, o.z, 1.0f));
+    if (!I.meta.z) oo = divs(oo, rowDot(I.m3, o.x, o.y, o.z, 1.0f));
+    dd = mk3(rowDot(I.m0, d.x, d.y, d.z, 0.0f), rowDot(I.m1, d.x, d.y, d.z, 0.0f), rowDot(I.m2, d.x, d.y, d.z, 0.0f));
+}
+
+/* ------------------------------------------------------- cooperative (one ray per wave)
+ * For the single-leaf TLAS with at most 64 instances: lane k traces instance
+ * tlasIdx[k] in parallel; the reference's sequential instance loop is then
+ * replayed on the results in TLAS order.  Lane k's result with depth kFarAway
+ * equals the sequential call with the running depth D exactly (hit when t < D,
+ * else miss) unless blasTraceTrack flagged a rounding hit; then lane k re-runs
+ * the sequential call with depth D (never observed on the bundled scene, kept
+ * for exactness).  All lanes must hold the same ray.  Returns the same
+ * (hit, depth, u, v, inst, prim) as traceScene<false>. */
+__device__ __forceinline__ bool traceSceneCoop(const DevScene& S, const TraceTables& Tt, V3 o, V3 d, float& depth, float& hu,
+                                               float& hv, uint32_t& hinst, uint32_t& hprim, uint32_t* stk, float* astk,
+                                               uint32_t stride) {
+    const uint32_t lane = laneIdx();
+    const uint32_t n = S.tlasLeafCount;
+    float t = kFarAway, u = 0.0f, v = 0.0f;
+    uint32_t prim = kUnset, ii = kUnset;
+    bool hit = false, patho = false;
+    V3 oo = mk3(0.0f, 0.0f, 0.0f), dd = oo, rd = oo;
+    if (lane < n) {
+        ii = Tt.order[lane];
+        const TraceInst& I = Tt.inst[ii];
+        instanceRay(I, o, d, oo, dd);
+        rd = mk3(1.0f / dd.x, 1.0f / dd.y, 1.0f / dd.z);
+        if (S.finiteBoxes && finite3(oo) && finite3(rd))
+            hit = blasTraceTrack<true>(S, I, oo, dd, rd, t, u, v, prim, stk, astk, stride, patho);
+        else
+            hit = blasTraceTrack<false>(S, I, oo, dd, rd, t, u, v, prim, stk, astk, stride, patho);
+    }
+    /* replay of BvhTLAS::intersect's leaf loop (bvh.cpp:654-716) in TLAS order */
+    bool any = false;
+    float best = depth;
+    /* wave-uniform loop: v_readlane into SGPRs (no LDS round trip per value) */
+    const unsigned long long hitMask = __ballot(hit), pathoMask = __ballot(patho);
+    for (uint32_t k = 0; k < n; ++k) {
+        if (!((hitMask >> k) & 1ull)) continue;
+        float tk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t), (int)k));
+        if (!(tk < best)) continue;
+        float uk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(u), (int)k));
+        float vk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), (int)k));
+        uint32_t pk = (uint32_t)__builtin_amdgcn_readlane((int)prim, (int)k);
+        if ((pathoMask >> k) & 1ull) {
+            /* rounding case: lane k re-runs the sequential call with depth `best` */
+            bool h2 = false;
+            float t2 = best, u2 = 0.0f, v2 = 0.0f;
+            uint32_t p2 = kUnset;
+            if (lane == k) h2 = blasTrace<false, false>(S, Tt.inst[ii], oo, dd, rd, t2, u2, v2, p2, stk, stride, 0u);
+            if (!__shfl((int)h2, (int)k)) continue;
+            tk = __shfl(t2, (int)k); uk = __shfl(u2, (int)k); vk = __shfl(v2, (int)k); pk = (uint32_t)__shfl((int)p2, (int)k);
+        }
+        best = tk; hu = uk; hv = vk; hprim = pk;
+        hinst = Tt.order[k];
+        any = true;
+    }
+    depth = best;
+    return any;
+}
+
+/* Any hit: each instance's test is independent of the others (no depth update
+ * survives a hit), so the sequential early-exit loop equals the OR. */
+__device__ __forceinline__ bool traceAnyCoop(const DevScene& S, const TraceTables& Tt, V3 o, V3 d, float tmaxv, uint32_t* stk,
+                                             uint32_t stride) {
+    const uint32_t lane = laneIdx();
+    bool occ = false;
+    if (lane < S.tlasLeafCount) {
+        float depth = tmaxv, u, v;
+        uint32_t prim;
+        occ = instanceTrace<true>(S, Tt.inst[Tt.order[lane]], o, d, depth, u, v, prim, stk, stride, 0u);
+    }
+    return __ballot(occ) != 0ull;
+}
+
 /* --------------------------------------------------------------- wave helpers */
 __device__ __forceinline__ uint32_t laneId() { return __lane_id(); }
 __device__ __forceinline__ uint32_t rankBelow(unsigned long long mask) {
@@ -430,7 +574,9 @@ __device__ __forceinline__ void addRadiance(float4* rad, uint32_t sid, V3 c) {
 /* Result of shading one hit: what the path does next. */
 struct ShadeOut {
     bool cont, shadow, hitGeom, accd, capped;
+    bool addRad;                     /* rad[sid] += radd (miss / light hit), done by the caller */
     uint32_t seg;                    /* extension rays of the path so far */
+    V3 radd;
     float4 o, d, T;                  /* continuation path record */
     float4 so, sd, sc;               /* shadow ray: (origin, tmax), (dir, sid), (T*Ld, 0) */
 };
@@ -456,8 +602,8 @@ __device__ __forceinline__ void stageTables(const DevScene& S, DevInstance* sIns
 }
 
 __device__ __forceinline__ void shadePath(const DevScene& S, const ShadeTables& Tb, float4 o4, float4 d4, float4 T4, float4 h4,
-                                          uint32_t inst, float4* __restrict__ rad, uint32_t maxSeg, uint32_t zeroCutoff, ShadeOut& r) {
-    r.cont = r.shadow = r.hitGeom = r.accd = r.capped = false;
+                                          uint32_t inst, uint32_t maxSeg, uint32_t zeroCutoff, ShadeOut& r) {
+    r.cont = r.shadow = r.hitGeom = r.accd = r.capped = r.addRad = false;
     const uint32_t sid = f2u(o4.w);
     uint32_t flags = f2u(d4.w);
     uint32_t seed = f2u(T4.w);
@@ -475,7 +621,7 @@ __device__ __forceinline__ void shadePath(const DevScene& S, const ShadeTables& 
             const float a = 0.5f * (1.0f + d.y);
             bg = add(lscl(a, ld3(S.bgB)), lscl(1.0f - a, ld3(S.bgA)));
         }
-        addRadiance(rad, sid, mul(T, bg));
+        r.addRad = true; r.radd = mul(T, bg);
         r.accd = true;
         return;
     }
@@ -485,7 +631,7 @@ __device__ __forceinline__ void shadePath(const DevScene& S, const ShadeTables& 
     const bool isLight = m.emit > 0.0f && (m.ec[0] > 0.0f || m.ec[1] > 0.0f || m.ec[2] > 0.0f);
     if (isLight) {
         const V3 le = lscl(m.emit, ld3(m.ec));
-        addRadiance(rad, sid, lastSpecular ? mul(T, le) : mk3(0.0f, 0.0f, 0.0f));
+        r.addRad = true; r.radd = lastSpecular ? mul(T, le) : mk3(0.0f, 0.0f, 0.0f);
         r.accd = lastSpecular;
         return;
     }
@@ -642,14 +788,15 @@ __global__ __launch_bounds__(kBlock, SURF_SHADE_WAVES) void k_shade(DevScene S, 
     for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x, it ^= 1u) {
         const uint32_t i = base + threadIdx.x;
         ShadeOut r;
-        r.cont = r.shadow = r.hitGeom = r.accd = r.capped = false;
+        r.cont = r.shadow = r.hitGeom = r.accd = r.capped = r.addRad = false;
         r.seg = 0;
         uint32_t slot = 0;
         const bool active = i < n;
         if (active) {
             const float4 o4 = cur.o[i];
             slot = f2u(o4.w) / npx;
-            shadePath(S, Tb, o4, cur.d[i], cur.T[i], hitTUV[i], hitInst[i], rad, maxSeg, zeroCutoff, r);
+            shadePath(S, Tb, o4, cur.d[i], cur.T[i], hitTUV[i], hitInst[i], maxSeg, zeroCutoff, r);
+            if (r.addRad) addRadiance(rad, f2u(o4.w), r.radd);
         }
         const unsigned long long mCont = __ballot(r.cont), mSh = __ballot(r.shadow);
         if (laneId() == 0) { sWave[it][wv][0] = (uint32_t)__popcll(mCont); sWave[it][wv][1] = (uint32_t)__popcll(mSh); }
@@ -807,7 +954,8 @@ __global__ __launch_bounds__(64) void k_tail(DevScene S, Pool cur, uint32_t n, u
         const bool hit = traceScene<false>(S, Tt, xyz(o4), xyz(d4), depth, u, v, inst, prim, stk, stride);
         ++nExt;
         ShadeOut r;
-        shadePath(S, Tb, o4, d4, T4, make_float4(depth, u, v, u2f(prim)), hit ? inst : kUnset, rad, maxSeg, zeroCutoff, r);
+        shadePath(S, Tb, o4, d4, T4, make_float4(depth, u, v, u2f(prim)), hit ? inst : kUnset, maxSeg, zeroCutoff, r);
+        if (r.addRad) addRadiance(rad, f2u(o4.w), r.radd);
         nHit += r.hitGeom; nAcc += r.accd;
         if (r.shadow) {
             ++nSh;
@@ -841,6 +989,74 @@ __global__ __launch_bounds__(64) void k_tail(DevScene S, Pool cur, uint32_t n, u
     atomicAdd(&ev[0], nExt - (unsigned long long)firstCounted); atomicAdd(&ev[1], nHit); atomicAdd(&ev[2], nCont);
     atomicAdd(&ev[3], nSh); atomicAdd(&ev[4], nAcc); atomicAdd(&ev[5], nUn);
     if (done) atomicAdd(&ev[6], 1ull);
+}
+
+/* Cooperative tail: one path per 64-lane wave (block), for the few very long
+ * paths left at the end of a drain, whose single-lane segment latency bounds
+ * the drain.  Each segment: closest hit with the instances traced in parallel
+ * lanes (traceSceneCoop), shading evaluated redundantly by every lane (same
+ * inputs, same results, no broadcast), shadow ray any-hit in parallel lanes;
+ * lane 0 does the writes.  Identical results to k_tail.  LDS: traversal stack,
+ * box-distance stack (stackWords words each), then the trace tables. */
+template <bool LDS_TABLES>
+__global__ __launch_bounds__(64) void k_tail_coop(DevScene S, Pool cur, uint32_t n, float4* __restrict__ rad,
+                                                  uint32_t* __restrict__ frameDone, uint32_t npx, uint32_t window, Counters* C,
+                                                  uint32_t stackWords, uint32_t firstCounted) {
+    extern __shared__ uint32_t lds[];
+    const TraceTables Tt = traceTables<LDS_TABLES>(S, lds, 2u * stackWords);
+    __shared__ DevInstance sInst[LDS_TABLES ? kLdsInst : 1];
+    __shared__ DevMaterial sMat[LDS_TABLES ? kLdsMats : 1];
+    __shared__ uint2 sLights[LDS_TABLES ? kLdsLights : 1];
+    ShadeTables Tb{S.inst, S.mats, S.lights};
+    if (LDS_TABLES) {
+        stageTables(S, sInst, sMat, sLights);
+        Tb = ShadeTables{sInst, sMat, sLights};
+    }
+    const uint32_t i = blockIdx.x;
+    if (i >= n) return;
+    const bool lead = threadIdx.x == 0;
+    uint32_t* stk = lds + threadIdx.x;
+    float* astk = reinterpret_cast<float*>(lds + stackWords) + threadIdx.x;
+    const uint32_t stride = blockDim.x;
+    const uint32_t maxSeg = C->maxSeg, zeroCutoff = C->zeroCutoff;
+    float4 o4 = cur.o[i], d4 = cur.d[i], T4 = cur.T[i];
+    const uint32_t slot = f2u(o4.w) / npx;
+    unsigned long long nExt = 0, nHit = 0, nCont = 0, nSh = 0, nAcc = 0, nUn = 0;
+    for (;;) {
+        float depth = kFarAway, u = 0.0f, v = 0.0f;
+        uint32_t inst = kUnset, prim = kUnset;
+        const bool hit = traceSceneCoop(S, Tt, xyz(o4), xyz(d4), depth, u, v, inst, prim, stk, astk, stride);
+        ++nExt;
+        ShadeOut r;
+        shadePath(S, Tb, o4, d4, T4, make_float4(depth, u, v, u2f(prim)), hit ? inst : kUnset, maxSeg, zeroCutoff, r);
+        if (lead && r.addRad) addRadiance(rad, f2u(o4.w), r.radd);
+        nHit += r.hitGeom; nAcc += r.accd;
+        if (r.shadow) {
+            ++nSh;
+            if (!traceAnyCoop(S, Tt, xyz(r.so), xyz(r.sd), r.so.w, stk, stride)) {
+                if (lead) addRadiance(rad, f2u(r.sd.w), xyz(r.sc));
+                ++nUn; ++nAcc;
+            }
+        }
+        if (lead && r.capped) {
+            const unsigned long long k = atomicAdd(&C->ev[7], 1ull);
+            if (k < 64) C->capped[k] = f2u(o4.w);
+        }
+        if (!r.cont) {
+            if (lead) atomicMax(&C->segMax, r.seg);
+            break;
+        }
+        ++nCont;
+        o4 = r.o; d4 = r.d; T4 = r.T;
+    }
+    if (lead) {
+        const uint32_t st = blockIdx.x % kStripes;
+        unsigned long long* ev = C->evS[st];
+        atomicAdd(&frameDone[st * window + slot], 1u);
+        atomicAdd(&ev[0], nExt - (unsigned long long)firstCounted); atomicAdd(&ev[1], nHit); atomicAdd(&ev[2], nCont);
+        atomicAdd(&ev[3], nSh); atomicAdd(&ev[4], nAcc); atomicAdd(&ev[5], nUn);
+        atomicAdd(&ev[6], 1ull);
+    }
 }
 
 /* acc[p] += (radiance, 1) for frames [f0, f0+count) of the stream, in frame
@@ -906,6 +1122,38 @@ __global__ __launch_bounds__(kBlock) void k_trace_any(DevScene S, const float* _
     uint32_t inst = kUnset, prim = kUnset;
     occ[i] = traceScene<true>(S, Tt, mk3(o[3 * i], o[3 * i + 1], o[3 * i + 2]), mk3(d[3 * i], d[3 * i + 1], d[3 * i + 2]),
                               depth, u, v, inst, prim, lds + threadIdx.x, blockDim.x) ? 1 : 0;
+}
+
+/* Cooperative traversal entry points (one ray per 64-lane block): the same
+ * results as k_trace_closest / k_trace_any, exposed for parity tests and
+ * latency measurements of the cooperative tail's traversal. */
+__global__ __launch_bounds__(64) void k_trace_closest_coop(DevScene S, const float* __restrict__ o, const float* __restrict__ d,
+                                                           uint32_t n, float4* __restrict__ tuv, uint2* __restrict__ ip,
+                                                           uint32_t stackWords) {
+    extern __shared__ uint32_t lds[];
+    const TraceTables Tt = stageTrace(S, lds, 2u * stackWords);
+    const uint32_t i = blockIdx.x;
+    if (i >= n) return;
+    float depth = kFarAway, u = 0.0f, v = 0.0f;
+    uint32_t inst = kUnset, prim = kUnset;
+    const bool hit = traceSceneCoop(S, Tt, mk3(o[3 * i], o[3 * i + 1], o[3 * i + 2]), mk3(d[3 * i], d[3 * i + 1], d[3 * i + 2]),
+                                    depth, u, v, inst, prim, lds + threadIdx.x,
+                                    reinterpret_cast<float*>(lds + stackWords) + threadIdx.x, blockDim.x);
+    if (threadIdx.x == 0) {
+        tuv[i] = make_float4(depth, hit ? u : 0.0f, hit ? v : 0.0f, 0.0f);
+        ip[i] = make_uint2(hit ? inst : kUnset, hit ? prim : kUnset);
+    }
+}
+__global__ __launch_bounds__(64) void k_trace_any_coop(DevScene S, const float* __restrict__ o, const float* __restrict__ d,
+                                                       const float* __restrict__ tmaxv, uint32_t n, uint8_t* __restrict__ occ,
+                                                       uint32_t stackWords) {
+    extern __shared__ uint32_t lds[];
+    const TraceTables Tt = stageTrace(S, lds, stackWords);
+    const uint32_t i = blockIdx.x;
+    if (i >= n) return;
+    const bool oc = traceAnyCoop(S, Tt, mk3(o[3 * i], o[3 * i + 1], o[3 * i + 2]), mk3(d[3 * i], d[3 * i + 1], d[3 * i + 2]),
+                                 tmaxv[i], lds + threadIdx.x, blockDim.x);
+    if (threadIdx.x == 0) occ[i] = oc ? 1 : 0;
 }
 
 }  // namespace surfdev

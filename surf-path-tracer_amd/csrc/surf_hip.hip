@@ -92,9 +92,12 @@ struct surf_ctx {
     bool zeroCutoff = true;        /* radiance-neutral early end of T == 0 paths */
     uint64_t pushedLimit = 0;
     uint32_t tailPaths = 0;        /* drain policy (surf_set_tail_policy), 0 = automatic */
-    uint32_t tailBudget = 0;       /* stage-1 segment budget of the drain tail (0 = one stage) */
-    Pool surv{};                   /* drain survivors (stage 2 input) */
+    uint32_t tailBudget = 64;      /* per-stage segment budget of the drain tail (0 = one stage) */
+    Pool surv[2]{};                /* drain survivors, ping-pong between stages */
     uint32_t survCap = 0;
+    uint32_t coopMax = 0;          /* survivors handled by the cooperative tail (one path per wave) */
+    bool coopEligible = false;     /* single-leaf TLAS of <= 64 instances, LDS tables */
+    int traceMode = 0;             /* surf_trace_closest/_any: 0 one ray per lane, 1 one ray per wave */
     uint32_t tailLanes = 0;
     uint32_t segMaxBase = 0;       /* longest path of finished streams */
 
@@ -236,9 +239,11 @@ int allocWavefront(surf_ctx* c) {
         if ((rc = devAlloc(c, c->wfAllocs, &c->pool[p].T, cap))) return rc;
     }
     c->survCap = (uint32_t)std::min<size_t>(std::max<size_t>(cap / 16, 4096), 1u << 18);
-    if ((rc = devAlloc(c, c->wfAllocs, &c->surv.o, c->survCap))) return rc;
-    if ((rc = devAlloc(c, c->wfAllocs, &c->surv.d, c->survCap))) return rc;
-    if ((rc = devAlloc(c, c->wfAllocs, &c->surv.T, c->survCap))) return rc;
+    for (int q = 0; q < 2; ++q) {
+        if ((rc = devAlloc(c, c->wfAllocs, &c->surv[q].o, c->survCap))) return rc;
+        if ((rc = devAlloc(c, c->wfAllocs, &c->surv[q].d, c->survCap))) return rc;
+        if ((rc = devAlloc(c, c->wfAllocs, &c->surv[q].T, c->survCap))) return rc;
+    }
     if ((rc = devAlloc(c, c->wfAllocs, &c->hitTUV, cap))) return rc;
     if ((rc = devAlloc(c, c->wfAllocs, &c->hitInst, cap))) return rc;
     if ((rc = devAlloc(c, c->wfAllocs, &c->Q.o, cap))) return rc;
@@ -258,6 +263,7 @@ int allocWavefront(surf_ctx* c) {
     if (hipGetDeviceProperties(&prop, c->device) == hipSuccess && prop.multiProcessorCount > 0) cus = prop.multiProcessorCount;
     const uint64_t maxBlocks = (cap + kBlock - 1) / kBlock;
     c->gridWork = (uint32_t)std::min<uint64_t>(maxBlocks, (uint64_t)cus * 8);
+    c->coopMax = (uint32_t)cus * 8;     /* 2 waves per SIMD of the cooperative tail */
     c->gridRegen = (uint32_t)std::min<uint64_t>(maxBlocks, (uint64_t)cus * 8);
     c->allocated = true;
     return SURF_OK;
@@ -398,39 +404,55 @@ int advance(surf_ctx* c) {
 
 /* Finishes every path of pool 0 in one k_tail launch (counters at an even
  * phase boundary: pool 0 is the next to be extended, nothing else pending). */
-void launchTail(surf_ctx* c, Pool in, uint32_t n, uint32_t lpw, uint32_t firstCounted, uint32_t budget) {
+void launchTail(surf_ctx* c, Pool in, uint32_t n, uint32_t lpw, uint32_t firstCounted, uint32_t budget, Pool out) {
     const uint32_t blocks = (n + lpw - 1) / lpw;
     const size_t lds = traversalLds(c, 64);
     if (c->ldsTables)
         hipLaunchKernelGGL(k_tail<true>, dim3(blocks), dim3(64), lds, c->stream, c->S, in, n, lpw, c->rad, c->frameDone,
-                           c->npx, c->window, c->ctr, stackWords(c, 64), firstCounted, budget, c->surv);
+                           c->npx, c->window, c->ctr, stackWords(c, 64), firstCounted, budget, out);
     else
         hipLaunchKernelGGL(k_tail<false>, dim3(blocks), dim3(64), lds, c->stream, c->S, in, n, lpw, c->rad, c->frameDone,
-                           c->npx, c->window, c->ctr, stackWords(c, 64), firstCounted, budget, c->surv);
+                           c->npx, c->window, c->ctr, stackWords(c, 64), firstCounted, budget, out);
 }
 
 /* Finishes every path of pool 0 (counters at an even phase boundary: pool 0 is
- * the next to be extended, nothing else pending).  Stage 1 runs each path up
- * to tailBudget segments, many paths per wave; the few still alive (lens TIR
- * orbits: thousands of segments) go to stage 2, one path per wave, so a long
- * path never drags a wave of finished lanes and never shares one. */
+ * the next to be extended, nothing else pending).  Lane-parallel stages (many
+ * paths per wave) run each path for up to tailBudget segments and hand the
+ * paths still alive to the next stage; once few enough remain (they are the
+ * reference's Russian-roulette survivors that run for thousands of segments),
+ * the cooperative tail runs each on a whole wave, which cuts the latency of a
+ * segment -- the quantity the last paths of a drain are bound by. */
 int runTail(surf_ctx* c) {
     const uint32_t n = c->hctr->nIn[0];
     if (n == 0) return SURF_OK;
-    const uint32_t lpw = c->tailLanes ? std::min<uint32_t>(64u, c->tailLanes)
-                                      : std::min<uint32_t>(64u, std::max<uint32_t>(1u, (n + 4095u) / 4096u));
     if (c->profiling) SURF_CHECK(c, hipEventRecord(c->pev[0], c->stream));
-    c->hctr->survN = 0;
-    SURF_CHECK(c, hipMemcpyAsync(&c->ctr->survN, &c->hctr->survN, sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
-    launchTail(c, c->pool[0], n, lpw, 1u, c->tailBudget);
-    SURF_CHECK(c, hipGetLastError());
-    SURF_CHECK(c, hipMemcpyAsync(&c->hctr->survN, &c->ctr->survN, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
-    SURF_CHECK(c, hipStreamSynchronize(c->stream));
-    const uint32_t m = std::min(c->hctr->survN, c->survCap);
-    if (m) {
-        const uint32_t lpw2 = std::min<uint32_t>(64u, std::max<uint32_t>(1u, (m + 2047u) / 2048u));
-        launchTail(c, c->surv, m, lpw2, 0u, 0u);
+    Pool in = c->pool[0];
+    uint32_t cnt = n, firstCounted = 1u;
+    int buf = 0;
+    for (int stage = 0; cnt; ++stage) {
+        if (c->coopEligible && c->tailBudget && cnt <= c->coopMax) {
+            const size_t lds = traversalLds(c, 64) + (size_t)stackWords(c, 64) * sizeof(float);
+            hipLaunchKernelGGL(k_tail_coop<true>, dim3(cnt), dim3(64), lds, c->stream, c->S, in, cnt, c->rad, c->frameDone,
+                               c->npx, c->window, c->ctr, stackWords(c, 64), firstCounted);
+            SURF_CHECK(c, hipGetLastError());
+            c->stats.tail_survivors += cnt;
+            break;
+        }
+        /* no more waves than fit at once (2 per SIMD at the tail's register
+         * count): a second round would wait for the first round's longest path */
+        const uint32_t lpw = c->tailLanes ? std::min<uint32_t>(64u, c->tailLanes)
+                                          : std::min<uint32_t>(64u, std::max<uint32_t>(1u, (cnt + c->coopMax - 1) / c->coopMax));
+        c->hctr->survN = 0;
+        SURF_CHECK(c, hipMemcpyAsync(&c->ctr->survN, &c->hctr->survN, sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+        launchTail(c, in, cnt, lpw, firstCounted, c->tailBudget, c->surv[buf]);
         SURF_CHECK(c, hipGetLastError());
+        if (!c->tailBudget) break;
+        SURF_CHECK(c, hipMemcpyAsync(&c->hctr->survN, &c->ctr->survN, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+        SURF_CHECK(c, hipStreamSynchronize(c->stream));
+        in = c->surv[buf];
+        cnt = std::min(c->hctr->survN, c->survCap);
+        firstCounted = 0u;
+        buf ^= 1;
     }
     if (c->profiling) {
         SURF_CHECK(c, hipEventRecord(c->pev[1], c->stream));
@@ -438,7 +460,6 @@ int runTail(surf_ctx* c) {
         float t; (void)hipEventElapsedTime(&t, c->pev[0], c->pev[1]);
         c->stats.ms_tail += t;
     }
-    c->stats.tail_survivors += m;
     /* pool 0 is now empty: the next phase starts from regen's refill */
     c->hctr->nIn[0] = 0;
     SURF_CHECK(c, hipMemcpyAsync(&c->ctr->nIn[0], &c->hctr->nIn[0], sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
@@ -648,6 +669,14 @@ int surf_set_tail_policy(surf_ctx* c, uint32_t threshold_paths, uint32_t lanes_p
     return SURF_OK;
 }
 
+int surf_set_trace_mode(surf_ctx* c, int mode) {
+    if (!c) return fail(nullptr, SURF_ERR_INVALID, "ctx is NULL");
+    if (mode != 0 && mode != 1) return fail(c, SURF_ERR_INVALID, "trace mode must be 0 or 1");
+    if (mode == 1 && !c->coopEligible) return fail(c, SURF_ERR_INVALID, "cooperative traversal needs a single-leaf TLAS of <= 64 instances");
+    c->traceMode = mode;
+    return SURF_OK;
+}
+
 int surf_set_zero_cutoff(surf_ctx* c, int enabled) {
     if (!c) return SURF_ERR_INVALID;
     int rc = endStream(c);
@@ -797,6 +826,7 @@ int surf_upload_scene(surf_ctx* c, const surf_scene_desc* d) {
     c->S = S;
     c->ldsTables = d->instance_count <= kLdsInst && d->instance_count <= kLdsTraceInst && d->material_count <= kLdsMats &&
                    d->light_count <= kLdsLights;
+    c->coopEligible = c->ldsTables && S.tlasLeafCount > 0 && S.tlasLeafCount <= 64;
     c->stackDepth = depth;
     c->nInstances = d->instance_count;
     c->nTriangles = d->triangle_count;
@@ -966,7 +996,10 @@ int surf_trace_closest(surf_ctx* c, uint32_t n, const float* o, const float* d, 
         (rc = devAlloc(c, tmp, &dT, n)) || (rc = devAlloc(c, tmp, &dI, n))) { freeList(tmp); return rc; }
     (void)hipMemcpyAsync(dO, o, 12 * (size_t)n, hipMemcpyHostToDevice, c->stream);
     (void)hipMemcpyAsync(dD, d, 12 * (size_t)n, hipMemcpyHostToDevice, c->stream);
-    if (c->ldsTables)
+    if (c->traceMode == 1)
+        hipLaunchKernelGGL(k_trace_closest_coop, dim3(n), dim3(64), traversalLds(c, 64) + (size_t)stackWords(c, 64) * sizeof(float),
+                           c->stream, c->S, (const float*)dO, (const float*)dD, n, dT, dI, stackWords(c, 64));
+    else if (c->ldsTables)
         hipLaunchKernelGGL(k_trace_closest<true>, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), traversalLds(c, kBlock), c->stream,
                            c->S, (const float*)dO, (const float*)dD, n, dT, dI, stackWords(c, kBlock));
     else
@@ -996,7 +1029,10 @@ int surf_trace_any(surf_ctx* c, uint32_t n, const float* o, const float* d, cons
     (void)hipMemcpyAsync(dO, o, 12 * (size_t)n, hipMemcpyHostToDevice, c->stream);
     (void)hipMemcpyAsync(dD, d, 12 * (size_t)n, hipMemcpyHostToDevice, c->stream);
     (void)hipMemcpyAsync(dM, tm, 4 * (size_t)n, hipMemcpyHostToDevice, c->stream);
-    if (c->ldsTables)
+    if (c->traceMode == 1)
+        hipLaunchKernelGGL(k_trace_any_coop, dim3(n), dim3(64), traversalLds(c, 64), c->stream, c->S, (const float*)dO,
+                           (const float*)dD, (const float*)dM, n, dR, stackWords(c, 64));
+    else if (c->ldsTables)
         hipLaunchKernelGGL(k_trace_any<true>, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), traversalLds(c, kBlock), c->stream,
                            c->S, (const float*)dO, (const float*)dD, (const float*)dM, n, dR, stackWords(c, kBlock));
     else

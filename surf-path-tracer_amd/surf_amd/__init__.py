@@ -96,7 +96,7 @@ def load() -> C.CDLL:
         "surf_destroy": ([P], None), "surf_last_error": ([P], C.c_char_p),
         "surf_shard_rows": ([P, P, C.POINTER(U32)], I32),
         "surf_set_pool_capacity": ([P, U32], I32), "surf_set_frame_batch": ([P, U32], I32),
-        "surf_set_profiling": ([P, I32], I32), "surf_set_zero_cutoff": ([P, I32], I32), "surf_set_tail_policy": ([P, U32, U32, U32], I32),
+        "surf_set_profiling": ([P, I32], I32), "surf_set_zero_cutoff": ([P, I32], I32), "surf_set_trace_mode": ([P, I32], I32), "surf_set_tail_policy": ([P, U32, U32, U32], I32),
         "surf_debug_capped": ([P, P, U32, C.POINTER(C.c_uint64)], I32),
         "surf_upload_scene": ([P, C.POINTER(SceneDesc)], I32),
         "surf_set_camera": ([P, P], I32),
@@ -259,11 +259,15 @@ class Renderer:
     def set_zero_cutoff(self, on: bool):
         _check(load().surf_set_zero_cutoff(self._h, 1 if on else 0), "surf_set_zero_cutoff", self._h)
 
-    def set_tail_policy(self, threshold_paths: int = 0, lanes_per_wave: int = 0, stage_segments: int = 0):
+    def set_tail_policy(self, threshold_paths: int = 0, lanes_per_wave: int = 0, stage_segments: int = 64):
         """Drain policy of the tail kernel (0 = automatic); stage_segments is the
-        first stage's per-path budget before survivors run one per wave (0 = one stage)."""
+        per-stage segment budget before the survivors move on (0 = one stage)."""
         _check(load().surf_set_tail_policy(self._h, threshold_paths, lanes_per_wave, stage_segments), "surf_set_tail_policy",
                self._h)
+
+    def set_trace_mode(self, mode: int):
+        """0: one ray per lane; 1: one ray per wave (cooperative), for trace_closest/trace_any."""
+        _check(load().surf_set_trace_mode(self._h, mode), "surf_set_trace_mode", self._h)
 
     def set_profiling(self, on: bool):
         _check(load().surf_set_profiling(self._h, 1 if on else 0), "surf_set_profiling", self._h)

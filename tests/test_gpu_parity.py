@@ -30,7 +30,8 @@ def l2_report(a, b):
     return float(np.sqrt((per ** 2).mean())), float(per.max()), float((per > 1e-3).mean())
 
 
-def test_closest_hit_records_bitexact(oracle_scene, product_scene):
+@pytest.mark.parametrize("mode", [0, 1], ids=["lane-per-ray", "wave-per-ray"])
+def test_closest_hit_records_bitexact(oracle_scene, product_scene, mode):
     W = H = 96
     (eo, ed), (so, sd, st) = oracle_scene.record_rays(W, H, 0, 0, W * H)
     rng = np.random.default_rng(5)
@@ -40,6 +41,7 @@ def test_closest_hit_records_bitexact(oracle_scene, product_scene):
     o = np.concatenate([eo, so, ro])
     d = np.concatenate([ed, sd, rd])
     r = surf_amd.Renderer(product_scene, W, H)
+    r.set_trace_mode(mode)
     gpu = r.trace_closest(o, d)
     cpu = oracle_scene.trace_closest(o, d)
     names = ["t", "u", "v", "inst", "prim"]
@@ -49,10 +51,12 @@ def test_closest_hit_records_bitexact(oracle_scene, product_scene):
     assert (gpu[3] != UNSET).mean() > 0.9
 
 
-def test_any_hit_bitexact(oracle_scene, product_scene):
+@pytest.mark.parametrize("mode", [0, 1], ids=["lane-per-ray", "wave-per-ray"])
+def test_any_hit_bitexact(oracle_scene, product_scene, mode):
     W = H = 96
     _, (so, sd, st) = oracle_scene.record_rays(W, H, 1, 0, W * H)
     r = surf_amd.Renderer(product_scene, W, H)
+    r.set_trace_mode(mode)
     g = r.trace_any(so, sd, st)
     c = oracle_scene.trace_any(so, sd, st)
     assert len(so) > 1000

@@ -10,9 +10,11 @@ z = np.load("/root/repo/tools/longpath_rays.npz")
 o, d = z["o"], z["d"]
 s = surf_amd.Scene.indoor()
 r = surf_amd.Renderer(s, 64, 64)
-for rep in range(3):
-    for k in (100, 1000, 2000):              # single rays deep in the path (inside the lens)
+for mode in (0, 1):
+  r.set_trace_mode(mode)
+  for rep in range(3):
+    for k in (100, 1000, 2000):              # single rays deep in a long path
         r.trace_closest(o[k:k + 1], d[k:k + 1])
-    r.trace_closest(o[1000:1064], d[1000:1064])   # one wave of lens rays
+    r.trace_closest(o[1000:1064], d[1000:1064])   # 64 rays
     r.trace_closest(o, d)                          # the whole path as a batch
 print("done", len(o))
