@@ -175,6 +175,12 @@ int surf_set_zero_cutoff(surf_ctx* ctx, int enabled);
  * that runs every path to its end; default 64).  Results do not depend on the
  * policy.  Drains the context first. */
 int surf_set_tail_policy(surf_ctx* ctx, uint32_t threshold_paths, uint32_t lanes_per_wave, uint32_t stage_segments);
+/* Long paths: a path whose next segment would be its `escape_segments`-th
+ * leaves the wavefront (one segment per iteration) for a worker kernel that
+ * runs concurrently on a second stream and advances it up to `budget`
+ * segments per graph replay (default off; escape_segments 0 = off).
+ * Results do not depend on it.  Drains the context first. */
+int surf_set_long_paths(surf_ctx* ctx, uint32_t escape_segments, uint32_t budget);
 /* Diagnostics: how many paths the segment cap ended in the current sample
  * stream, and the sample ids (frame slot * shard pixels + pixel) of the first
  * min(count, 64, max). */
@@ -185,7 +191,10 @@ int surf_set_profiling(surf_ctx* ctx, int enabled);
 
 /* ---- scene / camera ---- */
 int surf_upload_scene(surf_ctx* ctx, const surf_scene_desc* desc);
-/* Replaces instances + TLAS (same BLASes/materials): the animation re-upload. */
+/* GPUScene::update's re-upload (scene.cpp:276-282): new instance records, TLAS
+ * indices and nodes and lights for the uploaded BLASes/materials (same counts;
+ * each instance must name a (node, index, triangle) offset triple of the
+ * upload).  Drains the context first; geometry stays resident. */
 int surf_update_instances(surf_ctx* ctx, const surf_gpu_instance* instances, uint32_t instance_count,
                           const uint32_t* tlas_indices, const surf_bvh_node* tlas_nodes, uint32_t tlas_node_count,
                           const surf_light* lights, uint32_t light_count);
@@ -232,6 +241,10 @@ int surf_set_trace_mode(surf_ctx* ctx, int mode);
  * variant 0: bundled indoor scene; 1: C5 deep scene (+648 Suzannes in one mesh). */
 int surf_scene_build_indoor(const char* assets_dir, int variant, surf_scene** out);
 int surf_scene_desc_get(const surf_scene* scene, surf_scene_desc* out);
+/* GPUScene::update (sources/scene.cpp:267-282): rotate instance 3 by
+ * 1.0*delta_time radians about WORLD_UP, refit the TLAS, re-batch.  Follow
+ * with surf_update_instances (or surf_upload_scene) on each context. */
+int surf_scene_update(surf_scene* scene, float delta_time);
 /* Reference camera of main.cpp:141-149 for a width x height render. */
 int surf_scene_camera(const surf_scene* scene, uint32_t width, uint32_t height, surf_camera_ubo* out);
 /* Deepest root-to-leaf edge counts of the TLAS and of all BLASes. */

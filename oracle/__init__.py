@@ -53,6 +53,7 @@ def load():
         "orc_trace_brute": ([P, U32, P, P, P, P, P], None),
         "orc_trace_visits": ([P, U32, P, P, P, P], None),
         "orc_path_lengths": ([P, U32, U32, U32, P], None),
+        "orc_scene_update": ([P, F], None),
         "orc_record_rays": ([P, U32, U32, U32, U32, U32, U32, P, P, P, U32, P, P, P, P], None),
         "orc_bvh_depths": ([P, C.POINTER(U32), C.POINTER(U32)], None),
         "orc_init_seed": ([U32], U32), "orc_random_u32": ([C.POINTER(U32)], U32),
@@ -151,6 +152,10 @@ class OracleScene:
         nodes, tris = np.zeros((len(o), ni), np.uint32), np.zeros((len(o), ni), np.uint32)
         load().orc_trace_visits(self._h, len(o), _p(o), _p(d), _p(nodes), _p(tris))
         return nodes, tris
+
+    def update(self, dt: float):
+        """GPUScene::update: rotate instance 3 by dt radians about +y, refit the TLAS."""
+        load().orc_scene_update(self._h, dt)
 
     def path_lengths(self, width, height, frame):
         """Extension rays per pixel path of one frame (diagnostics)."""

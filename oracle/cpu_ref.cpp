@@ -947,6 +947,34 @@ double orc_render(orc_scene* h, uint32_t W, uint32_t H, uint32_t r0, uint32_t r1
     return std::chrono::duration<double>(t1 - t0).count();
 }
 
+void orc_scene_update(orc_scene* h, float dt) {
+    /* Scene::update / GPUScene::update (scene.cpp:53-59, 267-282): rotate
+     * instance 3 by 1.0*dt about WORLD_UP (camera.h:9), setTransform (inverse,
+     * bounds, area, bvh.cpp:524-531), then BvhTLAS::refit (bvh.cpp:793-819):
+     * leaves re-derive their instances' bounds and GROW their box (no reset,
+     * updateNodeBounds :933-944), interior nodes take min/max of children. */
+    Scene& S = *h->s;
+    Instance& in = S.inst[3];
+    in = makeInstance(in.blas, in.mat, rotate(in.M, 1.0f * dt, mk(0.0f, 1.0f, 0.0f)));
+    Bvh& b = S.tlas;
+    for (int64_t i = (int64_t)b.used - 1; i >= 0; --i) {
+        if (i == 1) continue;
+        Node& n = b.nodes[(size_t)i];
+        if (n.cnt != 0) {
+            for (uint32_t k = 0; k < n.cnt; ++k) {
+                Instance& x = S.inst[b.idx[n.lf + k]];
+                x = makeInstance(x.blas, x.mat, x.M);   /* updateInstanceData: same bounds/area recomputation */
+            }
+            for (uint32_t k = 0; k < n.cnt; ++k) grow(n.box, S.inst[b.idx[n.lf + k]].bounds);
+            continue;
+        }
+        const Node& l = b.nodes[n.lf];
+        const Node& r = b.nodes[n.lf + 1];
+        n.box.mn = mk(tmin(l.box.mn.x, r.box.mn.x), tmin(l.box.mn.y, r.box.mn.y), tmin(l.box.mn.z, r.box.mn.z));
+        n.box.mx = mk(tmax(l.box.mx.x, r.box.mx.x), tmax(l.box.mx.y, r.box.mx.y), tmax(l.box.mx.z, r.box.mx.z));
+    }
+}
+
 void orc_path_lengths(orc_scene* h, uint32_t W, uint32_t H, uint32_t frame, uint32_t* out) {
     Scene& S = *h->s;
     if (S.scrW != (float)W || S.scrH != (float)H) setCamera(S, W, H);

@@ -47,6 +47,9 @@ int orc_scene_mesh_tris(const orc_scene*, uint32_t* out, int max);
 uint32_t orc_scene_instance_count(const orc_scene*);
 uint32_t orc_scene_light_count(const orc_scene*);
 
+/* GPUScene::update(dt) (scene.cpp:267-282): rotate instance 3, refit the TLAS. */
+void orc_scene_update(orc_scene*, float dt);
+
 /* Camera of main.cpp:141-149 for a W x H render. */
 void orc_scene_set_camera(orc_scene*, uint32_t width, uint32_t height);
 /* Copy of the CameraUBO (128 B, camera.h:12-19) the camera produces. */

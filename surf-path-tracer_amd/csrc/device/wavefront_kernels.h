@@ -96,6 +96,13 @@ struct DevCamera {
 };
 
 struct Pool { float4* o; float4* d; float4* T; };
+/* Long paths (the reference's Russian roulette keeps some alive for thousands
+ * of segments): k_shade moves a path that reaches Counters::longThresh
+ * segments to an escape queue; k_long, running concurrently with the
+ * wavefront on a second stream, advances them many segments per graph replay. */
+struct LongQueues { Pool esc[3]; Pool lp[2]; };
+/* Where a path that used up its segment budget goes. */
+struct Sink { Pool q; uint32_t* n; uint32_t cap; };
 struct ShadowQ { float4* o; float4* d; float4* c; };
 
 /* Device counters of the sample stream.  Double-buffered by phase parity so no
@@ -109,7 +116,13 @@ struct Counters {
     uint32_t segMax;                 /* longest finished path (extension rays), diagnostics */
     uint32_t survN;                  /* k_tail survivors appended (may exceed survCap) */
     uint32_t survCap;
-    uint32_t _pad;
+    uint32_t longThresh;             /* a continuation with this many segments escapes the wavefront (0 = off) */
+    uint32_t eSel;                   /* escape queue k_shade appends to (host rotates it per graph replay) */
+    uint32_t eN[3];                  /* escapes appended to queue q (may exceed eCap) */
+    uint32_t eCap;
+    uint32_t lpN[2];                 /* long-path pool sizes (k_long output, may exceed lpCap) */
+    uint32_t lpCap;
+    uint32_t _pad2;
     unsigned long long issued[2];    /* stream samples issued, per parity */
     unsigned long long limit;        /* host-written issue limit (frame window) */
     unsigned long long baseFrame;    /* absolute frame index of stream frame 0 */
@@ -767,7 +780,7 @@ template <bool LDS_TABLES>
 __global__ __launch_bounds__(kBlock, SURF_SHADE_WAVES) void k_shade(DevScene S, Pool cur, Pool nxt, const float4* __restrict__ hitTUV,
                                                   const uint32_t* __restrict__ hitInst, ShadowQ Q,
                                                   float4* __restrict__ rad, uint32_t* __restrict__ frameDone,
-                                                  uint32_t npx, uint32_t window, Counters* C, int par) {
+                                                  uint32_t npx, uint32_t window, Counters* C, int par, LongQueues LQ) {
     __shared__ DevInstance sInst[LDS_TABLES ? kLdsInst : 1];
     __shared__ DevMaterial sMat[LDS_TABLES ? kLdsMats : 1];
     __shared__ uint2 sLights[LDS_TABLES ? kLdsLights : 1];
@@ -782,6 +795,8 @@ __global__ __launch_bounds__(kBlock, SURF_SHADE_WAVES) void k_shade(DevScene S, 
     __shared__ uint32_t sBase[2][2];
     const uint32_t n = C->nIn[par];
     const uint32_t maxSeg = C->maxSeg, zeroCutoff = C->zeroCutoff;
+    const uint32_t longThresh = C->longThresh, eSel = C->eSel % 3u, eCap = C->eCap;
+    const Pool eq = LQ.esc[eSel];
     const uint32_t wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
     uint32_t it = 0;
     unsigned long long cHit = 0, cCont = 0, cSh = 0, cAcc = 0;
@@ -798,7 +813,13 @@ __global__ __launch_bounds__(kBlock, SURF_SHADE_WAVES) void k_shade(DevScene S, 
             shadePath(S, Tb, o4, cur.d[i], cur.T[i], hitTUV[i], hitInst[i], maxSeg, zeroCutoff, r);
             if (r.addRad) addRadiance(rad, f2u(o4.w), r.radd);
         }
-        const unsigned long long mCont = __ballot(r.cont), mSh = __ballot(r.shadow);
+        /* a path reaching longThresh segments leaves for the k_long worker */
+        bool esc = false;
+        if (r.cont && longThresh != 0u && r.seg + 1u >= longThresh) {
+            const uint32_t k = atomicAdd(&C->eN[eSel], 1u);
+            if (k < eCap) { eq.o[k] = r.o; eq.d[k] = r.d; eq.T[k] = r.T; esc = true; }
+        }
+        const unsigned long long mCont = __ballot(r.cont && !esc), mSh = __ballot(r.shadow);
         if (laneId() == 0) { sWave[it][wv][0] = (uint32_t)__popcll(mCont); sWave[it][wv][1] = (uint32_t)__popcll(mSh); }
         __syncthreads();
         if (threadIdx.x == 0) {
@@ -812,7 +833,7 @@ __global__ __launch_bounds__(kBlock, SURF_SHADE_WAVES) void k_shade(DevScene S, 
         for (uint32_t k = 0; k < wv; ++k) { jc += sWave[it][k][0]; js += sWave[it][k][1]; }
         jc += rankBelow(mCont);
         js += rankBelow(mSh);
-        if (r.cont) { nxt.o[jc] = r.o; nxt.d[jc] = r.d; nxt.T[jc] = r.T; }
+        if (r.cont && !esc) { nxt.o[jc] = r.o; nxt.d[jc] = r.d; nxt.T[jc] = r.T; }
         if (r.shadow) { Q.o[js] = r.so; Q.d[js] = r.sd; Q.c[js] = r.sc; }
         /* a path that ends here may still have this phase's shadow ray pending:
          * connect runs before the host reads frameDone (end of the phase). */
@@ -823,7 +844,7 @@ __global__ __launch_bounds__(kBlock, SURF_SHADE_WAVES) void k_shade(DevScene S, 
             if (k < 64) C->capped[k] = f2u(cur.o[i].w);
         }
         cHit += (unsigned long long)__popcll(__ballot(r.hitGeom));
-        cCont += (unsigned long long)__popcll(mCont);
+        cCont += (unsigned long long)__popcll(__ballot(r.cont));
         cSh += (unsigned long long)__popcll(mSh);
         cAcc += (unsigned long long)__popcll(__ballot(r.accd));
     }
@@ -924,27 +945,14 @@ __global__ __launch_bounds__(kBlock) void k_regen(DevCamera cam, Pool nxt, float
  * then the survivors (lens TIR orbits run thousands of segments) one per wave,
  * so no long path shares a wave.  firstCounted: the first extension ray of
  * each input path is already in the event counts (regen counted it). */
-template <bool LDS_TABLES>
-__global__ __launch_bounds__(64) void k_tail(DevScene S, Pool cur, uint32_t n, uint32_t lpw, float4* __restrict__ rad,
-                                             uint32_t* __restrict__ frameDone, uint32_t npx, uint32_t window, Counters* C,
-                                             uint32_t stackWords, uint32_t firstCounted, uint32_t budget, Pool surv) {
-    extern __shared__ uint32_t lds[];
-    const TraceTables Tt = traceTables<LDS_TABLES>(S, lds, stackWords);
-    __shared__ DevInstance sInst[LDS_TABLES ? kLdsInst : 1];
-    __shared__ DevMaterial sMat[LDS_TABLES ? kLdsMats : 1];
-    __shared__ uint2 sLights[LDS_TABLES ? kLdsLights : 1];
-    ShadeTables Tb{S.inst, S.mats, S.lights};
-    if (LDS_TABLES) {
-        stageTables(S, sInst, sMat, sLights);
-        Tb = ShadeTables{sInst, sMat, sLights};
-    }
-    const uint32_t lane = threadIdx.x;
-    const uint32_t i = blockIdx.x * lpw + lane;
-    if (lane >= lpw || i >= n) return;
-    uint32_t* stk = lds + threadIdx.x;
-    const uint32_t stride = blockDim.x;
+/* One path run to its end (or for `budget` segments, after which the
+ * continuation goes to `sink`): extend -> shade -> connect per segment with
+ * the wavefront kernels' device functions.  Returns whether the path ended. */
+__device__ __forceinline__ bool runPath(const DevScene& S, const TraceTables& Tt, const ShadeTables& Tb, float4 o4, float4 d4,
+                                        float4 T4, uint32_t budget, const Sink& sink, float4* __restrict__ rad,
+                                        uint32_t* __restrict__ frameDone, uint32_t npx, uint32_t window, Counters* C,
+                                        uint32_t* stk, uint32_t stride, uint32_t firstCounted) {
     const uint32_t maxSeg = C->maxSeg, zeroCutoff = C->zeroCutoff;
-    float4 o4 = cur.o[i], d4 = cur.d[i], T4 = cur.T[i];
     const uint32_t slot = f2u(o4.w) / npx;
     unsigned long long nExt = 0, nHit = 0, nCont = 0, nSh = 0, nAcc = 0, nUn = 0;
     bool done = true;
@@ -973,10 +981,9 @@ __global__ __launch_bounds__(64) void k_tail(DevScene S, Pool cur, uint32_t n, u
         if (!r.cont) { atomicMax(&C->segMax, r.seg); break; }
         ++nCont;
         if (budget != 0u && nExt >= budget) {
-            /* survivor: hand the continuation to the one-path-per-wave stage */
-            const uint32_t k = atomicAdd(&C->survN, 1u);
-            if (k < C->survCap) {
-                surv.o[k] = r.o; surv.d[k] = r.d; surv.T[k] = r.T;
+            const uint32_t k = atomicAdd(sink.n, 1u);
+            if (k < sink.cap) {
+                sink.q.o[k] = r.o; sink.q.d[k] = r.d; sink.q.T[k] = r.T;
                 done = false;
                 break;
             }
@@ -985,10 +992,68 @@ __global__ __launch_bounds__(64) void k_tail(DevScene S, Pool cur, uint32_t n, u
     }
     const uint32_t st = blockIdx.x % kStripes;
     unsigned long long* ev = C->evS[st];
-    if (done) atomicAdd(&frameDone[st * window + slot], 1u);
+    if (done) {
+        __threadfence();          /* radiance before completion: other streams' kernels read it */
+        atomicAdd(&frameDone[st * window + slot], 1u);
+    }
     atomicAdd(&ev[0], nExt - (unsigned long long)firstCounted); atomicAdd(&ev[1], nHit); atomicAdd(&ev[2], nCont);
     atomicAdd(&ev[3], nSh); atomicAdd(&ev[4], nAcc); atomicAdd(&ev[5], nUn);
     if (done) atomicAdd(&ev[6], 1ull);
+    return done;
+}
+
+/* Finishes the last paths of the stream: one kernel, each active lane runs its
+ * path (extend -> shade -> connect per segment), so the long Russian-roulette
+ * tail pays no per-bounce launch.  lanes < lpw of each wave work.  With a
+ * budget, paths still alive after `budget` segments go to `surv` for the next
+ * drain stage.  firstCounted: the first extension ray of each input path is
+ * already in the event counts (regen counted it). */
+template <bool LDS_TABLES>
+__global__ __launch_bounds__(64) void k_tail(DevScene S, Pool cur, uint32_t n, uint32_t lpw, float4* __restrict__ rad,
+                                             uint32_t* __restrict__ frameDone, uint32_t npx, uint32_t window, Counters* C,
+                                             uint32_t stackWords, uint32_t firstCounted, uint32_t budget, Pool surv) {
+    extern __shared__ uint32_t lds[];
+    const TraceTables Tt = traceTables<LDS_TABLES>(S, lds, stackWords);
+    __shared__ DevInstance sInst[LDS_TABLES ? kLdsInst : 1];
+    __shared__ DevMaterial sMat[LDS_TABLES ? kLdsMats : 1];
+    __shared__ uint2 sLights[LDS_TABLES ? kLdsLights : 1];
+    ShadeTables Tb{S.inst, S.mats, S.lights};
+    if (LDS_TABLES) {
+        stageTables(S, sInst, sMat, sLights);
+        Tb = ShadeTables{sInst, sMat, sLights};
+    }
+    const uint32_t lane = threadIdx.x;
+    const uint32_t i = blockIdx.x * lpw + lane;
+    if (lane >= lpw || i >= n) return;
+    runPath(S, Tt, Tb, cur.o[i], cur.d[i], cur.T[i], budget, Sink{surv, &C->survN, C->survCap}, rad, frameDone, npx, window, C,
+            lds + threadIdx.x, blockDim.x, firstCounted);
+}
+
+/* Long-path worker (second stream, concurrent with a graph replay): advances
+ * every path of lp[in] and of escape queue `es` by up to `budget` segments;
+ * paths still alive go to lp[out].  Grid-stride over both inputs. */
+template <bool LDS_TABLES>
+__global__ __launch_bounds__(64) void k_long(DevScene S, LongQueues LQ, uint32_t in, uint32_t es, float4* __restrict__ rad,
+                                             uint32_t* __restrict__ frameDone, uint32_t npx, uint32_t window, Counters* C,
+                                             uint32_t stackWords, uint32_t budget) {
+    extern __shared__ uint32_t lds[];
+    const TraceTables Tt = traceTables<LDS_TABLES>(S, lds, stackWords);
+    __shared__ DevInstance sInst[LDS_TABLES ? kLdsInst : 1];
+    __shared__ DevMaterial sMat[LDS_TABLES ? kLdsMats : 1];
+    __shared__ uint2 sLights[LDS_TABLES ? kLdsLights : 1];
+    ShadeTables Tb{S.inst, S.mats, S.lights};
+    if (LDS_TABLES) {
+        stageTables(S, sInst, sMat, sLights);
+        Tb = ShadeTables{sInst, sMat, sLights};
+    }
+    const uint32_t nLp = min(C->lpN[in], C->lpCap), nEs = min(C->eN[es], C->eCap);
+    const Sink sink{LQ.lp[in ^ 1u], &C->lpN[in ^ 1u], C->lpCap};
+    for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < nLp + nEs; v += gridDim.x * blockDim.x) {
+        const Pool& src = v < nLp ? LQ.lp[in] : LQ.esc[es];
+        const uint32_t k = v < nLp ? v : v - nLp;
+        runPath(S, Tt, Tb, src.o[k], src.d[k], src.T[k], budget, sink, rad, frameDone, npx, window, C, lds + threadIdx.x,
+                blockDim.x, 0u);
+    }
 }
 
 /* Cooperative tail: one path per 64-lane wave (block), for the few very long
@@ -1052,6 +1117,7 @@ __global__ __launch_bounds__(64) void k_tail_coop(DevScene S, Pool cur, uint32_t
     if (lead) {
         const uint32_t st = blockIdx.x % kStripes;
         unsigned long long* ev = C->evS[st];
+        __threadfence();
         atomicAdd(&frameDone[st * window + slot], 1u);
         atomicAdd(&ev[0], nExt - (unsigned long long)firstCounted); atomicAdd(&ev[1], nHit); atomicAdd(&ev[2], nCont);
         atomicAdd(&ev[3], nSh); atomicAdd(&ev[4], nAcc); atomicAdd(&ev[5], nUn);

@@ -37,9 +37,13 @@ void WaveFrontRenderer::clearAccumulator() {
 }
 
 void WaveFrontRenderer::render(F32 /*deltaTime*/) {
-    if (m_scene.generation() != m_sceneGeneration) {     /* GPUScene::update re-upload, scene.cpp:267-282 */
+    if (m_scene.generation() != m_sceneGeneration) {
+        /* GPUScene::update (scene.cpp:267-282) re-uploads the instance records,
+         * TLAS indices and TLAS nodes; geometry and BLASes stay resident */
         const surf_scene_desc desc = m_scene.descriptor();
-        check(surf_upload_scene(m_ctx, &desc), m_ctx, "surf_upload_scene");
+        if (surf_update_instances(m_ctx, desc.instances, desc.instance_count, desc.tlas_indices, desc.tlas_nodes,
+                                  desc.tlas_node_count, desc.lights, desc.light_count) != SURF_OK)
+            check(surf_upload_scene(m_ctx, &desc), m_ctx, "surf_upload_scene");
         m_sceneGeneration = m_scene.generation();
     }
     const CameraUBO ubo = m_camera.toUBO();

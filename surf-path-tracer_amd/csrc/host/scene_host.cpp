@@ -721,6 +721,12 @@ int surf_scene_build_indoor(const char* assets_dir, int variant, surf_scene** ou
     return SURF_OK;
 }
 
+int surf_scene_update(surf_scene* scene, float delta_time) {
+    if (!scene) return SURF_ERR_INVALID;
+    scene->scene->update(delta_time);   /* scene.cpp:267-282: rotate instance 3 about WORLD_UP, TLAS refit, re-batch */
+    return SURF_OK;
+}
+
 int surf_scene_desc_get(const surf_scene* scene, surf_scene_desc* out) {
     if (!scene || !out) return SURF_ERR_INVALID;
     *out = scene->scene->descriptor();

@@ -14,7 +14,10 @@
 #include <cstdio>
 #include <cstring>
 #include <cfloat>
+#include <array>
+#include <map>
 #include <mutex>
+#include <tuple>
 #include <string>
 #include <vector>
 
@@ -61,6 +64,9 @@ struct surf_ctx {
     std::vector<void*> sceneAllocs;
     uint32_t stackDepth = 0;
     uint32_t nInstances = 0, nTriangles = 0;
+    /* what surf_update_instances may change: instance records, TLAS, lights */
+    uint32_t nMaterials = 0, nLightsUp = 0, tlasNodeCount = 0, maxBlasDepth = 0;
+    std::map<std::tuple<uint32_t, uint32_t, uint32_t>, std::array<float4, 4>> blasRoots;  /* (node, idx, tri offset) -> root record */
     /* camera */
     bool hasCamera = false;
     DevCamera cam{};
@@ -98,6 +104,15 @@ struct surf_ctx {
     uint32_t coopMax = 0;          /* survivors handled by the cooperative tail (one path per wave) */
     bool coopEligible = false;     /* single-leaf TLAS of <= 64 instances, LDS tables */
     int traceMode = 0;             /* surf_trace_closest/_any: 0 one ray per lane, 1 one ray per wave */
+    /* long paths: escape queues + long-path pools, advanced by k_long on stream2 */
+    uint32_t longThresh = 0;       /* escape length (surf_set_long_paths; 0 = off: measured slower) */
+    uint32_t longBudget = 64;      /* segments per path per k_long launch */
+    uint32_t longGrid = 0;         /* k_long workgroups (64 lanes) */
+    hipStream_t stream2 = nullptr;
+    hipEvent_t evG[3] = {}, evL[3] = {};
+    LongQueues LQ{};
+    uint32_t eCap = 0, lpCap = 0;
+    uint64_t replay = 0;           /* graph replays of the current stream */
     uint32_t tailLanes = 0;
     uint32_t segMaxBase = 0;       /* longest path of finished streams */
 
@@ -238,6 +253,18 @@ int allocWavefront(surf_ctx* c) {
         if ((rc = devAlloc(c, c->wfAllocs, &c->pool[p].d, cap))) return rc;
         if ((rc = devAlloc(c, c->wfAllocs, &c->pool[p].T, cap))) return rc;
     }
+    c->eCap = (uint32_t)std::min<size_t>(std::max<size_t>(cap / 32, 4096), 1u << 18);
+    c->lpCap = (uint32_t)std::min<size_t>(std::max<size_t>(cap / 8, 4096), 1u << 20);
+    for (int q = 0; q < 3; ++q) {
+        if ((rc = devAlloc(c, c->wfAllocs, &c->LQ.esc[q].o, c->eCap))) return rc;
+        if ((rc = devAlloc(c, c->wfAllocs, &c->LQ.esc[q].d, c->eCap))) return rc;
+        if ((rc = devAlloc(c, c->wfAllocs, &c->LQ.esc[q].T, c->eCap))) return rc;
+    }
+    for (int q = 0; q < 2; ++q) {
+        if ((rc = devAlloc(c, c->wfAllocs, &c->LQ.lp[q].o, c->lpCap))) return rc;
+        if ((rc = devAlloc(c, c->wfAllocs, &c->LQ.lp[q].d, c->lpCap))) return rc;
+        if ((rc = devAlloc(c, c->wfAllocs, &c->LQ.lp[q].T, c->lpCap))) return rc;
+    }
     c->survCap = (uint32_t)std::min<size_t>(std::max<size_t>(cap / 16, 4096), 1u << 18);
     for (int q = 0; q < 2; ++q) {
         if ((rc = devAlloc(c, c->wfAllocs, &c->surv[q].o, c->survCap))) return rc;
@@ -264,6 +291,7 @@ int allocWavefront(surf_ctx* c) {
     const uint64_t maxBlocks = (cap + kBlock - 1) / kBlock;
     c->gridWork = (uint32_t)std::min<uint64_t>(maxBlocks, (uint64_t)cus * 8);
     c->coopMax = (uint32_t)cus * 8;     /* 2 waves per SIMD of the cooperative tail */
+    c->longGrid = (uint32_t)cus;        /* one k_long wave per CU: the wavefront keeps the rest */
     c->gridRegen = (uint32_t)std::min<uint64_t>(maxBlocks, (uint64_t)cus * 8);
     c->allocated = true;
     return SURF_OK;
@@ -286,10 +314,10 @@ void launchPhase(surf_ctx* c, int par, hipEvent_t* ev) {
     if (ev) (void)hipEventRecord(ev[1], c->stream);
     if (c->ldsTables)
         hipLaunchKernelGGL(k_shade<true>, dim3(c->gridWork), dim3(kBlock), 0, c->stream, c->S, c->pool[par], c->pool[par ^ 1],
-                           c->hitTUV, (const uint32_t*)c->hitInst, c->Q, c->rad, c->frameDone, c->npx, c->window, c->ctr, par);
+                           c->hitTUV, (const uint32_t*)c->hitInst, c->Q, c->rad, c->frameDone, c->npx, c->window, c->ctr, par, c->LQ);
     else
         hipLaunchKernelGGL(k_shade<false>, dim3(c->gridWork), dim3(kBlock), 0, c->stream, c->S, c->pool[par], c->pool[par ^ 1],
-                           c->hitTUV, (const uint32_t*)c->hitInst, c->Q, c->rad, c->frameDone, c->npx, c->window, c->ctr, par);
+                           c->hitTUV, (const uint32_t*)c->hitInst, c->Q, c->rad, c->frameDone, c->npx, c->window, c->ctr, par, c->LQ);
     if (ev) (void)hipEventRecord(ev[2], c->stream);
     if (c->ldsTables)
         hipLaunchKernelGGL(k_connect<true>, dim3(c->gridWork), dim3(kBlock), lds, c->stream, c->S, c->Q, c->rad, c->ctr, par, sw);
@@ -318,10 +346,14 @@ int startStream(surf_ctx* c, uint64_t baseFrame, uint32_t maxSeg) {
     h.zeroCutoff = c->zeroCutoff ? 1u : 0u;
     h.baseFrame = baseFrame;
     h.survCap = c->survCap;
+    h.longThresh = c->longThresh;
+    h.eCap = c->eCap;
+    h.lpCap = c->lpCap;
     *c->hctr = h;
     SURF_CHECK(c, hipMemcpyAsync(c->ctr, c->hctr, sizeof(Counters), hipMemcpyHostToDevice, c->stream));
     SURF_CHECK(c, hipMemsetAsync(c->frameDone, 0, (size_t)kStripes * c->window * sizeof(uint32_t), c->stream));
     c->streamActive = true;
+    c->replay = 0;
     c->baseFrame = baseFrame;
     c->targetFrames = 0;
     c->accFrames = 0;
@@ -382,7 +414,35 @@ int syncAndAccumulate(surf_ctx* c) {
 
 /* One unit of forward progress: kPhasesPerGraph phases (graph replay, or
  * direct launches with per-kernel events when profiling). */
+/* k_long for replay j (j >= 1), on stream2 after graph j-1 (whose escapes it
+ * consumes): lp[j%2] + esc[(j-1)%3] -> lp[(j+1)%2]. */
+int launchLong(surf_ctx* c, uint64_t j) {
+    const uint32_t in = (uint32_t)(j & 1u), es = (uint32_t)((j - 1) % 3);
+    SURF_CHECK(c, hipStreamWaitEvent(c->stream2, c->evG[(j - 1) % 3], 0));
+    SURF_CHECK(c, hipMemsetAsync(&c->ctr->lpN[in ^ 1u], 0, sizeof(uint32_t), c->stream2));
+    const size_t lds = traversalLds(c, 64);
+    if (c->ldsTables)
+        hipLaunchKernelGGL(k_long<true>, dim3(c->longGrid), dim3(64), lds, c->stream2, c->S, c->LQ, in, es, c->rad, c->frameDone,
+                           c->npx, c->window, c->ctr, stackWords(c, 64), c->longBudget);
+    else
+        hipLaunchKernelGGL(k_long<false>, dim3(c->longGrid), dim3(64), lds, c->stream2, c->S, c->LQ, in, es, c->rad, c->frameDone,
+                           c->npx, c->window, c->ctr, stackWords(c, 64), c->longBudget);
+    SURF_CHECK(c, hipGetLastError());
+    SURF_CHECK(c, hipEventRecord(c->evL[j % 3], c->stream2));
+    return SURF_OK;
+}
+
 int advance(surf_ctx* c) {
+    const uint64_t j = c->replay;
+    const bool lng = c->longThresh != 0;
+    if (lng) {
+        /* esc[j%3] is free once k_long(j-2) -- its last reader -- has finished */
+        if (j >= 2) SURF_CHECK(c, hipStreamWaitEvent(c->stream, c->evL[(j - 2) % 3], 0));
+        c->hctr->eSel = (uint32_t)(j % 3);
+        c->hctr->eN[j % 3] = 0;
+        SURF_CHECK(c, hipMemcpyAsync(&c->ctr->eSel, &c->hctr->eSel, sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+        SURF_CHECK(c, hipMemcpyAsync(&c->ctr->eN[j % 3], &c->hctr->eN[j % 3], sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+    }
     if (c->profiling) {
         for (int ph = 0; ph < kPhasesPerGraph; ++ph) launchPhase(c, ph & 1, &c->pev[4 * ph]);
         SURF_CHECK(c, hipGetLastError());
@@ -396,6 +456,14 @@ int advance(surf_ctx* c) {
     } else {
         SURF_CHECK(c, hipGraphLaunch(c->graphExec, c->stream));
     }
+    if (lng) {
+        SURF_CHECK(c, hipEventRecord(c->evG[j % 3], c->stream));
+        if (j >= 1) {
+            const int rc = launchLong(c, j);
+            if (rc) return rc;
+        }
+    }
+    c->replay = j + 1;
     c->stats.iterations += kPhasesPerGraph;
     if (c->stats.iterations > kMaxIterations)
         return fail(c, SURF_ERR_LIMIT, "wavefront did not drain after " + std::to_string(c->stats.iterations) + " iterations");
@@ -422,7 +490,42 @@ void launchTail(surf_ctx* c, Pool in, uint32_t n, uint32_t lpw, uint32_t firstCo
  * reference's Russian-roulette survivors that run for thousands of segments),
  * the cooperative tail runs each on a whole wave, which cuts the latency of a
  * segment -- the quantity the last paths of a drain are bound by. */
+/* Drain: the long paths still held by k_long's pool and by the last replay's
+ * escape queue join pool 0, so the staged tail finishes one population.  They
+ * have not had their next extension ray counted (regen counts pool paths'). */
+int mergeLongPaths(surf_ctx* c) {
+    if (c->longThresh == 0 || c->replay == 0) return SURF_OK;
+    SURF_CHECK(c, hipStreamSynchronize(c->stream2));
+    SURF_CHECK(c, hipMemcpyAsync(c->hctr, c->ctr, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
+    SURF_CHECK(c, hipStreamSynchronize(c->stream));
+    const uint64_t j = c->replay;                       /* k_long(j-1) wrote lp[j%2]; esc[(j-1)%3] unconsumed */
+    const uint32_t lpIdx = (uint32_t)(j & 1u), es = (uint32_t)((j - 1) % 3);
+    const uint32_t nLp = j >= 2 ? std::min(c->hctr->lpN[lpIdx], c->lpCap) : 0u;
+    const uint32_t nE = std::min(c->hctr->eN[es], c->eCap);
+    uint32_t at = c->hctr->nIn[0];
+    if ((uint64_t)at + nLp + nE > c->capacity) return fail(c, SURF_ERR_LIMIT, "long paths exceed the pool at drain");
+    auto append = [&](const Pool& src, uint32_t n) -> int {
+        if (!n) return SURF_OK;
+        SURF_CHECK(c, hipMemcpyAsync(c->pool[0].o + at, src.o, n * sizeof(float4), hipMemcpyDeviceToDevice, c->stream));
+        SURF_CHECK(c, hipMemcpyAsync(c->pool[0].d + at, src.d, n * sizeof(float4), hipMemcpyDeviceToDevice, c->stream));
+        SURF_CHECK(c, hipMemcpyAsync(c->pool[0].T + at, src.T, n * sizeof(float4), hipMemcpyDeviceToDevice, c->stream));
+        at += n;
+        return SURF_OK;
+    };
+    int rc;
+    if ((rc = append(c->LQ.lp[lpIdx], nLp)) || (rc = append(c->LQ.esc[es], nE))) return rc;
+    c->evBase[0] += (uint64_t)nLp + nE;                 /* runTail counts their first extension as already counted */
+    c->hctr->nIn[0] = at;
+    c->hctr->lpN[0] = c->hctr->lpN[1] = 0;
+    c->hctr->eN[0] = c->hctr->eN[1] = c->hctr->eN[2] = 0;
+    SURF_CHECK(c, hipMemcpyAsync(c->ctr, c->hctr, sizeof(Counters), hipMemcpyHostToDevice, c->stream));
+    c->replay = 0;                                      /* no k_long work left; a later replay restarts the ring */
+    return SURF_OK;
+}
+
 int runTail(surf_ctx* c) {
+    int rc0 = mergeLongPaths(c);
+    if (rc0) return rc0;
     const uint32_t n = c->hctr->nIn[0];
     if (n == 0) return SURF_OK;
     if (c->profiling) SURF_CHECK(c, hipEventRecord(c->pev[0], c->stream));
@@ -477,7 +580,8 @@ int pump(surf_ctx* c, bool drain) {
     const uint64_t target = c->targetFrames * (uint64_t)c->npx;
     for (;;) {
         const uint64_t issued = c->hctr->issued[0];
-        const uint32_t inflight = c->hctr->nIn[0];
+        /* k_long's paths count as in flight until the drain merges them */
+        const uint32_t inflight = c->hctr->nIn[0] + ((c->longThresh && c->replay) ? 1u : 0u);
         if (!drain && issued >= target) return SURF_OK;
         if (drain && c->accFrames >= c->targetFrames) return SURF_OK;
         const bool starved = issued >= c->pushedLimit;     /* nothing more may be issued right now */
@@ -517,6 +621,7 @@ int ensureDrained(surf_ctx* c) {
 int endStream(surf_ctx* c) {
     int rc = ensureDrained(c);
     if (rc) return rc;
+    if (c->stream2) SURF_CHECK(c, hipStreamSynchronize(c->stream2));
     if (c->streamActive) {
         unsigned long long e[8];
         streamEvents(*c->hctr, e);
@@ -557,7 +662,14 @@ int createCtx(int dev, uint32_t w, uint32_t h, std::vector<uint32_t> rows, surf_
     c->height = h;
     c->rows = std::move(rows);
     c->npx = (uint32_t)(w * c->rows.size());
-    if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+    bool evOk = true;
+    if (hipSetDevice(dev) == hipSuccess) {
+        for (int k = 0; k < 3; ++k)
+            evOk = evOk && hipEventCreateWithFlags(&c->evG[k], hipEventDisableTiming) == hipSuccess &&
+                   hipEventCreateWithFlags(&c->evL[k], hipEventDisableTiming) == hipSuccess;
+    }
+    if (!evOk || hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
         delete c;
         return fail(nullptr, SURF_ERR_HIP, "stream/event creation failed");
@@ -612,7 +724,13 @@ void surf_destroy(surf_ctx* c) {
     if (c->dRows) (void)hipFree(c->dRows);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->stream2) (void)hipStreamSynchronize(c->stream2);
     if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->stream2) (void)hipStreamDestroy(c->stream2);
+    for (int k = 0; k < 3; ++k) {
+        if (c->evG[k]) (void)hipEventDestroy(c->evG[k]);
+        if (c->evL[k]) (void)hipEventDestroy(c->evL[k]);
+    }
     delete c;
 }
 
@@ -669,6 +787,17 @@ int surf_set_tail_policy(surf_ctx* c, uint32_t threshold_paths, uint32_t lanes_p
     return SURF_OK;
 }
 
+int surf_set_long_paths(surf_ctx* c, uint32_t escape_segments, uint32_t budget) {
+    if (!c) return fail(nullptr, SURF_ERR_INVALID, "ctx is NULL");
+    if (escape_segments != 0 && budget == 0) return fail(c, SURF_ERR_INVALID, "budget must be > 0");
+    SURF_CHECK(c, hipSetDevice(c->device));
+    const int rc = endStream(c);
+    if (rc) return rc;
+    c->longThresh = escape_segments;
+    c->longBudget = budget;
+    return SURF_OK;
+}
+
 int surf_set_trace_mode(surf_ctx* c, int mode) {
     if (!c) return fail(nullptr, SURF_ERR_INVALID, "ctx is NULL");
     if (mode != 0 && mode != 1) return fail(c, SURF_ERR_INVALID, "trace mode must be 0 or 1");
@@ -690,6 +819,65 @@ int surf_set_profiling(surf_ctx* c, int enabled) {
     int rc = endStream(c);
     if (rc) return rc;
     c->profiling = enabled != 0;
+    return SURF_OK;
+}
+
+/* Instance-dependent tables (GPUScene::update re-uploads exactly these,
+ * scene.cpp:267-282): DevInstance + TraceInst per instance, the TLAS node
+ * records and index array, the light list.  BLAS roots come from the upload. */
+struct InstanceTables {
+    std::vector<DevInstance> inst;
+    std::vector<TraceInst> tinst;
+    std::vector<float4> tnodes;
+    std::vector<uint32_t> tidx;
+    std::vector<uint2> lights;
+    uint32_t tlasDepth = 0, tlasLeafCount = 0;
+};
+
+int buildInstanceTables(surf_ctx* c, const surf_gpu_instance* instances, uint32_t n, const uint32_t* tlasIdx,
+                        const surf_bvh_node* tlasNodes, uint32_t nTlas, const surf_light* lights, uint32_t nLights, InstanceTables& T) {
+    auto affine = [](const float* m) { return m[3] == 0.0f && m[7] == 0.0f && m[11] == 0.0f && m[15] == 1.0f; };
+    T.inst.resize(n);
+    T.tinst.resize(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        const surf_gpu_instance& g = instances[i];
+        const auto root = c->blasRoots.find(std::make_tuple(g.bvh_node_offset, g.bvh_idx_offset, g.tri_offset));
+        if (root == c->blasRoots.end() || g.material_offset >= c->nMaterials)
+            return fail(c, SURF_ERR_INVALID, "instance " + std::to_string(i) + ": offsets do not name an uploaded BLAS/material");
+        DevInstance& D = T.inst[i];
+        std::memcpy(D.Minv, g.inv_transform, sizeof D.Minv);
+        std::memcpy(D.M, g.transform, sizeof D.M);
+        D.triOffset = g.tri_offset; D.idxOffset = g.bvh_idx_offset; D.nodeOffset = g.bvh_node_offset; D.material = g.material_offset;
+        D.area = g.area;
+        /* row 3 of a column-major matrix: elements 3, 7, 11, 15 */
+        D.affineInv = affine(g.inv_transform) ? 1u : 0u;
+        D.affine = affine(g.transform) ? 1u : 0u;
+        const float* m = D.Minv;
+        TraceInst& R = T.tinst[i];
+        R.m0 = make_float4(m[0], m[4], m[8], m[12]);
+        R.m1 = make_float4(m[1], m[5], m[9], m[13]);
+        R.m2 = make_float4(m[2], m[6], m[10], m[14]);
+        R.m3 = make_float4(m[3], m[7], m[11], m[15]);
+        R.meta = make_uint4(D.nodeOffset, D.idxOffset, D.affineInv, i);
+        R.r0 = root->second[0]; R.r1 = root->second[1]; R.r2 = root->second[2]; R.r3 = root->second[3];
+    }
+    T.tnodes.assign((size_t)nTlas * 4, make_float4(0, 0, 0, 0));
+    std::vector<uint8_t> tseen(n, 0);
+    TreeWalk tw = walkTree(tlasNodes, nTlas, 0, n, 0, T.tnodes, tseen);
+    if (!tw.ok) return fail(c, SURF_ERR_INVALID, "TLAS: " + tw.why);
+    T.tlasDepth = tw.depth;
+    T.tidx.assign(tlasIdx, tlasIdx + n);
+    for (uint32_t v : T.tidx) if (v >= n) return fail(c, SURF_ERR_INVALID, "TLAS index out of range");
+    T.tlasLeafCount = tlasNodes[0].count;        /* root leaf: wave-uniform instance loop */
+    if (T.tlasLeafCount && tlasNodes[0].left_first != 0) T.tlasLeafCount = 0;   /* general path unless indices start at 0 */
+    T.lights.resize(nLights);
+    for (uint32_t l = 0; l < nLights; ++l) {
+        const surf_light& L = lights[l];
+        if (L.light_instance_idx >= n || L.primitive_count == 0 ||
+            (uint64_t)instances[L.light_instance_idx].tri_offset + L.primitive_count > c->nTriangles)
+            return fail(c, SURF_ERR_INVALID, "light " + std::to_string(l) + " out of range");
+        T.lights[l] = make_uint2(L.light_instance_idx, L.primitive_count);
+    }
     return SURF_OK;
 }
 
@@ -741,6 +929,14 @@ int surf_upload_scene(surf_ctx* c, const surf_scene_desc* d) {
                 }
         }
     }
+    c->blasRoots.clear();
+    for (uint32_t i = 0; i < d->instance_count; ++i) {
+        const surf_gpu_instance& g = d->instances[i];
+        const size_t r = 4 * (size_t)g.bvh_node_offset;
+        c->blasRoots[std::make_tuple(g.bvh_node_offset, g.bvh_idx_offset, g.tri_offset)] = {nodes[r], nodes[r + 1], nodes[r + 2], nodes[r + 3]};
+    }
+    c->nTriangles = d->triangle_count;
+    c->nMaterials = d->material_count;
     /* BVH-ordered triangles: (v0, prim), e1 = v1 - v0, e2 = v2 - v0 (mesh.cpp:25-26) */
     std::vector<float4> tris((size_t)d->blas_index_count * 3, make_float4(0, 0, 0, 0));
     for (uint32_t k = 0; k < d->blas_index_count; ++k) {
@@ -764,38 +960,14 @@ int surf_upload_scene(surf_ctx* c, const surf_scene_desc* d) {
         verts[4 * (size_t)t + 2] = make_float4(T.v2.x, T.v2.y, T.v2.z, 0.0f);
         verts[4 * (size_t)t + 3] = make_float4(T.centroid.x, T.centroid.y, T.centroid.z, 0.0f);
     }
-    /* TLAS */
-    std::vector<float4> tnodes((size_t)d->tlas_node_count * 4, make_float4(0, 0, 0, 0));
-    std::vector<uint8_t> tseen(d->instance_count, 0);
-    TreeWalk tw = walkTree(d->tlas_nodes, d->tlas_node_count, 0, d->instance_count, 0, tnodes, tseen);
-    if (!tw.ok) return fail(c, SURF_ERR_INVALID, "TLAS: " + tw.why);
-    std::vector<uint32_t> tidx(d->tlas_indices, d->tlas_indices + d->instance_count);
-    for (uint32_t v : tidx) if (v >= d->instance_count) return fail(c, SURF_ERR_INVALID, "TLAS index out of range");
-    std::vector<uint2> lights(d->light_count);
-    for (uint32_t l = 0; l < d->light_count; ++l) {
-        const surf_light& L = d->lights[l];
-        if (L.light_instance_idx >= d->instance_count || L.primitive_count == 0 ||
-            (uint64_t)d->instances[L.light_instance_idx].tri_offset + L.primitive_count > d->triangle_count)
-            return fail(c, SURF_ERR_INVALID, "light " + std::to_string(l) + " out of range");
-        lights[l] = make_uint2(L.light_instance_idx, L.primitive_count);
-    }
-    /* traversal records: M^-1 rows, offsets, BLAS root record (TraceInst) */
-    std::vector<TraceInst> tinst(d->instance_count);
-    for (uint32_t i = 0; i < d->instance_count; ++i) {
-        const float* m = inst[i].Minv;
-        TraceInst& T = tinst[i];
-        T.m0 = make_float4(m[0], m[4], m[8], m[12]);
-        T.m1 = make_float4(m[1], m[5], m[9], m[13]);
-        T.m2 = make_float4(m[2], m[6], m[10], m[14]);
-        T.m3 = make_float4(m[3], m[7], m[11], m[15]);
-        T.meta = make_uint4(inst[i].nodeOffset, inst[i].idxOffset, inst[i].affineInv, i);
-        const size_t r = 4 * (size_t)inst[i].nodeOffset;
-        T.r0 = nodes[r]; T.r1 = nodes[r + 1]; T.r2 = nodes[r + 2]; T.r3 = nodes[r + 3];
-    }
+    InstanceTables IT;
+    int rcT = buildInstanceTables(c, d->instances, d->instance_count, d->tlas_indices, d->tlas_nodes, d->tlas_node_count,
+                                  d->lights, d->light_count, IT);
+    if (rcT) return rcT;
     std::vector<DevMaterial> mats(d->material_count);
     std::memcpy(mats.data(), d->materials, d->material_count * sizeof(DevMaterial));
 
-    const uint32_t depth = tw.depth + maxBlasDepth + 1;
+    const uint32_t depth = IT.tlasDepth + maxBlasDepth + 1;
     if (depth > kMaxStack) return fail(c, SURF_ERR_LIMIT, "BVH too deep for the LDS traversal stack (" + std::to_string(depth) + " entries)");
 
     DevScene S{};
@@ -804,20 +976,19 @@ int surf_upload_scene(surf_ctx* c, const surf_scene_desc* d) {
     if ((rc = upload(c, tris, &S.tris))) return rc;
     if ((rc = upload(c, normals, &S.normals))) return rc;
     if ((rc = upload(c, verts, &S.verts))) return rc;
-    if ((rc = upload(c, tnodes, &S.tlasNodes))) return rc;
-    if ((rc = upload(c, tidx, &S.tlasIdx))) return rc;
-    if ((rc = upload(c, inst, &S.inst))) return rc;
-    if ((rc = upload(c, tinst, &S.tinst))) return rc;
+    if ((rc = upload(c, IT.tnodes, &S.tlasNodes))) return rc;
+    if ((rc = upload(c, IT.tidx, &S.tlasIdx))) return rc;
+    if ((rc = upload(c, IT.inst, &S.inst))) return rc;
+    if ((rc = upload(c, IT.tinst, &S.tinst))) return rc;
     if ((rc = upload(c, mats, &S.mats))) return rc;
-    if ((rc = upload(c, lights, &S.lights))) return rc;
+    if ((rc = upload(c, IT.lights, &S.lights))) return rc;
     S.nLights = d->light_count;
     S.nInst = d->instance_count;
     S.nMats = d->material_count;
     S.finiteBoxes = 1u;
     for (const float4& q : nodes)
         if (!(std::fabs(q.x) <= FLT_MAX && std::fabs(q.y) <= FLT_MAX && std::fabs(q.z) <= FLT_MAX)) { S.finiteBoxes = 0u; break; }
-    S.tlasLeafCount = d->tlas_nodes[0].count;   /* root leaf: wave-uniform instance loop */
-    if (S.tlasLeafCount && d->tlas_nodes[0].left_first != 0) S.tlasLeafCount = 0;   /* general path unless indices start at 0 */
+    S.tlasLeafCount = IT.tlasLeafCount;
     const surf_background& bg = *d->background;
     S.bgType = bg.type;
     S.bgColor[0] = bg.color.x; S.bgColor[1] = bg.color.y; S.bgColor[2] = bg.color.z;
@@ -829,15 +1000,40 @@ int surf_upload_scene(surf_ctx* c, const surf_scene_desc* d) {
     c->coopEligible = c->ldsTables && S.tlasLeafCount > 0 && S.tlasLeafCount <= 64;
     c->stackDepth = depth;
     c->nInstances = d->instance_count;
-    c->nTriangles = d->triangle_count;
+    c->nLightsUp = d->light_count;
+    c->tlasNodeCount = d->tlas_node_count;
+    c->maxBlasDepth = maxBlasDepth;
     c->hasScene = true;
     return SURF_OK;
 }
 
 int surf_update_instances(surf_ctx* c, const surf_gpu_instance* instances, uint32_t n, const uint32_t* tlasIdx,
                           const surf_bvh_node* tlasNodes, uint32_t nTlas, const surf_light* lights, uint32_t nLights) {
-    (void)instances; (void)n; (void)tlasIdx; (void)tlasNodes; (void)nTlas; (void)lights; (void)nLights;
-    return fail(c, SURF_ERR_INVALID, "surf_update_instances: re-upload the scene with surf_upload_scene (animation row f3 not built yet)");
+    if (!c || !instances || !tlasIdx || !tlasNodes || (nLights && !lights)) return SURF_ERR_INVALID;
+    if (!c->hasScene) return fail(c, SURF_ERR_NO_SCENE, "no scene uploaded");
+    if (n != c->nInstances || nTlas != c->tlasNodeCount || nLights != c->nLightsUp)
+        return fail(c, SURF_ERR_INVALID, "instance/TLAS/light counts differ from the uploaded scene: use surf_upload_scene");
+    SURF_CHECK(c, hipSetDevice(c->device));
+    int rc = endStream(c);            /* in-flight paths belong to the old transforms */
+    if (rc) return rc;
+    InstanceTables IT;
+    if ((rc = buildInstanceTables(c, instances, n, tlasIdx, tlasNodes, nTlas, lights, nLights, IT))) return rc;
+    const uint32_t depth = IT.tlasDepth + c->maxBlasDepth + 1;
+    if (depth > kMaxStack) return fail(c, SURF_ERR_LIMIT, "BVH too deep for the LDS traversal stack (" + std::to_string(depth) + " entries)");
+    SURF_CHECK(c, hipStreamSynchronize(c->stream));
+    auto put = [&](const void* dst, const void* src, size_t bytes) {
+        return hipMemcpy(const_cast<void*>(dst), src, bytes, hipMemcpyHostToDevice);
+    };
+    SURF_CHECK(c, put(c->S.inst, IT.inst.data(), IT.inst.size() * sizeof(DevInstance)));
+    SURF_CHECK(c, put(c->S.tinst, IT.tinst.data(), IT.tinst.size() * sizeof(TraceInst)));
+    SURF_CHECK(c, put(c->S.tlasNodes, IT.tnodes.data(), IT.tnodes.size() * sizeof(float4)));
+    SURF_CHECK(c, put(c->S.tlasIdx, IT.tidx.data(), IT.tidx.size() * sizeof(uint32_t)));
+    if (nLights) SURF_CHECK(c, put(c->S.lights, IT.lights.data(), IT.lights.size() * sizeof(uint2)));
+    c->S.tlasLeafCount = IT.tlasLeafCount;
+    c->coopEligible = c->ldsTables && c->S.tlasLeafCount > 0 && c->S.tlasLeafCount <= 64;
+    c->stackDepth = std::max(c->stackDepth, depth);
+    destroyGraph(c);                  /* kernel arguments carry the scene descriptor */
+    return SURF_OK;
 }
 
 int surf_set_camera(surf_ctx* c, const surf_camera_ubo* u) {

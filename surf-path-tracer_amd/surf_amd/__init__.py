@@ -96,7 +96,7 @@ def load() -> C.CDLL:
         "surf_destroy": ([P], None), "surf_last_error": ([P], C.c_char_p),
         "surf_shard_rows": ([P, P, C.POINTER(U32)], I32),
         "surf_set_pool_capacity": ([P, U32], I32), "surf_set_frame_batch": ([P, U32], I32),
-        "surf_set_profiling": ([P, I32], I32), "surf_set_zero_cutoff": ([P, I32], I32), "surf_set_trace_mode": ([P, I32], I32), "surf_set_tail_policy": ([P, U32, U32, U32], I32),
+        "surf_set_profiling": ([P, I32], I32), "surf_set_zero_cutoff": ([P, I32], I32), "surf_set_trace_mode": ([P, I32], I32), "surf_set_long_paths": ([P, U32, U32], I32), "surf_set_tail_policy": ([P, U32, U32, U32], I32),
         "surf_debug_capped": ([P, P, U32, C.POINTER(C.c_uint64)], I32),
         "surf_upload_scene": ([P, C.POINTER(SceneDesc)], I32),
         "surf_set_camera": ([P, P], I32),
@@ -108,6 +108,8 @@ def load() -> C.CDLL:
         "surf_trace_any": ([P, U32, P, P, P, P], I32),
         "surf_scene_build_indoor": ([C.c_char_p, I32, C.POINTER(P)], I32),
         "surf_scene_desc_get": ([P, C.POINTER(SceneDesc)], I32),
+        "surf_scene_update": ([P, F], I32),
+        "surf_update_instances": ([P, P, U32, P, P, U32, P, U32], I32),
         "surf_scene_camera": ([P, U32, U32, P], I32),
         "surf_scene_bvh_depths": ([P, C.POINTER(U32), C.POINTER(U32)], I32),
         "surf_scene_destroy": ([P], None),
@@ -152,6 +154,10 @@ class Scene:
     @property
     def handle(self):
         return self._h
+
+    def update(self, delta_time: float):
+        """GPUScene::update (scene.cpp:267-282): rotate instance 3, refit the TLAS, re-batch."""
+        _check(load().surf_scene_update(self._h, delta_time), "surf_scene_update")
 
     def desc(self) -> SceneDesc:
         d = SceneDesc()
@@ -259,11 +265,21 @@ class Renderer:
     def set_zero_cutoff(self, on: bool):
         _check(load().surf_set_zero_cutoff(self._h, 1 if on else 0), "surf_set_zero_cutoff", self._h)
 
+    def update_instances(self, scene: Scene):
+        """Re-uploads the scene's instance records, TLAS and lights (after Scene.update)."""
+        d = scene.desc()
+        _check(load().surf_update_instances(self._h, d.instances, d.instance_count, d.tlas_indices, d.tlas_nodes,
+                                            d.tlas_node_count, d.lights, d.light_count), "surf_update_instances", self._h)
+
     def set_tail_policy(self, threshold_paths: int = 0, lanes_per_wave: int = 0, stage_segments: int = 64):
         """Drain policy of the tail kernel (0 = automatic); stage_segments is the
         per-stage segment budget before the survivors move on (0 = one stage)."""
         _check(load().surf_set_tail_policy(self._h, threshold_paths, lanes_per_wave, stage_segments), "surf_set_tail_policy",
                self._h)
+
+    def set_long_paths(self, escape_segments: int = 64, budget: int = 64):
+        """Paths reaching escape_segments move to the concurrent long-path worker (0 = off)."""
+        _check(load().surf_set_long_paths(self._h, escape_segments, budget), "surf_set_long_paths", self._h)
 
     def set_trace_mode(self, mode: int):
         """0: one ray per lane; 1: one ray per wave (cooperative), for trace_closest/trace_any."""

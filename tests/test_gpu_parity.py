@@ -195,3 +195,36 @@ def test_deterministic_rerun(product_scene):
     r.clear_accumulator()
     r.render(2)
     assert np.array_equal(a.view(np.uint32), r.accumulator().view(np.uint32))
+
+
+def test_animation_update_render_bitexact():
+    """Row f3: GPUScene::update (rotate instance 3, TLAS refit) then the
+    instance/TLAS re-upload (surf_update_instances): renders before and after
+    match the oracle's, bit for bit, and the re-upload equals a fresh upload."""
+    W, H, F = 48, 32, 2
+    o = oracle.OracleScene()
+    p = surf_amd.Scene.indoor()
+    try:
+        r = surf_amd.Renderer(p, W, H)
+        r.set_zero_cutoff(False)
+        r.render(F, 0, 0)
+        c, _, _ = o.render(W, H, F)
+        assert np.array_equal(r.accumulator().view(np.uint32), c.view(np.uint32))
+        for dt in (0.7, 2.1):
+            o.update(dt)
+            p.update(dt)
+            r.update_instances(p)
+            r.clear_accumulator()
+            r.render(F, 4, 0)
+            g = r.accumulator()
+            c, _, _ = o.render(W, H, F, first_frame=4)
+            _assert_bitexact(g, c, f"after update dt={dt}")
+            fresh = surf_amd.Renderer(p, W, H)
+            fresh.set_zero_cutoff(False)
+            fresh.render(F, 4, 0)
+            assert np.array_equal(fresh.accumulator().view(np.uint32), g.view(np.uint32))
+            fresh.close()
+        r.close()
+    finally:
+        o.close()
+        p.close()

@@ -47,3 +47,28 @@ def test_scene_counts(product_scene):
     d = product_scene.desc()
     assert d.triangle_count == 16894 and d.instance_count == 11 and d.light_count == 2
     assert d.material_count == 8
+
+
+def test_animation_update_identical():
+    """GPUScene::update (scene.cpp:267-282, row f3): rotate instance 3 about
+    WORLD_UP, refit the TLAS (leaf boxes grow, never shrink), re-batch --
+    host API and oracle stay byte-identical over a sequence of updates."""
+    import surf_amd
+    o = oracle.OracleScene()
+    p = surf_amd.Scene.indoor()
+    try:
+        before = p.buffers()["instances"]
+        for dt in (0.016, 0.5, 1.25, 3.0):
+            o.update(dt)
+            p.update(dt)
+            a_all, b_all = o.export(), p.buffers()
+            for buf in ("instances", "tlas_nodes", "tlas_indices", "lights", "blas_nodes", "triangles"):
+                rec, ranges = MASK[buf]
+                a = np.frombuffer(a_all[buf], np.uint8).reshape(-1, rec)
+                b = np.frombuffer(b_all[buf], np.uint8).reshape(-1, rec)
+                for lo, hi in ranges:
+                    assert np.array_equal(a[:, lo:hi], b[:, lo:hi]), f"after dt={dt}: {buf} bytes {lo}:{hi}"
+        assert p.buffers()["instances"] != before
+    finally:
+        o.close()
+        p.close()
