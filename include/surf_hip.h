@@ -172,7 +172,7 @@ int surf_set_zero_cutoff(surf_ctx* ctx, int enabled);
  * runs `lanes_per_wave` paths per 64-lane wave for up to `stage_segments`
  * segments; once few paths remain, the cooperative tail runs each on a whole
  * wave (0 = automatic for the first two; stage_segments 0 = a single stage
- * that runs every path to its end; default 64).  Results do not depend on the
+ * that runs every path to its end, the default).  Results do not depend on the
  * policy.  Drains the context first. */
 int surf_set_tail_policy(surf_ctx* ctx, uint32_t threshold_paths, uint32_t lanes_per_wave, uint32_t stage_segments);
 /* Long paths: a path whose next segment would be its `escape_segments`-th

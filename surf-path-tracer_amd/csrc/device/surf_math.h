@@ -117,6 +117,37 @@ SURF_HD float glibcSinCos(float y, int cosine) {
 }
 SURF_HD float gSinf(float y) { return glibcSinCos(y, 0); }
 SURF_HD float gCosf(float y) { return glibcSinCos(y, 1); }
+/* sinf(y) and cosf(y) with one shared range reduction (glibc's s_sincosf.c
+ * uses the same reduction and polynomials as s_sinf.c / s_cosf.c, so both
+ * results are bit-identical to the separate calls); the cosine polynomial is
+ * finished before the sine one starts, which keeps the f64 temporaries of the
+ * two from being live at once. */
+SURF_HD void gSinCosf(float y, float& sn, float& cs) {
+    const uint32_t top = absTop12(y);
+    double x = (double)y;
+    if (top < absTop12(0x1.921fb6p-1f)) {                    /* |y| < pi/4 */
+        if (top < absTop12(0x1p-12f)) { sn = y; cs = 1.0f; return; }
+        const double x2 = x * x;
+        cs = sincosPoly(x, x2, false, 1);
+        sn = sincosPoly(x, x2, false, 0);
+        return;
+    }
+    if (top < absTop12(120.0f)) {
+        const double hpiInv = 0x1.45F306DC9C883p+23, hpi = 0x1.921FB54442D18p0;
+        double r = x * hpiInv;
+        int n = (((int32_t)r) + 0x800000) >> 24;
+        x = fmad(-(double)n, hpi, x);
+        const int q = n & 3;
+        const double sg = (q == 1 || q == 2) ? -1.0 : 1.0;   /* sign[] = {1,-1,-1,1} */
+        const bool neg = (n & 2) != 0;
+        const double xs = x * sg, x2 = x * x;
+        cs = sincosPoly(xs, x2, neg, n ^ 1);
+        sn = sincosPoly(xs, x2, neg, n);
+        return;
+    }
+    sn = (float)sin((double)y);
+    cs = (float)cos((double)y);
+}
 
 /* ---- glibc 2.35 expf (e_expf.c + e_exp2f_data.c, N = 32, FMA variant) ---- */
 SURF_HD float gExpf(float x) {

@@ -568,7 +568,9 @@ __device__ __forceinline__ V3 cosineSample(uint32_t& seed, V3 n) {
         const float r0 = rndF(seed), r1 = rndF(seed);
         const float r = sqrtf(r0);
         const float theta = k2Pi * r1;
-        const V3 dir = mk3(r * gCosf(theta), r * gSinf(theta), sqrtf(1.0f - r0));
+        float sn, cs;
+        gSinCosf(theta, sn, cs);
+        const V3 dir = mk3(r * cs, r * sn, sqrtf(1.0f - r0));
         const float xMax = 1.0f - kEps;
         const V3 tmp = (fabsf(n.x) > xMax) ? mk3(0.0f, 1.0f, 0.0f) : mk3(1.0f, 0.0f, 0.0f);
         const V3 B = normalize(cross(n, tmp));
@@ -954,7 +956,7 @@ __device__ __forceinline__ bool runPath(const DevScene& S, const TraceTables& Tt
                                         uint32_t* stk, uint32_t stride, uint32_t firstCounted) {
     const uint32_t maxSeg = C->maxSeg, zeroCutoff = C->zeroCutoff;
     const uint32_t slot = f2u(o4.w) / npx;
-    unsigned long long nExt = 0, nHit = 0, nCont = 0, nSh = 0, nAcc = 0, nUn = 0;
+    uint32_t nExt = 0, nHit = 0, nCont = 0, nSh = 0, nAcc = 0, nUn = 0;   /* per path: 32 bits suffice */
     bool done = true;
     for (;;) {
         float depth = kFarAway, u = 0.0f, v = 0.0f;
@@ -996,8 +998,9 @@ __device__ __forceinline__ bool runPath(const DevScene& S, const TraceTables& Tt
         __threadfence();          /* radiance before completion: other streams' kernels read it */
         atomicAdd(&frameDone[st * window + slot], 1u);
     }
-    atomicAdd(&ev[0], nExt - (unsigned long long)firstCounted); atomicAdd(&ev[1], nHit); atomicAdd(&ev[2], nCont);
-    atomicAdd(&ev[3], nSh); atomicAdd(&ev[4], nAcc); atomicAdd(&ev[5], nUn);
+    atomicAdd(&ev[0], (unsigned long long)(nExt - firstCounted)); atomicAdd(&ev[1], (unsigned long long)nHit);
+    atomicAdd(&ev[2], (unsigned long long)nCont); atomicAdd(&ev[3], (unsigned long long)nSh);
+    atomicAdd(&ev[4], (unsigned long long)nAcc); atomicAdd(&ev[5], (unsigned long long)nUn);
     if (done) atomicAdd(&ev[6], 1ull);
     return done;
 }
@@ -1009,7 +1012,7 @@ __device__ __forceinline__ bool runPath(const DevScene& S, const TraceTables& Tt
  * drain stage.  firstCounted: the first extension ray of each input path is
  * already in the event counts (regen counted it). */
 template <bool LDS_TABLES>
-__global__ __launch_bounds__(64) void k_tail(DevScene S, Pool cur, uint32_t n, uint32_t lpw, float4* __restrict__ rad,
+__global__ __launch_bounds__(64, 3) void k_tail(DevScene S, Pool cur, uint32_t n, uint32_t lpw, float4* __restrict__ rad,
                                              uint32_t* __restrict__ frameDone, uint32_t npx, uint32_t window, Counters* C,
                                              uint32_t stackWords, uint32_t firstCounted, uint32_t budget, Pool surv) {
     extern __shared__ uint32_t lds[];
@@ -1033,7 +1036,7 @@ __global__ __launch_bounds__(64) void k_tail(DevScene S, Pool cur, uint32_t n, u
  * every path of lp[in] and of escape queue `es` by up to `budget` segments;
  * paths still alive go to lp[out].  Grid-stride over both inputs. */
 template <bool LDS_TABLES>
-__global__ __launch_bounds__(64) void k_long(DevScene S, LongQueues LQ, uint32_t in, uint32_t es, float4* __restrict__ rad,
+__global__ __launch_bounds__(64, 3) void k_long(DevScene S, LongQueues LQ, uint32_t in, uint32_t es, float4* __restrict__ rad,
                                              uint32_t* __restrict__ frameDone, uint32_t npx, uint32_t window, Counters* C,
                                              uint32_t stackWords, uint32_t budget) {
     extern __shared__ uint32_t lds[];
@@ -1064,7 +1067,7 @@ __global__ __launch_bounds__(64) void k_long(DevScene S, LongQueues LQ, uint32_t
  * lane 0 does the writes.  Identical results to k_tail.  LDS: traversal stack,
  * box-distance stack (stackWords words each), then the trace tables. */
 template <bool LDS_TABLES>
-__global__ __launch_bounds__(64) void k_tail_coop(DevScene S, Pool cur, uint32_t n, float4* __restrict__ rad,
+__global__ __launch_bounds__(64, 3) void k_tail_coop(DevScene S, Pool cur, uint32_t n, float4* __restrict__ rad,
                                                   uint32_t* __restrict__ frameDone, uint32_t npx, uint32_t window, Counters* C,
                                                   uint32_t stackWords, uint32_t firstCounted) {
     extern __shared__ uint32_t lds[];

@@ -12,6 +12,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <cfloat>
 #include <array>
@@ -98,7 +99,7 @@ struct surf_ctx {
     bool zeroCutoff = true;        /* radiance-neutral early end of T == 0 paths */
     uint64_t pushedLimit = 0;
     uint32_t tailPaths = 0;        /* drain policy (surf_set_tail_policy), 0 = automatic */
-    uint32_t tailBudget = 64;      /* per-stage segment budget of the drain tail (0 = one stage) */
+    uint32_t tailBudget = 0;       /* per-stage segment budget of the drain tail (0 = one stage: measured fastest) */
     Pool surv[2]{};                /* drain survivors, ping-pong between stages */
     uint32_t survCap = 0;
     uint32_t coopMax = 0;          /* survivors handled by the cooperative tail (one path per wave) */
@@ -290,7 +291,7 @@ int allocWavefront(surf_ctx* c) {
     if (hipGetDeviceProperties(&prop, c->device) == hipSuccess && prop.multiProcessorCount > 0) cus = prop.multiProcessorCount;
     const uint64_t maxBlocks = (cap + kBlock - 1) / kBlock;
     c->gridWork = (uint32_t)std::min<uint64_t>(maxBlocks, (uint64_t)cus * 8);
-    c->coopMax = (uint32_t)cus * 8;     /* 2 waves per SIMD of the cooperative tail */
+    c->coopMax = (uint32_t)cus * 12;    /* 3 waves per SIMD of the tail kernels (launch bounds) */
     c->longGrid = (uint32_t)cus;        /* one k_long wave per CU: the wavefront keeps the rest */
     c->gridRegen = (uint32_t)std::min<uint64_t>(maxBlocks, (uint64_t)cus * 8);
     c->allocated = true;
@@ -532,7 +533,14 @@ int runTail(surf_ctx* c) {
     Pool in = c->pool[0];
     uint32_t cnt = n, firstCounted = 1u;
     int buf = 0;
+    static const bool dbg = std::getenv("SURF_DEBUG_TAIL") != nullptr;   /* diagnostics: per-stage log on stderr */
+    auto t0 = std::chrono::steady_clock::now();
     for (int stage = 0; cnt; ++stage) {
+        if (dbg) {
+            SURF_CHECK(c, hipStreamSynchronize(c->stream));
+            const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+            std::fprintf(stderr, "[surf tail] stage %d: %u paths at %.2f ms\n", stage, cnt, ms);
+        }
         if (c->coopEligible && c->tailBudget && cnt <= c->coopMax) {
             const size_t lds = traversalLds(c, 64) + (size_t)stackWords(c, 64) * sizeof(float);
             hipLaunchKernelGGL(k_tail_coop<true>, dim3(cnt), dim3(64), lds, c->stream, c->S, in, cnt, c->rad, c->frameDone,

@@ -271,7 +271,7 @@ class Renderer:
         _check(load().surf_update_instances(self._h, d.instances, d.instance_count, d.tlas_indices, d.tlas_nodes,
                                             d.tlas_node_count, d.lights, d.light_count), "surf_update_instances", self._h)
 
-    def set_tail_policy(self, threshold_paths: int = 0, lanes_per_wave: int = 0, stage_segments: int = 64):
+    def set_tail_policy(self, threshold_paths: int = 0, lanes_per_wave: int = 0, stage_segments: int = 0):
         """Drain policy of the tail kernel (0 = automatic); stage_segments is the
         per-stage segment budget before the survivors move on (0 = one stage)."""
         _check(load().surf_set_tail_policy(self._h, threshold_paths, lanes_per_wave, stage_segments), "surf_set_tail_policy",
