@@ -236,6 +236,10 @@ int surf_trace_any(surf_ctx* ctx, uint32_t n, const float* o, const float* d, co
  * traversal; needs a scene uploaded with a single-leaf TLAS of <= 64
  * instances).  Results are identical; selects what surf_trace_* run. */
 int surf_set_trace_mode(surf_ctx* ctx, int mode);
+/* Wavefront traversal variant (default 0): lanes run out of step, each
+ * fetching the next ray of its wave's range when done; 0 = one ray per lane in
+ * lockstep.  Identical results; single-leaf TLAS scenes only use it. */
+int surf_set_persistent(surf_ctx* ctx, int enabled);
 
 /* ---- host scene build (the reference's main.cpp scene, OBJ assets) ----
  * variant 0: bundled indoor scene; 1: C5 deep scene (+648 Suzannes in one mesh). */

@@ -142,6 +142,44 @@ struct StreamGeom {
 };
 
 SURF_HD V3 ld3(const float* p) { return mk3(p[0], p[1], p[2]); }
+
+/* Streaming (non-temporal) access to the path pools, hit records and shadow
+ * queue: each record is touched once per phase, so it should not evict the
+ * BVH nodes and triangles the traversal re-reads from L2. */
+#ifndef SURF_STREAM_NT
+#define SURF_STREAM_NT 1
+#endif
+typedef float ntf4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 ldS(const float4* p) {
+#if SURF_STREAM_NT
+    const ntf4 v = __builtin_nontemporal_load(reinterpret_cast<const ntf4*>(p));
+    return make_float4(v.x, v.y, v.z, v.w);
+#else
+    return *p;
+#endif
+}
+__device__ __forceinline__ void stS(float4* p, float4 v) {
+#if SURF_STREAM_NT
+    const ntf4 w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, reinterpret_cast<ntf4*>(p));
+#else
+    *p = v;
+#endif
+}
+__device__ __forceinline__ uint32_t ldSu(const uint32_t* p) {
+#if SURF_STREAM_NT
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
+}
+__device__ __forceinline__ void stSu(uint32_t* p, uint32_t v) {
+#if SURF_STREAM_NT
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
 SURF_HD V3 xyz(float4 v) { return mk3(v.x, v.y, v.z); }
 
 /* ------------------------------------------------------------------ traversal
@@ -553,12 +591,170 @@ __global__ __launch_bounds__(kBlock, SURF_TRACE_WAVES) void k_extend(DevScene S,
     const uint32_t stride = blockDim.x;
     uint32_t* stk = lds + threadIdx.x;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const float4 o = cur.o[i], d = cur.d[i];
+        const float4 o = ldS(&cur.o[i]), d = ldS(&cur.d[i]);
         float depth = kFarAway, u = 0.0f, v = 0.0f;
         uint32_t inst = kUnset, prim = kUnset;
         const bool hit = traceScene<false>(S, Tt, xyz(o), xyz(d), depth, u, v, inst, prim, stk, stride);
-        hitTUV[i] = make_float4(depth, u, v, u2f(prim));
-        hitInst[i] = hit ? inst : kUnset;
+        stS(&hitTUV[i], make_float4(depth, u, v, u2f(prim)));
+        stSu(&hitInst[i], hit ? inst : kUnset);
+    }
+}
+
+/* ------------------------------------------------ persistent traversal
+ * One ray per lane with the lanes running out of step: a lane whose ray is
+ * done fetches the next ray of its wave's range while the others keep
+ * traversing, and each lane walks the instance list on its own (the wave-
+ * uniform instance loop of traceScene makes every instance cost the slowest
+ * lane's BLAS walk).  Per lane the work is exactly traceScene's -- the same
+ * instances in the same order, the same BLAS traversal -- only the
+ * interleaving across rays changes, so results are identical.  Single-leaf
+ * TLAS only (the bundled scene); the wave alternates between a setup phase
+ * (fetch rays, enter the next instance) and a traversal phase (one node visit
+ * per lane per step) that runs until kRefill lanes are waiting. */
+constexpr int kRefill = 16;
+
+struct PRay {                 /* a lane's ray state */
+    V3 o, d;                  /* world space */
+    V3 oo, dd, rd;            /* object space of instance k */
+    float depth, u, v;
+    uint32_t prim, inst, ii, k;
+    uint32_t node, nodeOff;
+    uint32_t* sp;
+    const float4* tri;
+    bool inB, fin, hitThis;
+};
+
+/* Enter instance pr.k (the reference's leaf loop body, bvh.cpp:481-513 + the
+ * root step of BvhBLAS::intersect): transform, root leaf or root children.
+ * Leaves pr.inB set when a BLAS walk starts; otherwise pr.k has advanced. */
+template <bool ANY>
+__device__ __forceinline__ void pEnter(const DevScene& S, const TraceTables& Tt, PRay& r, uint32_t* bottom, uint32_t stride) {
+    r.ii = Tt.order[r.k];
+    const TraceInst& I = Tt.inst[r.ii];
+    instanceRay(I, r.o, r.d, r.oo, r.dd);
+    r.rd = mk3(1.0f / r.dd.x, 1.0f / r.dd.y, 1.0f / r.dd.z);
+    r.fin = S.finiteBoxes && finite3(r.oo) && finite3(r.rd);
+    r.nodeOff = I.meta.x;
+    r.tri = S.tris + 3u * I.meta.y;
+    const float4 r0 = I.r0, r1 = I.r1;
+    const uint32_t rlf = f2u(r0.w), rcnt = f2u(r1.w);
+    if (rcnt != 0u) {
+        if (leafTest<ANY>(r.tri, rlf, rcnt, r.oo, r.dd, r.depth, r.u, r.v, r.prim)) { r.inst = r.ii; r.hitThis = true; }
+        ++r.k;
+        return;
+    }
+    float dn = r.fin ? slabFinite(r0.x, r0.y, r0.z, r1.x, r1.y, r1.z, r.oo, r.rd, r.depth)
+                     : slab(r0.x, r0.y, r0.z, r1.x, r1.y, r1.z, r.oo, r.rd, r.depth);
+    const float4 r2 = I.r2, r3 = I.r3;
+    float df = r.fin ? slabFinite(r2.x, r2.y, r2.z, r3.x, r3.y, r3.z, r.oo, r.rd, r.depth)
+                     : slab(r2.x, r2.y, r2.z, r3.x, r3.y, r3.z, r.oo, r.rd, r.depth);
+    uint32_t cn = r.nodeOff + rlf, cf = cn + 1u;
+    if (dn > df) { const float t = dn; dn = df; df = t; const uint32_t c = cn; cn = cf; cf = c; }
+    if (dn == kFarAway) { ++r.k; return; }
+    r.node = cn;
+    r.sp = bottom;
+    if (df != kFarAway) { *r.sp = cf; r.sp += stride; }
+    r.inB = true;
+}
+
+/* One node visit of the BLAS walk (BvhBLAS::intersect loop, bvh.cpp:129-191). */
+template <bool ANY>
+__device__ __forceinline__ void pStep(const DevScene& S, PRay& r, uint32_t* bottom, uint32_t stride) {
+    const float4* nd = S.nodes + 4u * r.node;
+    float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
+    pin(q0); pin(q1); pin(q2); pin(q3);
+    const uint32_t lf = f2u(q0.w), cnt = f2u(q1.w);
+    bool pop = false;
+    if (cnt != 0u) {
+        if (leafTest<ANY>(r.tri, lf, cnt, r.oo, r.dd, r.depth, r.u, r.v, r.prim)) {
+            r.hitThis = true;
+            if (ANY) { r.inB = false; return; }
+        }
+        pop = true;
+    } else {
+        float dn = r.fin ? slabFinite(q0.x, q0.y, q0.z, q1.x, q1.y, q1.z, r.oo, r.rd, r.depth)
+                         : slab(q0.x, q0.y, q0.z, q1.x, q1.y, q1.z, r.oo, r.rd, r.depth);
+        float df = r.fin ? slabFinite(q2.x, q2.y, q2.z, q3.x, q3.y, q3.z, r.oo, r.rd, r.depth)
+                         : slab(q2.x, q2.y, q2.z, q3.x, q3.y, q3.z, r.oo, r.rd, r.depth);
+        uint32_t cn = r.nodeOff + lf, cf = cn + 1u;
+        if (dn > df) { const float t = dn; dn = df; df = t; const uint32_t c = cn; cn = cf; cf = c; }
+        if (dn == kFarAway) pop = true;
+        else {
+            r.node = cn;
+            if (df != kFarAway) { *r.sp = cf; r.sp += stride; }
+        }
+    }
+    if (pop) {
+        if (r.sp == bottom) {          /* BLAS done: next instance */
+            r.inB = false;
+            if (r.hitThis) r.inst = r.ii;
+            ++r.k;
+        } else {
+            r.sp -= stride;
+            r.node = *r.sp;
+        }
+    }
+}
+
+template <bool LDS>
+__global__ __launch_bounds__(kBlock, SURF_TRACE_WAVES) void k_extend_p(DevScene S, Pool cur, float4* __restrict__ hitTUV,
+                                                                       uint32_t* __restrict__ hitInst, const Counters* C, int par,
+                                                                       uint32_t stackWords) {
+    extern __shared__ uint32_t lds[];
+    const TraceTables Tt = traceTables<LDS>(S, lds, stackWords);
+    const uint32_t n = C->nIn[par];
+    const uint32_t nInst = S.tlasLeafCount;
+    const uint32_t stride = blockDim.x;
+    uint32_t* const bottom = lds + threadIdx.x;
+    /* this wave's contiguous range of rays */
+    const uint32_t waves = gridDim.x * (blockDim.x >> 6);
+    const uint32_t w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const uint32_t per = (n + waves - 1) / waves;
+    const uint32_t begin = min(n, w * per), end = min(n, begin + per);
+    uint32_t next = begin;
+    PRay r;
+    r.inB = false;
+    int ray = -1;
+    bool live = true;
+    for (;;) {
+        /* setup phase: refill lanes without a ray, advance lanes between instances */
+        for (;;) {
+            const bool need = live && ray < 0;
+            const unsigned long long mNeed = __ballot(need);
+            if (mNeed) {
+                const uint32_t cand = next + rankBelow(mNeed);
+                if (need) {
+                    if (cand < end) {
+                        ray = (int)cand;
+                        const float4 o4 = cur.o[cand], d4 = cur.d[cand];
+                        r.o = xyz(o4); r.d = xyz(d4);
+                        r.depth = kFarAway; r.u = 0.0f; r.v = 0.0f; r.prim = kUnset; r.inst = kUnset; r.k = 0;
+                    } else {
+                        live = false;
+                    }
+                }
+                next = min(end, next + (uint32_t)__popcll(mNeed));
+            }
+            const bool setup = live && ray >= 0 && !r.inB;
+            if (!__ballot(setup)) break;
+            if (setup) {
+                if (r.k >= nInst) {
+                    hitTUV[ray] = make_float4(r.depth, r.u, r.v, u2f(r.prim));
+                    hitInst[ray] = r.inst;
+                    ray = -1;
+                } else {
+                    r.hitThis = false;
+                    pEnter<false>(S, Tt, r, bottom, stride);
+                }
+            }
+        }
+        if (!__ballot(live)) break;
+        /* traversal phase */
+        for (;;) {
+            if (r.inB) pStep<false>(S, r, bottom, stride);
+            const unsigned long long waiting = __ballot(live && !r.inB);
+            if (__popcll(waiting) >= kRefill || !__ballot(r.inB)) break;
+        }
     }
 }
 
@@ -810,9 +1006,9 @@ __global__ __launch_bounds__(kBlock, SURF_SHADE_WAVES) void k_shade(DevScene S, 
         uint32_t slot = 0;
         const bool active = i < n;
         if (active) {
-            const float4 o4 = cur.o[i];
+            const float4 o4 = ldS(&cur.o[i]);
             slot = f2u(o4.w) / npx;
-            shadePath(S, Tb, o4, cur.d[i], cur.T[i], hitTUV[i], hitInst[i], maxSeg, zeroCutoff, r);
+            shadePath(S, Tb, o4, ldS(&cur.d[i]), ldS(&cur.T[i]), ldS(&hitTUV[i]), ldSu(&hitInst[i]), maxSeg, zeroCutoff, r);
             if (r.addRad) addRadiance(rad, f2u(o4.w), r.radd);
         }
         /* a path reaching longThresh segments leaves for the k_long worker */
@@ -835,8 +1031,8 @@ __global__ __launch_bounds__(kBlock, SURF_SHADE_WAVES) void k_shade(DevScene S, 
         for (uint32_t k = 0; k < wv; ++k) { jc += sWave[it][k][0]; js += sWave[it][k][1]; }
         jc += rankBelow(mCont);
         js += rankBelow(mSh);
-        if (r.cont && !esc) { nxt.o[jc] = r.o; nxt.d[jc] = r.d; nxt.T[jc] = r.T; }
-        if (r.shadow) { Q.o[js] = r.so; Q.d[js] = r.sd; Q.c[js] = r.sc; }
+        if (r.cont && !esc) { stS(&nxt.o[jc], r.o); stS(&nxt.d[jc], r.d); stS(&nxt.T[jc], r.T); }
+        if (r.shadow) { stS(&Q.o[js], r.so); stS(&Q.d[js], r.sd); stS(&Q.c[js], r.sc); }
         /* a path that ends here may still have this phase's shadow ray pending:
          * connect runs before the host reads frameDone (end of the phase). */
         frameDoneAdd(frameDone + (blockIdx.x % kStripes) * window, active && !r.cont, slot);
@@ -866,12 +1062,12 @@ __global__ __launch_bounds__(kBlock, SURF_TRACE_WAVES) void k_connect(DevScene S
         const uint32_t i = base + threadIdx.x;
         bool unocc = false;
         if (i < n) {
-            const float4 o = Q.o[i], d = Q.d[i];
+            const float4 o = ldS(&Q.o[i]), d = ldS(&Q.d[i]);
             float depth = o.w, u = 0.0f, v = 0.0f;
             uint32_t inst = kUnset, prim = kUnset;
             const bool occ = traceScene<true>(S, Tt, xyz(o), xyz(d), depth, u, v, inst, prim, stk, stride);
             if (!occ) {
-                const float4 c = Q.c[i];
+                const float4 c = ldS(&Q.c[i]);
                 addRadiance(rad, f2u(d.w), xyz(c));
                 unocc = true;
             }
@@ -925,9 +1121,9 @@ __global__ __launch_bounds__(kBlock) void k_regen(DevCamera cam, Pool nxt, float
         const V3 plane = add(add(ld3(cam.firstPixel), lscl(u, ld3(cam.uVec))), lscl(v, ld3(cam.vVec)));
         const V3 dir = normalize(sub(plane, origin));
         const uint32_t slotIdx = cont + k;
-        nxt.o[slotIdx] = make_float4(origin.x, origin.y, origin.z, u2f(sid));
-        nxt.d[slotIdx] = make_float4(dir.x, dir.y, dir.z, u2f(kFlagSpecular | (1u << 2)));
-        nxt.T[slotIdx] = make_float4(1.0f, 1.0f, 1.0f, u2f(seed));
+        stS(&nxt.o[slotIdx], make_float4(origin.x, origin.y, origin.z, u2f(sid)));
+        stS(&nxt.d[slotIdx], make_float4(dir.x, dir.y, dir.z, u2f(kFlagSpecular | (1u << 2))));
+        stS(&nxt.T[slotIdx], make_float4(1.0f, 1.0f, 1.0f, u2f(seed)));
         rad[sid] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     }
     if (gid == 0) {

@@ -105,6 +105,7 @@ struct surf_ctx {
     uint32_t coopMax = 0;          /* survivors handled by the cooperative tail (one path per wave) */
     bool coopEligible = false;     /* single-leaf TLAS of <= 64 instances, LDS tables */
     int traceMode = 0;             /* surf_trace_closest/_any: 0 one ray per lane, 1 one ray per wave */
+    bool persistent = false;       /* out-of-step lanes with per-wave ray ranges: measured 4x slower */
     /* long paths: escape queues + long-path pools, advanced by k_long on stream2 */
     uint32_t longThresh = 0;       /* escape length (surf_set_long_paths; 0 = off: measured slower) */
     uint32_t longBudget = 64;      /* segments per path per k_long launch */
@@ -306,7 +307,10 @@ void launchPhase(surf_ctx* c, int par, hipEvent_t* ev) {
     const size_t lds = traversalLds(c, kBlock);
     const uint32_t sw = stackWords(c, kBlock);
     if (ev) (void)hipEventRecord(ev[0], c->stream);
-    if (c->ldsTables)
+    if (c->persistent && c->ldsTables && c->S.tlasLeafCount > 0)
+        hipLaunchKernelGGL(k_extend_p<true>, dim3(c->gridWork), dim3(kBlock), lds, c->stream, c->S, c->pool[par], c->hitTUV,
+                           c->hitInst, (const Counters*)c->ctr, par, sw);
+    else if (c->ldsTables)
         hipLaunchKernelGGL(k_extend<true>, dim3(c->gridWork), dim3(kBlock), lds, c->stream, c->S, c->pool[par], c->hitTUV,
                            c->hitInst, (const Counters*)c->ctr, par, sw);
     else
@@ -803,6 +807,16 @@ int surf_set_long_paths(surf_ctx* c, uint32_t escape_segments, uint32_t budget) 
     if (rc) return rc;
     c->longThresh = escape_segments;
     c->longBudget = budget;
+    return SURF_OK;
+}
+
+int surf_set_persistent(surf_ctx* c, int enabled) {
+    if (!c) return fail(nullptr, SURF_ERR_INVALID, "ctx is NULL");
+    SURF_CHECK(c, hipSetDevice(c->device));
+    const int rc = endStream(c);
+    if (rc) return rc;
+    c->persistent = enabled != 0;
+    destroyGraph(c);
     return SURF_OK;
 }
 

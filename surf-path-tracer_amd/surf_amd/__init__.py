@@ -96,7 +96,7 @@ def load() -> C.CDLL:
         "surf_destroy": ([P], None), "surf_last_error": ([P], C.c_char_p),
         "surf_shard_rows": ([P, P, C.POINTER(U32)], I32),
         "surf_set_pool_capacity": ([P, U32], I32), "surf_set_frame_batch": ([P, U32], I32),
-        "surf_set_profiling": ([P, I32], I32), "surf_set_zero_cutoff": ([P, I32], I32), "surf_set_trace_mode": ([P, I32], I32), "surf_set_long_paths": ([P, U32, U32], I32), "surf_set_tail_policy": ([P, U32, U32, U32], I32),
+        "surf_set_profiling": ([P, I32], I32), "surf_set_zero_cutoff": ([P, I32], I32), "surf_set_trace_mode": ([P, I32], I32), "surf_set_persistent": ([P, I32], I32), "surf_set_long_paths": ([P, U32, U32], I32), "surf_set_tail_policy": ([P, U32, U32, U32], I32),
         "surf_debug_capped": ([P, P, U32, C.POINTER(C.c_uint64)], I32),
         "surf_upload_scene": ([P, C.POINTER(SceneDesc)], I32),
         "surf_set_camera": ([P, P], I32),
@@ -280,6 +280,10 @@ class Renderer:
     def set_long_paths(self, escape_segments: int = 64, budget: int = 64):
         """Paths reaching escape_segments move to the concurrent long-path worker (0 = off)."""
         _check(load().surf_set_long_paths(self._h, escape_segments, budget), "surf_set_long_paths", self._h)
+
+    def set_persistent(self, on: bool):
+        """Out-of-step (persistent) wavefront traversal on/off (identical results)."""
+        _check(load().surf_set_persistent(self._h, 1 if on else 0), "surf_set_persistent", self._h)
 
     def set_trace_mode(self, mode: int):
         """0: one ray per lane; 1: one ray per wave (cooperative), for trace_closest/trace_any."""

@@ -100,6 +100,27 @@ def test_render_64x64x4_bitexact(oracle_scene, product_scene):
     _assert_counts(stats, cnt)
 
 
+@pytest.mark.parametrize("policy", [(0, 0, 16), (0, 8, 4), (1 << 30, 0, 8), (1, 0, 0)],
+                         ids=["staged+coop", "8-lanes-staged", "tail-from-start", "wavefront-to-end"])
+def test_drain_policies_bitexact(oracle_scene, product_scene, policy):
+    """Every drain schedule (lane stages with survivor hand-off, the cooperative
+    one-path-per-wave tail, tail from the first phase, wavefront to the end)
+    gives the same radiance and event counts."""
+    r0 = surf_amd.Renderer(product_scene, 96, 64)
+    r0.set_tail_policy(*policy)
+    r0.render(4, 0, 0)
+    g = r0.accumulator()
+    st = r0.stats()
+    oracle.set_zero_cutoff(True)
+    try:
+        c2, cnt, _ = oracle_scene.render(96, 64, 4)
+    finally:
+        oracle.set_zero_cutoff(False)
+    _assert_bitexact(g, c2, f"drain policy {policy}")
+    _assert_counts(st, cnt)
+    r0.close()
+
+
 def test_render_c1_256x256x16_bitexact(oracle_scene, product_scene):
     g, c, stats, cnt, _ = _render_both(oracle_scene, product_scene, 256, 256, 16)
     _assert_bitexact(g, c, "C1 256x256x16")
