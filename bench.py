@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--frames-per-step", type=int, default=16)
     ap.add_argument("--max-segments", type=int, default=0, help="0 = unbounded + RR (C3); 8 = C2")
     ap.add_argument("--row-block", type=int, default=16)
+    ap.add_argument("--scene", choices=["indoor", "c5"], default="indoor",
+                    help="indoor = bundled scene (C2/C3); c5 = +648-Suzanne 10.2M-triangle lattice BLAS (C5)")
     ap.add_argument("--cpu-frames", type=int, default=48, help="frames of the CPU baseline sample (full frame)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
@@ -54,18 +56,27 @@ def parse():
     return ap.parse_args()
 
 
+def workload(args):
+    if args.scene == "c5":
+        return "C5" if args.max_segments == 0 else f"C5-max{args.max_segments}seg"
+    return {0: "C3", 8: "C2"}.get(args.max_segments, f"max{args.max_segments}seg")
+
+
 def cpu_baseline(args):
     """Reference CPU algorithm (oracle restatement, OpenMP rows) on a bounded sample."""
     exe = os.path.join(REPO, "oracle", "cpu_ref_bench")
     if not os.path.exists(exe):
         subprocess.run(["make", "-s", "-C", os.path.join(REPO, "oracle")], check=True)
     env = dict(os.environ, OMP_NUM_THREADS=str(args.cpu_threads))
-    cmd = [exe, "--cutoff", os.path.join(REPO, "assets"), str(args.width), str(args.height), str(args.cpu_frames),
-           "0", str(args.height), str(args.max_segments), str(args.cpu_threads)]
+    r0, r1, frames = 0, args.height, args.cpu_frames
+    if args.scene == "c5":                # ~60x slower per sample: a centred row band, one frame
+        r0, r1, frames = args.height // 2 - 32, args.height // 2 + 32, 1
+    cmd = [exe, "--cutoff"] + (["--variant", "1"] if args.scene == "c5" else []) + [os.path.join(REPO, "assets"),
+           str(args.width), str(args.height), str(frames), str(r0), str(r1), str(args.max_segments), str(args.cpu_threads)]
     out = subprocess.run(cmd, capture_output=True, text=True, env=env, check=True).stdout.strip().splitlines()[-1]
     r = json.loads(out)
     return {"value": round(r["mrays_per_s"], 4), "unit": "Mrays/s", "cores": r["threads"], "kind": "port",
-            "sample": f"{args.width}x{args.height}, frames 0..{args.cpu_frames - 1} (1 spp each), "
+            "sample": f"{args.width}x{args.height} rows {r0}..{r1 - 1}, frames 0..{frames - 1} (1 spp each), "
                       f"{'unbounded+RR' if args.max_segments == 0 else 'max %d segments' % args.max_segments}, "
                       f"throughput cutoff on (as the GPU), oracle/cpu_ref_bench, {r['seconds']:.2f} s",
             "seconds": r["seconds"], "samples": r["samples"],
@@ -91,7 +102,9 @@ def main():
 
     surf_amd.load()
     W, H, F = args.width, args.height, args.frames_per_step
-    scene = surf_amd.Scene.indoor()
+    tb = time.perf_counter()
+    scene = surf_amd.Scene.indoor(variant=1 if args.scene == "c5" else 0)
+    scene_build_s = time.perf_counter() - tb
     spec = surf_amd.ShardSpec(rank, world, args.row_block if world > 1 else 0)
     r = surf_amd.Renderer(scene, W, H, device=local, shard=spec)
     rows = len(r.rows)
@@ -190,8 +203,10 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic camera samples of the bundled indoor scene (reference OBJ assets)",
-            "config": {"workload": "C3" if args.max_segments == 0 else f"max{args.max_segments}seg",
-                       "scene": "bundled indoor (main.cpp:161-346)", "width": W, "height": H,
+            "config": {"workload": workload(args),
+                       "scene": "bundled indoor (main.cpp:161-346)" if args.scene == "indoor"
+                                else "C5: indoor + 648 Suzannes in one 10.2M-triangle BLAS",
+                       "width": W, "height": H,
                        "spp": F * args.steps, "frames_per_step": F,
                        "bounces": "unbounded + russian roulette" if args.max_segments == 0 else f"<= {args.max_segments} segments",
                        "parallelism": f"row-shard x{world} (16-row interleave) + RCCL gather" if world > 1 else "single GPU"},
@@ -202,6 +217,7 @@ def main():
             "iterations": ev["iterations"],
             "tail_paths": ev["tail_paths"],
             "kernel_ms_profile_pass": kernel_ms,
+            "scene_build_s": round(scene_build_s, 3),
         }
         print(json.dumps(out))
     if dist_on:

@@ -131,8 +131,8 @@ public:
 struct alignas(16) AABB {
     alignas(16) Float3 bbMin = Float3(INFINITY);
     alignas(16) Float3 bbMax = Float3(-INFINITY);
-    void grow(const Float3& p);
-    void grow(const AABB& b);
+    void grow(const Float3& p) { bbMin = min(bbMin, p); bbMax = max(bbMax, p); }
+    void grow(const AABB& b) { bbMin = min(bbMin, b.bbMin); bbMax = max(bbMax, b.bbMax); }
     F32 area() const;
     Float3 center() const;                        /* the reference's half-extent quirk, bvh.cpp:35-38 */
 };
@@ -144,10 +144,16 @@ struct alignas(16) BvhNode {
     bool isLeaf() const { return count != 0; }
 };
 
+/* Threads of the parallel BVH build: SURF_BUILD_THREADS, else OMP_NUM_THREADS,
+ * else the hardware concurrency (capped at 64). */
+unsigned defaultBuildThreads();
+
 class BvhBLAS {
 public:
     explicit BvhBLAS(Mesh* mesh);
-    void build();
+    BvhBLAS(Mesh* mesh, unsigned threads);
+    void build();                                 /* SURF_BUILD_THREADS / OMP_NUM_THREADS threads */
+    void build(unsigned threads);                 /* same arrays for every thread count */
     void refit();
     const Mesh* mesh() const { return m_mesh; }
     SizeType triCount() const { return m_mesh->triangles.size(); }

@@ -255,6 +255,14 @@ int surf_scene_camera(const surf_scene* scene, uint32_t width, uint32_t height, 
 int surf_scene_bvh_depths(const surf_scene* scene, uint32_t* tlas_depth, uint32_t* max_blas_depth);
 void surf_scene_destroy(surf_scene* scene);
 
+/* BvhBLAS::build (sources/bvh.cpp:255-465: binned SAH, 8 bins, pre-order pair
+ * allocation) over `count` reference Triangles, multi-threaded (threads = 0:
+ * SURF_BUILD_THREADS / OMP_NUM_THREADS / hardware).  Writes the reference's
+ * index permutation (count) and node pool (nodes_out needs 2*count records;
+ * *nodes_used are written).  The arrays are identical for every thread count. */
+int surf_bvh_build(const surf_triangle* triangles, uint32_t count, uint32_t threads, uint32_t* indices_out,
+                   surf_bvh_node* nodes_out, uint32_t* nodes_used);
+
 #ifdef __cplusplus
 }  /* extern "C" */
 

@@ -60,6 +60,7 @@ def load():
         "orc_random_f32": ([C.POINTER(U32)], F),
         "orc_finalize_rgba8": ([P, U32, F, P], None),
         "orc_set_zero_cutoff": ([I32], None),
+        "orc_bvh_build": ([P, U32, P, P], U32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)
@@ -208,3 +209,16 @@ def finalize_rgba8(acc: np.ndarray, inv_samples: float) -> np.ndarray:
     out = np.zeros(len(acc), np.uint32)
     load().orc_finalize_rgba8(_p(acc), len(acc), inv_samples, _p(out))
     return out
+
+
+def bvh_build(tris: np.ndarray):
+    """Sequential reference BLAS build over (n, 16) float32 Triangle records
+    (v0, v1, v2, centroid at 16-B strides).  Returns (indices (n,) u32,
+    nodes (used, 12) float32 view of the 48-B BvhNode records)."""
+    tris = np.ascontiguousarray(tris, dtype=np.float32)
+    n = tris.shape[0]
+    idx = np.empty(n, np.uint32)
+    nodes = np.zeros((2 * n, 12), np.float32)
+    used = load().orc_bvh_build(_p(tris), n, _p(idx), _p(nodes))
+    return idx, nodes[:used]
+

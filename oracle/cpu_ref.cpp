@@ -1078,6 +1078,32 @@ void orc_bvh_depths(const orc_scene* h, uint32_t* td, uint32_t* bd) {
     *bd = m;
 }
 
+/* BvhBLAS::build over raw reference Triangles (64 B: v0, v1, v2, centroid at
+ * 16-B strides); writes the index permutation and the node pool as 48-B
+ * BvhNode records (leftFirst, count, pad, bbMin, pad, bbMax, pad).  Sequential,
+ * the reference's recursion order. */
+uint32_t orc_bvh_build(const float* tris, uint32_t n, uint32_t* idxOut, float* nodesOut) {
+    Mesh m;
+    m.tris.resize(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        const float* t = tris + 16 * (size_t)i;
+        Tri& d = m.tris[i];
+        d.v0 = V3{t[0], t[1], t[2]}; d.v1 = V3{t[4], t[5], t[6]}; d.v2 = V3{t[8], t[9], t[10]}; d.c = V3{t[12], t[13], t[14]};
+    }
+    TriPrims P; P.m = &m;
+    Bvh b;
+    buildBvh(b, P, n);
+    memcpy(idxOut, b.idx.data(), (size_t)n * 4);
+    for (uint32_t k = 0; k < b.used; ++k) {
+        float* o = nodesOut + 12 * (size_t)k;
+        memset(o, 0, 48);
+        memcpy(o, &b.nodes[k].lf, 4); memcpy(o + 1, &b.nodes[k].cnt, 4);
+        o[4] = b.nodes[k].box.mn.x; o[5] = b.nodes[k].box.mn.y; o[6] = b.nodes[k].box.mn.z;
+        o[8] = b.nodes[k].box.mx.x; o[9] = b.nodes[k].box.mx.y; o[10] = b.nodes[k].box.mx.z;
+    }
+    return b.used;
+}
+
 void orc_set_zero_cutoff(int on) { gZeroCutoff = on != 0; }
 
 uint32_t orc_init_seed(uint32_t s) { return seedOf(s); }

@@ -106,6 +106,8 @@ void orc_bvh_depths(const orc_scene*, uint32_t* tlas_depth, uint32_t* max_blas_d
 /* Ends paths whose throughput is exactly zero (radiance-neutral; see cpu_ref.cpp).
  * Default off = reference semantics. */
 void orc_set_zero_cutoff(int on);
+/* Sequential BvhBLAS::build over n 64-B Triangles; returns nodesUsed. */
+uint32_t orc_bvh_build(const float* tris, uint32_t n, uint32_t* idx_out, float* nodes_out);
 
 /* RNG of surf_math.cpp:31-95, for known-answer tests. */
 uint32_t orc_init_seed(uint32_t seed);

@@ -16,11 +16,18 @@
 #include <omp.h>
 
 int main(int argc, char** argv) {
-    int cutoff = 0;
-    if (argc > 1 && std::string(argv[1]) == "--cutoff") {
-        cutoff = 1;
-        orc_set_zero_cutoff(1);
-        ++argv; --argc;
+    int cutoff = 0, variant = 0;
+    for (;;) {
+        if (argc > 1 && std::string(argv[1]) == "--cutoff") {
+            cutoff = 1;
+            orc_set_zero_cutoff(1);
+            ++argv; --argc;
+        } else if (argc > 2 && std::string(argv[1]) == "--variant") {
+            variant = atoi(argv[2]);             /* 1 = C5 deep scene */
+            argv += 2; argc -= 2;
+        } else {
+            break;
+        }
     }
     if (argc < 5) { fprintf(stderr, "usage: %s ASSETS W H FRAMES [ROW_BEGIN ROW_END [MAX_SEG [THREADS [OUT.pfm]]]]\n", argv[0]); return 2; }
     const char* assets = argv[1];
@@ -30,7 +37,7 @@ int main(int argc, char** argv) {
     int threads = argc > 8 ? atoi(argv[8]) : 0;
     const char* out = argc > 9 ? argv[9] : nullptr;
     if (r1 > H || r0 >= r1 || W == 0 || F == 0) { fprintf(stderr, "bad arguments\n"); return 2; }
-    orc_scene* s = orc_scene_create(assets, 0);
+    orc_scene* s = orc_scene_create(assets, variant);
     if (!s) return 1;
     std::vector<float> acc((size_t)(r1 - r0) * W * 4, 0.0f);
     orc_counters c;

@@ -15,7 +15,12 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <array>
+#include <chrono>
+#include <atomic>
+#include <cmath>
 #include <memory>
+#include <thread>
 #include <stdexcept>
 
 namespace surf {
@@ -247,8 +252,6 @@ Mesh::Mesh(const std::string& path) {
 }
 
 /* =================================================================== AABB */
-void AABB::grow(const Float3& p) { bbMin = min(bbMin, p); bbMax = max(bbMax, p); }
-void AABB::grow(const AABB& b) { bbMin = min(bbMin, b.bbMin); bbMax = max(bbMax, b.bbMax); }
 F32 AABB::area() const { const Float3 e = bbMax - bbMin; return e.x * e.y + e.y * e.z + e.z * e.x; }
 Float3 AABB::center() const { return 0.5f * (bbMax - bbMin); }
 
@@ -256,100 +259,243 @@ Float3 AABB::center() const { return 0.5f * (bbMax - bbMin); }
  * One builder for both levels.  Prim access is a policy: key(p, axis) is the
  * binning coordinate, addTo(box, p) grows a box by the primitive.  Build order
  * reproduces the reference's recursive subdivide exactly (pre-order, children
- * allocated in pairs at split time) with an explicit stack. */
+ * allocated in pairs at split time).
+ *
+ * Parallel build.  Two facts make a multi-threaded build
+ * produce the reference's arrays byte for byte:
+ *   - every reduction in findSplitPlane/updateNodeBounds is a min, a max or an
+ *     integer count, which are order-independent for finite inputs (checked
+ *     once; a non-finite key or vertex selects the sequential builder), and the
+ *     sweep over the 8 bins is done exactly as the reference does it;
+ *   - subdivide(X) allocates all nodes of X's subtree in one contiguous block
+ *     of the pool that starts at the `used` value on entry, so a subtree built
+ *     elsewhere with local numbering only needs its interior child indices
+ *     shifted by the block's final base.
+ * Large nodes bin in parallel chunks and run their two children concurrently;
+ * the index partition stays the reference's sequential swap loop (it defines
+ * the index order).  Subtrees below kSeqPrims are built by the sequential
+ * builder into a local block, then placed with one offset. */
 namespace {
 
 constexpr int kBins = 8;
 constexpr int kPlanes = kBins - 1;
+constexpr U32 kSeqPrims = 1u << 15;          /* subtree size built sequentially */
+constexpr U32 kChunk = 1u << 16;             /* prims per binning chunk */
+
+}  // namespace
+
+unsigned defaultBuildThreads() {
+    if (const char* e = getenv("SURF_BUILD_THREADS")) { const int v = atoi(e); if (v > 0) return (unsigned)v; }
+    if (const char* e = getenv("OMP_NUM_THREADS")) { const int v = atoi(e); if (v > 0) return (unsigned)v; }
+    const unsigned hc = std::thread::hardware_concurrency();
+    return hc ? std::min(hc, 64u) : 1u;
+}
+
+namespace {
+
+/* Per-axis bins of one node (bvh.cpp:302-340). */
+struct Bins {
+    F32 lo[3], hi[3];
+    U32 cnt[3][kBins];
+    AABB box[3][kBins];
+};
+
+/* Runs f(chunk) for chunk in [0, n) on up to `threads` threads. */
+template <class F>
+void forChunks(U32 n, unsigned threads, F&& f) {
+    const unsigned t = std::min<unsigned>(threads, n);
+    if (t <= 1) { for (U32 c = 0; c < n; ++c) f(c); return; }
+    std::atomic<U32> next{0};
+    auto work = [&]() { for (U32 c; (c = next.fetch_add(1)) < n;) f(c); };
+    std::vector<std::thread> pool;
+    for (unsigned i = 1; i < t; ++i) pool.emplace_back(work);
+    work();
+    for (auto& th : pool) th.join();
+}
+
+/* A primitive as the build sees it: its binning key, its id and its box (the
+ * box of its vertices, or the instance bounds).  The build permutes these
+ * records in place of the reference's index array (same swaps), so every pass
+ * streams through memory; the index array is read off the ids at the end. */
+struct alignas(16) PrimRef {
+    F32 key[3];
+    U32 id;
+    AABB box;
+};
 
 template <class Prims>
 struct SahBuilder {
     const Prims& prims;
     std::vector<U32>& idx;
+    std::vector<PrimRef>& refs;
     std::vector<BvhNode>& nodes;
     U32& used;
+    unsigned threads = 1;
+    std::atomic<int>* active = nullptr;           /* concurrent subtree builders */
 
-    void bounds(U32 ni) {
-        BvhNode& n = nodes[ni];
-        for (U32 i = 0; i < n.count; ++i) prims.addTo(n.boundingBox, idx[n.leftFirst + i]);
+    unsigned chunkThreads() const {
+        const int a = active ? active->load() : 0;      /* extra builder threads */
+        return std::max(1u, threads / (unsigned)(1 + a));
     }
 
-    /* returns split position; cost/axis out (bvh.cpp:294-377) */
+    void bounds(BvhNode& n) const {
+        for (U32 i = 0; i < n.count; ++i) n.boundingBox.grow(refs[n.leftFirst + i].box);
+    }
+
+    /* updateNodeBounds over parallel chunks (min/max: exact in any order) */
+    void boundsPar(BvhNode& n) const {
+        const U32 nc = (n.count + kChunk - 1) / kChunk;
+        std::vector<AABB> part(nc);
+        forChunks(nc, chunkThreads(), [&](U32 c) {
+            const U32 b = n.leftFirst + c * kChunk, e = std::min(n.leftFirst + n.count, b + kChunk);
+            for (U32 i = b; i < e; ++i) part[c].grow(refs[i].box);
+        });
+        for (const AABB& p : part) n.boundingBox.grow(p);
+    }
+
+    /* The sweep over the bins and the cost comparison (bvh.cpp:341-377). */
+    static void sweep(const U32* cnt, const AABB* box, F32 lo, F32 hi, U32 axis, F32& bestCost, F32& bestSplit,
+                      U32& bestAxis) {
+        F32 lArea[kPlanes], rArea[kPlanes];
+        U32 lCnt[kPlanes], rCnt[kPlanes];
+        AABB lBox, rBox;
+        U32 lSum = 0, rSum = 0;
+        for (int k = 0; k < kPlanes; ++k) {
+            lSum += cnt[k];
+            lCnt[k] = lSum;
+            lBox.grow(box[k]);
+            lArea[k] = lBox.area();
+            const int rb = kBins - 1 - k;
+            rSum += cnt[rb];
+            rCnt[rb - 1] = rSum;
+            rBox.grow(box[rb]);
+            rArea[rb - 1] = rBox.area();
+        }
+        const F32 extent = (hi - lo) / (F32)kBins;
+        for (int k = 0; k < kPlanes; ++k) {
+            const F32 c = (F32)lCnt[k] * lArea[k] + (F32)rCnt[k] * rArea[k];
+            if (c < bestCost) {
+                bestCost = c;
+                bestSplit = lo + extent * (F32)(k + 1);
+                bestAxis = axis;
+            }
+        }
+    }
+
+    static U32 binOf(F32 key, F32 lo, F32 scaleK) {
+        const size_t s = (size_t)((key - lo) * scaleK);
+        return (U32)(s < (size_t)(kBins - 1) ? s : (size_t)(kBins - 1));
+    }
+
+    /* findSplitPlane (bvh.cpp:294-377); returns split position, cost/axis out.
+     * The reference makes two passes per axis (key range, then bins); here one
+     * pass finds all three key ranges and one pass fills all three axes' bins
+     * from the triangle's box.  Same values: min, max and counts only. */
     F32 plane(const BvhNode& n, F32& bestCost, U32& bestAxis) const {
         bestCost = INFINITY;
         bestAxis = 0;
         F32 bestSplit = 0.0f;
         const U32 first = n.leftFirst, cnt = n.count;
-        for (U32 axis = 0; axis < 3; ++axis) {
-            F32 lo = 3.40282347e+38f, hi = 1.17549435e-38f;    /* F32_MAX / F32_MIN (sic) */
-            for (U32 i = 0; i < cnt; ++i) {
-                const F32 k = prims.key(idx[first + i], axis);
-                lo = lo < k ? lo : k;
-                hi = hi > k ? hi : k;
+        F32 lo[3] = {3.40282347e+38f, 3.40282347e+38f, 3.40282347e+38f};   /* F32_MAX / F32_MIN (sic) */
+        F32 hi[3] = {1.17549435e-38f, 1.17549435e-38f, 1.17549435e-38f};
+        for (U32 i = 0; i < cnt; ++i)
+            for (U32 a = 0; a < 3; ++a) {
+                const F32 k = refs[first + i].key[a];
+                lo[a] = lo[a] < k ? lo[a] : k;
+                hi[a] = hi[a] > k ? hi[a] : k;
             }
-            if (lo == hi) continue;
-            const F32 scaleK = (F32)kBins / (hi - lo);
-            U32 binCount[kBins] = {0};
-            AABB binBox[kBins];
-            for (U32 i = 0; i < cnt; ++i) {
-                const U32 pr = idx[first + i];
-                const size_t s = (size_t)((prims.key(pr, axis) - lo) * scaleK);
-                const size_t b = s < (size_t)(kBins - 1) ? s : (size_t)(kBins - 1);
-                binCount[b]++;
-                prims.addTo(binBox[b], pr);
+        F32 scaleK[3];
+        U32 binCount[3][kBins] = {};
+        AABB binBox[3][kBins];
+        for (U32 a = 0; a < 3; ++a) scaleK[a] = lo[a] == hi[a] ? 0.0f : (F32)kBins / (hi[a] - lo[a]);
+        for (U32 i = 0; i < cnt; ++i) {
+            const PrimRef& pr = refs[first + i];
+            const AABB& tb = pr.box;
+            for (U32 a = 0; a < 3; ++a) {
+                if (lo[a] == hi[a]) continue;
+                const U32 k = binOf(pr.key[a], lo[a], scaleK[a]);
+                binCount[a][k]++;
+                binBox[a][k].grow(tb);
             }
-            F32 lArea[kPlanes], rArea[kPlanes];
-            U32 lCnt[kPlanes], rCnt[kPlanes];
-            AABB lBox, rBox;
-            U32 lSum = 0, rSum = 0;
-            for (int k = 0; k < kPlanes; ++k) {
-                lSum += binCount[k];
-                lCnt[k] = lSum;
-                lBox.grow(binBox[k]);
-                lArea[k] = lBox.area();
-                const int rb = kBins - 1 - k;
-                rSum += binCount[rb];
-                rCnt[rb - 1] = rSum;
-                rBox.grow(binBox[rb]);
-                rArea[rb - 1] = rBox.area();
+        }
+        for (U32 a = 0; a < 3; ++a)
+            if (lo[a] != hi[a]) sweep(binCount[a], binBox[a], lo[a], hi[a], a, bestCost, bestSplit, bestAxis);
+        return bestSplit;
+    }
+
+    /* Same result as plane(): the three axes' key ranges and bins are min/max
+     * and count reductions over parallel chunks, merged in chunk order. */
+    F32 planePar(const BvhNode& n, F32& bestCost, U32& bestAxis) const {
+        bestCost = INFINITY;
+        bestAxis = 0;
+        F32 bestSplit = 0.0f;
+        const U32 first = n.leftFirst, cnt = n.count;
+        const U32 nc = (cnt + kChunk - 1) / kChunk;
+        std::vector<std::array<F32, 6>> rng(nc);
+        forChunks(nc, chunkThreads(), [&](U32 c) {
+            F32 lo[3] = {3.40282347e+38f, 3.40282347e+38f, 3.40282347e+38f};
+            F32 hi[3] = {1.17549435e-38f, 1.17549435e-38f, 1.17549435e-38f};
+            const U32 b = first + c * kChunk, e = std::min(first + cnt, b + kChunk);
+            for (U32 i = b; i < e; ++i)
+                for (U32 a = 0; a < 3; ++a) {
+                    const F32 k = refs[i].key[a];
+                    lo[a] = lo[a] < k ? lo[a] : k;
+                    hi[a] = hi[a] > k ? hi[a] : k;
+                }
+            rng[c] = {lo[0], lo[1], lo[2], hi[0], hi[1], hi[2]};
+        });
+        Bins B;
+        for (U32 a = 0; a < 3; ++a) {
+            F32 lo = 3.40282347e+38f, hi = 1.17549435e-38f;
+            for (U32 c = 0; c < nc; ++c) { lo = lo < rng[c][a] ? lo : rng[c][a]; hi = hi > rng[c][3 + a] ? hi : rng[c][3 + a]; }
+            B.lo[a] = lo; B.hi[a] = hi;
+        }
+        std::vector<Bins> part(nc);
+        forChunks(nc, chunkThreads(), [&](U32 c) {
+            Bins& P = part[c];
+            F32 scaleK[3];
+            for (U32 a = 0; a < 3; ++a) {
+                scaleK[a] = B.lo[a] == B.hi[a] ? 0.0f : (F32)kBins / (B.hi[a] - B.lo[a]);
+                for (int k = 0; k < kBins; ++k) { P.cnt[a][k] = 0; P.box[a][k] = AABB(); }
             }
-            const F32 extent = (hi - lo) / (F32)kBins;
-            for (int k = 0; k < kPlanes; ++k) {
-                const F32 c = (F32)lCnt[k] * lArea[k] + (F32)rCnt[k] * rArea[k];
-                if (c < bestCost) {
-                    bestCost = c;
-                    bestSplit = lo + extent * (F32)(k + 1);
-                    bestAxis = axis;
+            const U32 b = first + c * kChunk, e = std::min(first + cnt, b + kChunk);
+            for (U32 i = b; i < e; ++i) {
+                const PrimRef& pr = refs[i];
+                const AABB& tb = pr.box;
+                for (U32 a = 0; a < 3; ++a) {
+                    if (B.lo[a] == B.hi[a]) continue;
+                    const U32 k = binOf(pr.key[a], B.lo[a], scaleK[a]);
+                    P.cnt[a][k]++;
+                    P.box[a][k].grow(tb);
                 }
             }
+        });
+        for (U32 a = 0; a < 3; ++a) {
+            if (B.lo[a] == B.hi[a]) continue;
+            for (int k = 0; k < kBins; ++k) {
+                B.cnt[a][k] = 0; B.box[a][k] = AABB();
+                for (U32 c = 0; c < nc; ++c) { B.cnt[a][k] += part[c].cnt[a][k]; B.box[a][k].grow(part[c].box[a][k]); }
+            }
+            sweep(B.cnt[a], B.box[a], B.lo[a], B.hi[a], a, bestCost, bestSplit, bestAxis);
         }
         return bestSplit;
     }
 
+    /* partitionNode (bvh.cpp:379-399): the reference's swap loop */
     U32 split(const BvhNode& n, F32 pos, U32 axis) {
         I32 i = (I32)n.leftFirst;
         I32 j = (I32)(n.leftFirst + (n.count - 1));
         while (i <= j) {
-            if (prims.key(idx[i], axis) < pos) ++i;
-            else { std::swap(idx[i], idx[j]); --j; }
+            if (refs[i].key[axis] < pos) ++i;
+            else { std::swap(refs[i], refs[j]); --j; }
         }
         return (U32)i;
     }
 
-    void run(U32 count) {
-        idx.resize(count);
-        for (U32 i = 0; i < count; ++i) idx[i] = i;
-        BvhNode zero;                                /* MALLOC64 + memset(0): root box starts at the origin */
-        zero.leftFirst = 0;
-        zero.count = 0;
-        zero.boundingBox.bbMin = Float3(0.0f);
-        zero.boundingBox.bbMax = Float3(0.0f);
-        nodes.assign(2 * (size_t)count, zero);
-        used = 2;
-        nodes[0].leftFirst = 0;
-        nodes[0].count = count;
-        bounds(0);
-        std::vector<U32> todo{0};
+    /* subdivide (bvh.cpp:401-465) from `start` with an explicit stack; nodes
+     * are appended at `used` (pairs), left subtree first like the recursion. */
+    void grow(U32 start) {
+        std::vector<U32> todo{start};
         while (!todo.empty()) {
             const U32 ni = todo.back();
             todo.pop_back();
@@ -361,21 +507,164 @@ struct SahBuilder {
             if (nl == 0 || nl == nodes[ni].count) continue;
             const U32 l = used, r = used + 1;
             used += 2;
+            if (nodes.size() < used) nodes.resize(std::max<size_t>(used, 2 * nodes.size()));
             nodes[l].leftFirst = nodes[ni].leftFirst; nodes[l].count = nl; nodes[l].boundingBox = AABB();
             nodes[r].leftFirst = pivot; nodes[r].count = nodes[ni].count - nl; nodes[r].boundingBox = AABB();
             nodes[ni].leftFirst = l;
             nodes[ni].count = 0;
-            bounds(l);
-            bounds(r);
-            todo.push_back(r);                        /* left subtree first, like the recursion */
+            bounds(nodes[l]);
+            bounds(nodes[r]);
+            todo.push_back(r);
             todo.push_back(l);
         }
+    }
+
+    /* A subtree built away from the pool: its root record, and either a local
+     * block (sequential build; local slot 0 is the root, children from 1) or
+     * two child subtrees.  size = nodes the subtree allocates in the pool. */
+    struct Sub {
+        BvhNode root;
+        std::vector<BvhNode> block;
+        std::unique_ptr<Sub> l, r;
+        size_t size = 0;
+    };
+
+    std::unique_ptr<Sub> buildSub(BvhNode root) {
+        auto s = std::make_unique<Sub>();
+        if (root.count < kSeqPrims) {
+            std::vector<BvhNode> loc(1, root);
+            U32 u = 1;
+            SahBuilder<Prims> seq{prims, idx, refs, loc, u, 1, nullptr};
+            seq.grow(0);
+            loc.resize(u);
+            s->root = loc[0];
+            s->size = u - 1;
+            s->block = std::move(loc);
+            return s;
+        }
+        F32 cost; U32 axis;
+        const F32 pos = planePar(root, cost, axis);
+        s->root = root;
+        if (cost >= (F32)root.count * root.boundingBox.area()) return s;
+        const U32 pivot = split(root, pos, axis);
+        const U32 nl = pivot - root.leftFirst;
+        if (nl == 0 || nl == root.count) return s;
+        BvhNode L, R;
+        L.leftFirst = root.leftFirst; L.count = nl; L.boundingBox = AABB();
+        R.leftFirst = pivot; R.count = root.count - nl; R.boundingBox = AABB();
+        if (L.count >= kSeqPrims) boundsPar(L); else bounds(L);
+        if (R.count >= kSeqPrims) boundsPar(R); else bounds(R);
+        /* the children own disjoint index ranges: the left one runs on a new
+         * thread while fewer than threads-1 extra builder threads exist */
+        int cur = active->load();
+        bool spawn = false;
+        while (cur < (int)threads - 1 && !(spawn = active->compare_exchange_weak(cur, cur + 1))) {}
+        if (spawn) {
+            std::thread lt([&]() { s->l = buildSub(L); });
+            s->r = buildSub(R);
+            lt.join();
+            active->fetch_sub(1);
+        } else {
+            s->l = buildSub(L);
+            s->r = buildSub(R);
+        }
+        s->root.count = 0;
+        s->size = 2 + s->l->size + s->r->size;
+        return s;
+    }
+
+    /* Writes subtree s with its root at pool slot `at` and its block at
+     * `base`; sequential blocks are queued for a parallel copy. */
+    void place(Sub& s, U32 at, U32 base, std::vector<std::pair<Sub*, U32>>& jobs) {
+        nodes[at] = s.root;
+        if (!s.block.empty()) {
+            if (s.size == 0) return;
+            nodes[at].leftFirst = base + (s.root.leftFirst - 1);
+            jobs.emplace_back(&s, base);
+            return;
+        }
+        if (!s.l) return;                                /* leaf */
+        nodes[at].leftFirst = base;
+        place(*s.l, base, base + 2, jobs);
+        place(*s.r, base + 1, base + 2 + (U32)s.l->size, jobs);
+    }
+
+    void run(U32 count, bool finite) {
+        const bool log = getenv("SURF_BUILD_LOG") != nullptr && count >= kSeqPrims;
+        auto now = []() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+        double t0 = now();
+        auto phase = [&](const char* what) {
+            if (log) fprintf(stderr, "[surf build]   %-12s %8.3f s\n", what, now() - t0);
+            t0 = now();
+        };
+        refs.resize(count);
+        forChunks((count + kChunk - 1) / kChunk, threads, [&](U32 c) {
+            const U32 b = c * kChunk, e = std::min(count, b + kChunk);
+            for (U32 i = b; i < e; ++i) {
+                PrimRef& r = refs[i];
+                for (U32 a = 0; a < 3; ++a) r.key[a] = prims.key(i, a);
+                r.id = i;
+                r.box = AABB();
+                prims.addTo(r.box, i);
+            }
+        });
+        auto ids = [&]() {
+            idx.resize(count);
+            forChunks((count + kChunk - 1) / kChunk, threads, [&](U32 c) {
+                const U32 b = c * kChunk, e = std::min(count, b + kChunk);
+                for (U32 i = b; i < e; ++i) idx[i] = refs[i].id;
+            });
+            std::vector<PrimRef>().swap(refs);
+        };
+        BvhNode zero;                                /* MALLOC64 + memset(0): root box starts at the origin */
+        zero.leftFirst = 0;
+        zero.count = 0;
+        zero.boundingBox.bbMin = Float3(0.0f);
+        zero.boundingBox.bbMax = Float3(0.0f);
+        if (threads <= 1 || !finite || count < kSeqPrims) {
+            nodes.assign(2 * (size_t)count, zero);
+            used = 2;
+            nodes[0].leftFirst = 0;
+            nodes[0].count = count;
+            bounds(nodes[0]);
+            grow(0);
+            ids();
+            return;
+        }
+        /* only [0, used) of the reference's 2*count pool is ever read; node 1 stays zero */
+        BvhNode root = zero;
+        root.count = count;
+        std::atomic<int> act{0};
+        active = &act;
+        boundsPar(root);
+        phase("root bounds");
+        std::unique_ptr<Sub> tree = buildSub(root);
+        phase("subtrees");
+        used = 2 + (U32)tree->size;
+        nodes.clear();
+        nodes.resize(used, zero);
+        phase("pool alloc");
+        std::vector<std::pair<Sub*, U32>> jobs;
+        place(*tree, 0, 2, jobs);
+        forChunks((U32)jobs.size(), threads, [&](U32 j) {
+            const Sub& b = *jobs[j].first;
+            const U32 base = jobs[j].second;
+            for (size_t k = 1; k < b.block.size(); ++k) {
+                BvhNode n = b.block[k];
+                if (n.count == 0) n.leftFirst = base + (n.leftFirst - 1);
+                nodes[base + (k - 1)] = n;
+            }
+        });
+        phase("place");
+        tree.reset();
+        ids();
+        phase("ids, free");
     }
 };
 
 struct MeshPrims {
     const Mesh* mesh;
-    F32 key(U32 p, U32 axis) const { return mesh->triangles[p].centroid[axis]; }
+    F32 key(U32 p, U32 axis) const { return (&mesh->triangles[p].centroid.x)[axis]; }
     void addTo(AABB& b, U32 p) const {
         const Triangle& t = mesh->triangles[p];
         b.grow(t.v0); b.grow(t.v1); b.grow(t.v2);
@@ -405,11 +694,19 @@ U32 depthOf(const std::vector<BvhNode>& nodes, U32 root) {
 
 /* ================================================================= BvhBLAS */
 BvhBLAS::BvhBLAS(Mesh* mesh) : m_mesh(mesh) { build(); }
+BvhBLAS::BvhBLAS(Mesh* mesh, unsigned threads) : m_mesh(mesh) { build(threads); }
 
-void BvhBLAS::build() {
+void BvhBLAS::build() { build(defaultBuildThreads()); }
+
+void BvhBLAS::build(unsigned threads) {
     MeshPrims prims{m_mesh};
-    SahBuilder<MeshPrims> b{prims, m_indices, m_nodes, m_nodesUsed};
-    b.run((U32)m_mesh->triangles.size());
+    std::vector<PrimRef> refs;
+    SahBuilder<MeshPrims> b{prims, m_indices, refs, m_nodes, m_nodesUsed, threads};
+    bool finite = true;
+    for (const Triangle& t : m_mesh->triangles)
+        for (const Float3* v : {&t.v0, &t.v1, &t.v2, &t.centroid})
+            finite = finite && std::isfinite(v->x) && std::isfinite(v->y) && std::isfinite(v->z);
+    b.run((U32)m_mesh->triangles.size(), finite);
 }
 
 /* bvh.cpp:268-287 */
@@ -480,8 +777,9 @@ BvhTLAS::BvhTLAS(std::vector<Instance> instances) : m_instances(std::move(instan
 
 void BvhTLAS::build() {
     InstancePrims prims{&m_instances};
-    SahBuilder<InstancePrims> b{prims, m_indices, m_nodes, m_nodesUsed};
-    b.run((U32)m_instances.size());
+    std::vector<PrimRef> refs;
+    SahBuilder<InstancePrims> b{prims, m_indices, refs, m_nodes, m_nodesUsed, 1};
+    b.run((U32)m_instances.size(), false);
 }
 
 /* bvh.cpp:793-819 */
@@ -637,6 +935,14 @@ namespace {
 /* The scene of the reference's main.cpp:161-346 (and the C5 deep variant). */
 void buildIndoor(surf_scene& S, const std::string& dir, int variant) {
     using namespace surf;
+    /* SURF_BUILD_LOG=1: phase times on stderr */
+    const bool log = getenv("SURF_BUILD_LOG") != nullptr;
+    auto now = []() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+    double t0 = now();
+    auto phase = [&](const char* what) {
+        if (log) fprintf(stderr, "[surf build] %-14s %8.3f s\n", what, now() - t0);
+        t0 = now();
+    };
     for (const char* name : {"susanne", "cube", "lens", "plane"})
         S.meshes.push_back(std::make_unique<Mesh>(dir + "/" + name + ".obj"));
     Mesh* sus = S.meshes[0].get();
@@ -644,6 +950,7 @@ void buildIndoor(surf_scene& S, const std::string& dir, int variant) {
     Mesh* lens = S.meshes[2].get();
     Mesh* plane = S.meshes[3].get();
     Mesh* lattice = nullptr;
+    phase("obj load");
     if (variant == 1) {
         /* C5: 648 Suzannes, translate(-8+2i, -0.4+1.2j, -4+1.5k) * scale(0.5), one mesh */
         auto m = std::make_unique<Mesh>();
@@ -663,8 +970,11 @@ void buildIndoor(surf_scene& S, const std::string& dir, int variant) {
         lattice = m.get();
         S.meshes.push_back(std::move(m));
     }
+    phase("lattice mesh");
     for (Mesh* m : {sus, cube, lens, plane}) S.blases.push_back(std::make_unique<BvhBLAS>(m));
+    phase("blas build");
     if (lattice) S.blases.push_back(std::make_unique<BvhBLAS>(lattice));
+    phase("lattice blas");
     BvhBLAS* susB = S.blases[0].get();
     BvhBLAS* cubeB = S.blases[1].get();
     BvhBLAS* lensB = S.blases[2].get();
@@ -700,7 +1010,9 @@ void buildIndoor(surf_scene& S, const std::string& dir, int variant) {
     bg.type = BackgroundType::ColorGradient;
     bg.gradient.colorA = Float3(0.8f, 0.8f, 0.8f);
     bg.gradient.colorB = Float3(0.1f, 0.4f, 0.6f);
+    phase("instances");
     S.scene = std::make_unique<GPUScene>(&S.context, bg, std::move(inst));
+    phase("tlas + batch");
 }
 
 }  // namespace
@@ -751,5 +1063,23 @@ int surf_scene_bvh_depths(const surf_scene* scene, uint32_t* tlas_depth, uint32_
 }
 
 void surf_scene_destroy(surf_scene* scene) { delete scene; }
+
+int surf_bvh_build(const surf_triangle* triangles, uint32_t count, uint32_t threads, uint32_t* indices_out,
+                   surf_bvh_node* nodes_out, uint32_t* nodes_used) {
+    if (!triangles || count == 0 || !indices_out || !nodes_out || !nodes_used) return SURF_ERR_INVALID;
+    try {
+        surf::Mesh mesh;
+        mesh.triangles.resize(count, surf::Triangle(surf::Float3(0.0f), surf::Float3(0.0f), surf::Float3(0.0f)));
+        std::memcpy(static_cast<void*>(mesh.triangles.data()), triangles, (size_t)count * sizeof(surf_triangle));
+        surf::BvhBLAS b(&mesh, threads ? threads : surf::defaultBuildThreads());
+        std::memcpy(indices_out, b.indices(), (size_t)count * sizeof(uint32_t));
+        std::memcpy(nodes_out, b.nodePool(), (size_t)b.nodesUsed() * sizeof(surf_bvh_node));
+        *nodes_used = b.nodesUsed();
+    } catch (const std::exception& e) {
+        fprintf(stderr, "surf_bvh_build: %s\n", e.what());
+        return SURF_ERR_OOM;
+    }
+    return SURF_OK;
+}
 
 }  // extern "C"

@@ -113,6 +113,7 @@ def load() -> C.CDLL:
         "surf_scene_camera": ([P, U32, U32, P], I32),
         "surf_scene_bvh_depths": ([P, C.POINTER(U32), C.POINTER(U32)], I32),
         "surf_scene_destroy": ([P], None),
+        "surf_bvh_build": ([P, U32, U32, P, P, C.POINTER(U32)], I32),
         "surf_ref_sinf": ([F], F), "surf_ref_cosf": ([F], F), "surf_ref_expf": ([F], F),
     }
     for name, (args, res) in sig.items():
@@ -197,6 +198,20 @@ class Scene:
             self.close()
         except Exception:
             pass
+
+
+def bvh_build(triangles: np.ndarray, threads: int = 0) -> tuple[np.ndarray, np.ndarray]:
+    """BvhBLAS::build (bvh.cpp:255-465) over (n, 16) float32 Triangle records
+    (v0, v1, v2, centroid), multi-threaded (0 = default thread count).
+    Returns (indices (n,) uint32, nodes (nodes_used, 12) float32 view of the
+    48-B BvhNode records); identical for every thread count."""
+    tris = np.ascontiguousarray(triangles, dtype=np.float32)
+    n = tris.shape[0]
+    idx = np.empty(n, np.uint32)
+    nodes = np.zeros((2 * n, 12), np.float32)
+    used = C.c_uint32()
+    _check(load().surf_bvh_build(_ptr(tris), n, threads, _ptr(idx), _ptr(nodes), C.byref(used)), "surf_bvh_build")
+    return idx, nodes[: used.value]
 
 
 @dataclass

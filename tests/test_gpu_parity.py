@@ -249,3 +249,27 @@ def test_animation_update_render_bitexact():
     finally:
         o.close()
         p.close()
+
+
+def test_c5_deep_bvh_bitexact():
+    """C5: 10.2M-triangle lattice BLAS (HBM-resident, depth 36,
+    built by the parallel builder) -- hit records and a small render equal the
+    oracle's, whose BLAS comes from the reference's sequential build."""
+    W, H, F = 64, 48, 2
+    o = oracle.OracleScene(variant=1)
+    p = surf_amd.Scene.indoor(variant=1)
+    try:
+        r = surf_amd.Renderer(p, W, H)
+        (eo, ed), _ = o.record_rays(W, H, 0, 0, W * H)
+        g = r.trace_closest(eo, ed)
+        c = o.trace_closest(eo, ed)
+        for k in range(5):
+            assert np.array_equal(np.asarray(g[k]).view(np.uint32), np.asarray(c[k]).view(np.uint32)), f"hit field {k}"
+        r.set_zero_cutoff(False)
+        r.render(F, 0, 0)
+        c, _, _ = o.render(W, H, F)
+        _assert_bitexact(r.accumulator(), c, "C5 64x48x2")
+        r.close()
+    finally:
+        o.close()
+        p.close()

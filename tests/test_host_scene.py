@@ -72,3 +72,27 @@ def test_animation_update_identical():
     finally:
         o.close()
         p.close()
+
+
+def test_c5_deep_scene_identical():
+    """C5: 648 Suzannes baked into one 10.2M-triangle mesh.  The
+    product builds its BLAS with the parallel builder (row f1); the oracle with
+    the reference's sequential recursion.  Buffers and depths must agree."""
+    import surf_amd
+    o = oracle.OracleScene(variant=1)
+    p = surf_amd.Scene.indoor(variant=1)
+    try:
+        assert o.bvh_depths() == p.bvh_depths()
+        assert p.bvh_depths()[1] < 64, "BLAS deeper than the 64-entry traversal stack"
+        a, b = o.export(), p.buffers()
+        for buf in ("blas_indices", "blas_nodes", "triangles", "instances", "tlas_nodes", "lights"):
+            rec, ranges = MASK[buf]
+            x = np.frombuffer(a[buf], np.uint8).reshape(-1, rec)
+            y = np.frombuffer(b[buf], np.uint8).reshape(-1, rec)
+            assert x.shape == y.shape, buf
+            for lo, hi in ranges:
+                assert np.array_equal(x[:, lo:hi], y[:, lo:hi]), f"{buf} bytes {lo}:{hi}"
+            del x, y
+    finally:
+        o.close()
+        p.close()
