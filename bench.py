@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--cpu-frames", type=int, default=48, help="frames of the CPU baseline sample (full frame)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--tail", type=str, default="", help="tuning: drain policy 'threshold,lanes_per_wave,stage_segments'")
+    ap.add_argument("--persistent", type=int, default=-1, help="tuning: force the out-of-step traversal on (1) / off (0)")
     ap.add_argument("--profile-pass", type=int, default=-1,
                     help="steps re-run with per-kernel HIP events for the roofline (-1 = --steps, same composition as the timed run)")
     return ap.parse_args()
@@ -107,6 +109,10 @@ def main():
     scene_build_s = time.perf_counter() - tb
     spec = surf_amd.ShardSpec(rank, world, args.row_block if world > 1 else 0)
     r = surf_amd.Renderer(scene, W, H, device=local, shard=spec)
+    if args.tail:
+        r.set_tail_policy(*[int(x) for x in args.tail.split(",")])
+    if args.persistent >= 0:
+        r.set_persistent(bool(args.persistent))
     rows = len(r.rows)
     acc_dev = torch.empty((rows, W, 4), dtype=torch.float32, device=dev)
     gather = None

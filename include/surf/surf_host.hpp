@@ -122,6 +122,7 @@ struct alignas(16) TriExtension {
 class Mesh {
 public:
     explicit Mesh(const std::string& path);      /* reads .obj or .obj.gz; throws std::runtime_error */
+    Mesh(const std::string& path, unsigned threads);   /* parallel parse; same arrays for any thread count */
     Mesh() = default;
     std::vector<Triangle> triangles;
     std::vector<TriExtension> triExtensions;

@@ -255,6 +255,16 @@ int surf_scene_camera(const surf_scene* scene, uint32_t width, uint32_t height, 
 int surf_scene_bvh_depths(const surf_scene* scene, uint32_t* tlas_depth, uint32_t* max_blas_depth);
 void surf_scene_destroy(surf_scene* scene);
 
+/* Mesh::Mesh(path) (sources/mesh.cpp:69-154, tinyobjloader triangulate=true):
+ * .obj or .obj.gz parsed in parallel chunks (threads = 0: default count).  The
+ * triangles (64 B reference Triangle, OBJ corner 0 stored in v1) and
+ * TriExtensions (80 B) are identical for every thread count. */
+typedef struct surf_mesh surf_mesh;
+int surf_obj_load(const char* path, uint32_t threads, surf_mesh** out);
+int surf_mesh_data(const surf_mesh* mesh, const surf_triangle** triangles, const surf_tri_extension** tri_ext,
+                   uint32_t* count);
+void surf_mesh_destroy(surf_mesh* mesh);
+
 /* BvhBLAS::build (sources/bvh.cpp:255-465: binned SAH, 8 bins, pre-order pair
  * allocation) over `count` reference Triangles, multi-threaded (threads = 0:
  * SURF_BUILD_THREADS / OMP_NUM_THREADS / hardware).  Writes the reference's

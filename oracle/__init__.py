@@ -61,6 +61,7 @@ def load():
         "orc_finalize_rgba8": ([P, U32, F, P], None),
         "orc_set_zero_cutoff": ([I32], None),
         "orc_bvh_build": ([P, U32, P, P], U32),
+        "orc_obj_load": ([C.c_char_p, P, P, C.c_uint64], C.c_long),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)
@@ -221,4 +222,16 @@ def bvh_build(tris: np.ndarray):
     nodes = np.zeros((2 * n, 12), np.float32)
     used = load().orc_bvh_build(_p(tris), n, _p(idx), _p(nodes))
     return idx, nodes[:used]
+
+
+def obj_load(path: str):
+    """Mesh(path) with tinyobj semantics: ((n, 16) float32 Triangle records,
+    (n, 20) float32 TriExtension records)."""
+    n = load().orc_obj_load(path.encode(), None, None, 0)
+    if n < 0:
+        raise OSError(f"oracle: cannot read {path}")
+    tris = np.zeros((n, 16), np.float32)
+    ext = np.zeros((n, 20), np.float32)
+    load().orc_obj_load(path.encode(), _p(tris), _p(ext), n)
+    return tris, ext
 

@@ -1078,6 +1078,30 @@ void orc_bvh_depths(const orc_scene* h, uint32_t* td, uint32_t* bd) {
     *bd = m;
 }
 
+/* Mesh(path): returns the triangle count (-1 if unreadable); with non-NULL
+ * outputs writes 64-B Triangle and 80-B TriExtension records (up to cap). */
+long orc_obj_load(const char* path, float* trisOut, float* extOut, uint64_t cap) {
+    Mesh m;
+    if (!loadObj(path, m)) return -1;
+    if (trisOut && extOut) {
+        const size_t n = std::min<size_t>(m.tris.size(), cap);
+        for (size_t i = 0; i < n; ++i) {
+            float* t = trisOut + 16 * i;
+            memset(t, 0, 64);
+            const Tri& r = m.tris[i];
+            t[0] = r.v0.x; t[1] = r.v0.y; t[2] = r.v0.z; t[4] = r.v1.x; t[5] = r.v1.y; t[6] = r.v1.z;
+            t[8] = r.v2.x; t[9] = r.v2.y; t[10] = r.v2.z; t[12] = r.c.x; t[13] = r.c.y; t[14] = r.c.z;
+            float* x = extOut + 20 * i;
+            memset(x, 0, 80);
+            const TriExt& e = m.ext[i];
+            x[0] = e.n0.x; x[1] = e.n0.y; x[2] = e.n0.z; x[4] = e.n1.x; x[5] = e.n1.y; x[6] = e.n1.z;
+            x[8] = e.n2.x; x[9] = e.n2.y; x[10] = e.n2.z;
+            for (int j = 0; j < 6; ++j) x[12 + j] = e.uv[j];
+        }
+    }
+    return (long)m.tris.size();
+}
+
 /* BvhBLAS::build over raw reference Triangles (64 B: v0, v1, v2, centroid at
  * 16-B strides); writes the index permutation and the node pool as 48-B
  * BvhNode records (leftFirst, count, pad, bbMin, pad, bbMax, pad).  Sequential,

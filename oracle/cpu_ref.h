@@ -106,6 +106,8 @@ void orc_bvh_depths(const orc_scene*, uint32_t* tlas_depth, uint32_t* max_blas_d
 /* Ends paths whose throughput is exactly zero (radiance-neutral; see cpu_ref.cpp).
  * Default off = reference semantics. */
 void orc_set_zero_cutoff(int on);
+/* tinyobj-semantics OBJ load (Mesh(path)); -1 if unreadable. */
+long orc_obj_load(const char* path, float* tris_out, float* ext_out, uint64_t cap);
 /* Sequential BvhBLAS::build over n 64-B Triangles; returns nodesUsed. */
 uint32_t orc_bvh_build(const float* tris, uint32_t n, uint32_t* idx_out, float* nodes_out);
 

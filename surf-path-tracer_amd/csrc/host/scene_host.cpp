@@ -137,9 +137,47 @@ Triangle::Triangle(Float3 a, Float3 b, Float3 c) : v0(b), v1(a), v2(c), centroid
     centroid = (v0 + v1 + v2) * 0.333f;               /* mesh.cpp:20 */
 }
 
+unsigned defaultBuildThreads() {
+    if (const char* e = getenv("SURF_BUILD_THREADS")) { const int v = atoi(e); if (v > 0) return (unsigned)v; }
+    if (const char* e = getenv("OMP_NUM_THREADS")) { const int v = atoi(e); if (v > 0) return (unsigned)v; }
+    const unsigned hc = std::thread::hardware_concurrency();
+    return hc ? std::min(hc, 64u) : 1u;
+}
+
 namespace {
 
+/* Runs f(chunk) for chunk in [0, n) on up to `threads` threads. */
+template <class F>
+void forChunks(U32 n, unsigned threads, F&& f) {
+    const unsigned t = std::min<unsigned>(threads, n);
+    if (t <= 1) { for (U32 c = 0; c < n; ++c) f(c); return; }
+    std::atomic<U32> next{0};
+    auto work = [&]() { for (U32 c; (c = next.fetch_add(1)) < n;) f(c); };
+    std::vector<std::thread> pool;
+    for (unsigned i = 1; i < t; ++i) pool.emplace_back(work);
+    work();
+    for (auto& th : pool) th.join();
+}
+
 std::string slurp(const std::string& path) {
+    /* plain files in one read; gzip (magic 1f 8b) through zlib */
+    if (FILE* f = fopen(path.c_str(), "rb")) {
+        unsigned char magic[2] = {0, 0};
+        const size_t m = fread(magic, 1, 2, f);
+        if (!(m == 2 && magic[0] == 0x1f && magic[1] == 0x8b) && fseek(f, 0, SEEK_END) == 0) {
+            const long size = ftell(f);
+            std::string out;
+            if (size >= 0) {
+                out.resize((size_t)size);
+                rewind(f);
+                const size_t got = size ? fread(&out[0], 1, (size_t)size, f) : 0;
+                fclose(f);
+                if (got != (size_t)size) throw std::runtime_error("short read " + path);
+                return out;
+            }
+        }
+        fclose(f);
+    }
     gzFile f = gzopen(path.c_str(), "rb");
     if (!f) throw std::runtime_error("cannot open " + path);
     std::string out;
@@ -162,93 +200,186 @@ inline long objIndex(long raw, size_t count) {
 
 struct Corner { long v = -1, t = -1, n = -1; };
 
-/* tinyobjloader-compatible reader (triangulate = true).  Floats parse through
- * double then narrow to float, like tinyobj's real_t = float path. */
-void parseObj(const std::string& text, Mesh& mesh) {
+/* OBJ ingestion: tinyobjloader-compatible semantics
+ * (mesh.cpp:69-154, triangulate = true) parsed in parallel chunks.
+ *
+ * The text is cut into chunks at line starts.  Pass 1 (parallel) parses every
+ * chunk on its own: v / vn / vt records into chunk-local arrays and faces as
+ * raw OBJ indices together with the chunk-local record counts at that line --
+ * all a relative (negative) index needs.  A prefix sum over the chunks' counts
+ * then fixes every record's global position, so pass 2 (parallel) resolves the
+ * indices exactly as a front-to-back reader would (1-based, or relative to the
+ * records read so far) and writes the triangles at their global offsets.
+ * Lines are cut at '\n' in place, so every number is parsed from a
+ * NUL-terminated line, exactly like the line-by-line reader.  Floats go through
+ * strtod then narrow to float (tinyobj's real_t = float path). */
+struct ObjFace {
+    uint32_t first, n;               /* corners [first, first + n) of the chunk */
+    uint32_t lv, lt, ln;             /* chunk-local record counts before this face */
+};
+struct RawCorner { long v, t, n; bool hasT, hasN; };
+struct ObjChunk {
+    char* b = nullptr;
+    char* e = nullptr;
     std::vector<F32> pos, nrm, tex;
-    std::vector<Corner> corners;          /* three per triangle */
-    const char* p = text.data();
-    const char* end = p + text.size();
-    while (p < end) {
-        const char* eol = static_cast<const char*>(memchr(p, '\n', (size_t)(end - p)));
-        if (!eol) eol = end;
-        std::string line(p, eol);
+    std::vector<RawCorner> corners;
+    std::vector<ObjFace> faces;
+    size_t tris = 0;
+};
+
+void parseChunk(ObjChunk& C) {
+    char* p = C.b;
+    while (p < C.e) {
+        char* eol = static_cast<char*>(memchr(p, '\n', (size_t)(C.e - p)));
+        if (!eol) eol = C.e;
+        *eol = '\0';                                    /* one NUL-terminated line */
+        const char* s = p;
         p = eol + 1;
-        const char* s = line.c_str();
         while (*s == ' ' || *s == '\t') ++s;
         auto floats = [&](const char* q, int k, std::vector<F32>& dst) {
             char* e = nullptr;
             for (int i = 0; i < k; ++i) { dst.push_back((F32)strtod(q, &e)); q = e; }
         };
-        if (s[0] == 'v' && (s[1] == ' ' || s[1] == '\t')) floats(s + 2, 3, pos);
-        else if (s[0] == 'v' && s[1] == 'n') floats(s + 2, 3, nrm);
-        else if (s[0] == 'v' && s[1] == 't') floats(s + 2, 2, tex);
+        if (s[0] == 'v' && (s[1] == ' ' || s[1] == '\t')) floats(s + 2, 3, C.pos);
+        else if (s[0] == 'v' && s[1] == 'n') floats(s + 2, 3, C.nrm);
+        else if (s[0] == 'v' && s[1] == 't') floats(s + 2, 2, C.tex);
         else if (s[0] == 'f' && (s[1] == ' ' || s[1] == '\t')) {
-            std::vector<Corner> face;
+            ObjFace f;
+            f.first = (uint32_t)C.corners.size();
+            f.lv = (uint32_t)(C.pos.size() / 3); f.lt = (uint32_t)(C.tex.size() / 2); f.ln = (uint32_t)(C.nrm.size() / 3);
             const char* q = s + 1;
             while (true) {
                 while (*q == ' ' || *q == '\t' || *q == '\r') ++q;
                 if (*q == '\0') break;
-                Corner c;
+                RawCorner c{0, 0, 0, false, false};
                 char* e = nullptr;
-                c.v = objIndex(strtol(q, &e, 10), pos.size() / 3);
+                c.v = strtol(q, &e, 10);
                 q = e;
                 if (*q == '/') {
                     ++q;
-                    if (*q != '/') { c.t = objIndex(strtol(q, &e, 10), tex.size() / 2); q = e; }
-                    if (*q == '/') { ++q; c.n = objIndex(strtol(q, &e, 10), nrm.size() / 3); q = e; }
+                    if (*q != '/') { c.t = strtol(q, &e, 10); c.hasT = true; q = e; }
+                    if (*q == '/') { ++q; c.n = strtol(q, &e, 10); c.hasN = true; q = e; }
                 }
-                face.push_back(c);
+                C.corners.push_back(c);
                 while (*q && *q != ' ' && *q != '\t') ++q;
             }
-            const size_t n = face.size();
-            if (n < 3) continue;
-            if (n == 4) {
-                /* quad: split on the shorter diagonal; ties -> (0,1,3),(1,2,3) */
-                auto P = [&](int k) { const long v = face[k].v; return Float3(pos[3 * v], pos[3 * v + 1], pos[3 * v + 2]); };
-                const Float3 d02 = P(2) - P(0), d13 = P(3) - P(1);
-                const F32 l02 = d02.x * d02.x + d02.y * d02.y + d02.z * d02.z;
-                const F32 l13 = d13.x * d13.x + d13.y * d13.y + d13.z * d13.z;
-                static const int kA[6] = {0, 1, 2, 0, 2, 3}, kB[6] = {0, 1, 3, 1, 2, 3};
-                const int* k = (l02 < l13) ? kA : kB;
-                for (int j = 0; j < 6; ++j) corners.push_back(face[k[j]]);
-            } else {
-                for (size_t j = 1; j + 1 < n; ++j) { corners.push_back(face[0]); corners.push_back(face[j]); corners.push_back(face[j + 1]); }
-            }
+            f.n = (uint32_t)(C.corners.size() - f.first);
+            if (f.n < 3) { C.corners.resize(f.first); continue; }
+            C.faces.push_back(f);
+            C.tris += f.n - 2;                          /* quad: 2, n-gon fan: n - 2 */
         }
     }
-    auto vtx = [&](const Corner& c) {
-        if (c.v < 0 || (size_t)(3 * c.v + 2) >= pos.size()) throw std::runtime_error("OBJ vertex index out of range");
-        return Float3(pos[3 * c.v], pos[3 * c.v + 1], pos[3 * c.v + 2]);
-    };
-    auto nor = [&](const Corner& c) {
-        if (c.n < 0 || (size_t)(3 * c.n + 2) >= nrm.size()) return Float3(0.0f);
-        return Float3(nrm[3 * c.n], nrm[3 * c.n + 1], nrm[3 * c.n + 2]);
-    };
-    auto uv = [&](const Corner& c) {
-        if (c.t < 0 || (size_t)(2 * c.t + 1) >= tex.size()) return Float2(0.0f, 0.0f);
-        return Float2(tex[2 * c.t], tex[2 * c.t + 1]);
-    };
-    const size_t nt = corners.size() / 3;
-    mesh.triangles.reserve(nt);
-    mesh.triExtensions.reserve(nt);
-    for (size_t t = 0; t < nt; ++t) {
-        const Corner* c = &corners[3 * t];
-        mesh.triangles.emplace_back(vtx(c[0]), vtx(c[1]), vtx(c[2]));
-        TriExtension x;
-        x.n0 = nor(c[0]); x.n1 = nor(c[1]); x.n2 = nor(c[2]);
-        x.uv0 = uv(c[0]); x.uv1 = uv(c[1]); x.uv2 = uv(c[2]);
-        mesh.triExtensions.push_back(x);
+}
+
+void parseObj(std::string& text, Mesh& mesh, unsigned threads) {
+    const size_t len = text.size();
+    if (len == 0) return;
+    char* base = &text[0];
+    /* chunks of >= 1 MiB starting at line starts */
+    const size_t want = std::max<size_t>(1, std::min<size_t>((size_t)threads * 4, len / (1u << 20) + 1));
+    std::vector<ObjChunk> chunks;
+    size_t at = 0;
+    for (size_t k = 0; k < want && at < len; ++k) {
+        size_t end = (k + 1 == want) ? len : std::max(at, len * (k + 1) / want);
+        if (end < len) {
+            const char* nl = static_cast<const char*>(memchr(base + end, '\n', len - end));
+            end = nl ? (size_t)(nl - base) + 1 : len;
+        }
+        ObjChunk c;
+        c.b = base + at;
+        c.e = base + end;
+        chunks.push_back(std::move(c));
+        at = end;
     }
+    const U32 nc = (U32)chunks.size();
+    forChunks(nc, threads, [&](U32 k) { parseChunk(chunks[k]); });
+    /* global record offsets of every chunk */
+    std::vector<size_t> vBase(nc + 1, 0), tBase(nc + 1, 0), nBase(nc + 1, 0), triBase(nc + 1, 0);
+    for (U32 k = 0; k < nc; ++k) {
+        vBase[k + 1] = vBase[k] + chunks[k].pos.size() / 3;
+        tBase[k + 1] = tBase[k] + chunks[k].tex.size() / 2;
+        nBase[k + 1] = nBase[k] + chunks[k].nrm.size() / 3;
+        triBase[k + 1] = triBase[k] + chunks[k].tris;
+    }
+    std::vector<F32> pos(3 * vBase[nc]), nrm(3 * nBase[nc]), tex(2 * tBase[nc]);
+    forChunks(nc, threads, [&](U32 k) {
+        std::copy(chunks[k].pos.begin(), chunks[k].pos.end(), pos.begin() + 3 * vBase[k]);
+        std::copy(chunks[k].nrm.begin(), chunks[k].nrm.end(), nrm.begin() + 3 * nBase[k]);
+        std::copy(chunks[k].tex.begin(), chunks[k].tex.end(), tex.begin() + 2 * tBase[k]);
+        std::vector<F32>().swap(chunks[k].pos);
+        std::vector<F32>().swap(chunks[k].nrm);
+        std::vector<F32>().swap(chunks[k].tex);
+    });
+    const size_t nt = triBase[nc];
+    mesh.triangles.assign(nt, Triangle(Float3(0.0f), Float3(0.0f), Float3(0.0f)));
+    mesh.triExtensions.assign(nt, TriExtension{});
+    std::atomic<bool> bad{false};
+    forChunks(nc, threads, [&](U32 k) {
+        const ObjChunk& C = chunks[k];
+        size_t out = triBase[k];
+        auto resolve = [&](const RawCorner& r, const ObjFace& f) {
+            Corner c;
+            c.v = objIndex(r.v, vBase[k] + f.lv);
+            if (r.hasT) c.t = objIndex(r.t, tBase[k] + f.lt);
+            if (r.hasN) c.n = objIndex(r.n, nBase[k] + f.ln);
+            return c;
+        };
+        auto vtx = [&](const Corner& c, bool& ok) {
+            if (c.v < 0 || (size_t)(3 * c.v + 2) >= pos.size()) { ok = false; return Float3(0.0f); }
+            return Float3(pos[3 * c.v], pos[3 * c.v + 1], pos[3 * c.v + 2]);
+        };
+        auto nor = [&](const Corner& c) {
+            if (c.n < 0 || (size_t)(3 * c.n + 2) >= nrm.size()) return Float3(0.0f);
+            return Float3(nrm[3 * c.n], nrm[3 * c.n + 1], nrm[3 * c.n + 2]);
+        };
+        auto uv = [&](const Corner& c) {
+            if (c.t < 0 || (size_t)(2 * c.t + 1) >= tex.size()) return Float2(0.0f, 0.0f);
+            return Float2(tex[2 * c.t], tex[2 * c.t + 1]);
+        };
+        bool ok = true;
+        Corner face[64];
+        std::vector<Corner> big;
+        for (const ObjFace& f : C.faces) {
+            Corner* fc = face;
+            if (f.n > 64) { big.resize(f.n); fc = big.data(); }
+            for (uint32_t j = 0; j < f.n; ++j) fc[j] = resolve(C.corners[f.first + j], f);
+            auto emit = [&](const Corner& a, const Corner& b, const Corner& c) {
+                mesh.triangles[out] = Triangle(vtx(a, ok), vtx(b, ok), vtx(c, ok));
+                TriExtension& x = mesh.triExtensions[out];
+                x.n0 = nor(a); x.n1 = nor(b); x.n2 = nor(c);
+                x.uv0 = uv(a); x.uv1 = uv(b); x.uv2 = uv(c);
+                ++out;
+            };
+            if (f.n == 4) {
+                /* quad: split on the shorter diagonal; ties -> (0,1,3),(1,2,3) */
+                const Float3 d02 = vtx(fc[2], ok) - vtx(fc[0], ok), d13 = vtx(fc[3], ok) - vtx(fc[1], ok);
+                const F32 l02 = d02.x * d02.x + d02.y * d02.y + d02.z * d02.z;
+                const F32 l13 = d13.x * d13.x + d13.y * d13.y + d13.z * d13.z;
+                if (l02 < l13) { emit(fc[0], fc[1], fc[2]); emit(fc[0], fc[2], fc[3]); }
+                else { emit(fc[0], fc[1], fc[3]); emit(fc[1], fc[2], fc[3]); }
+            } else {
+                for (uint32_t j = 1; j + 1 < f.n; ++j) emit(fc[0], fc[j], fc[j + 1]);
+            }
+        }
+        if (!ok) bad = true;
+    });
+    if (bad) throw std::runtime_error("OBJ vertex index out of range");
 }
 
 }  // namespace
 
-Mesh::Mesh(const std::string& path) {
+Mesh::Mesh(const std::string& path) : Mesh(path, defaultBuildThreads()) {}
+
+Mesh::Mesh(const std::string& path, unsigned threads) {
+    const bool log = getenv("SURF_BUILD_LOG") != nullptr;
+    auto now = []() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+    const double t0 = now();
     std::string text;
     try { text = slurp(path); }
     catch (const std::exception&) { text = slurp(path + ".gz"); }
-    parseObj(text, *this);
+    const double t1 = now();
+    parseObj(text, *this, std::max(1u, threads));
+    if (log) fprintf(stderr, "[surf obj] %s: read %.3f s, parse %.3f s, %zu triangles\n", path.c_str(), t1 - t0, now() - t1, triangles.size());
 }
 
 /* =================================================================== AABB */
@@ -284,13 +415,6 @@ constexpr U32 kChunk = 1u << 16;             /* prims per binning chunk */
 
 }  // namespace
 
-unsigned defaultBuildThreads() {
-    if (const char* e = getenv("SURF_BUILD_THREADS")) { const int v = atoi(e); if (v > 0) return (unsigned)v; }
-    if (const char* e = getenv("OMP_NUM_THREADS")) { const int v = atoi(e); if (v > 0) return (unsigned)v; }
-    const unsigned hc = std::thread::hardware_concurrency();
-    return hc ? std::min(hc, 64u) : 1u;
-}
-
 namespace {
 
 /* Per-axis bins of one node (bvh.cpp:302-340). */
@@ -299,19 +423,6 @@ struct Bins {
     U32 cnt[3][kBins];
     AABB box[3][kBins];
 };
-
-/* Runs f(chunk) for chunk in [0, n) on up to `threads` threads. */
-template <class F>
-void forChunks(U32 n, unsigned threads, F&& f) {
-    const unsigned t = std::min<unsigned>(threads, n);
-    if (t <= 1) { for (U32 c = 0; c < n; ++c) f(c); return; }
-    std::atomic<U32> next{0};
-    auto work = [&]() { for (U32 c; (c = next.fetch_add(1)) < n;) f(c); };
-    std::vector<std::thread> pool;
-    for (unsigned i = 1; i < t; ++i) pool.emplace_back(work);
-    work();
-    for (auto& th : pool) th.join();
-}
 
 /* A primitive as the build sees it: its binning key, its id and its box (the
  * box of its vertices, or the instance bounds).  The build permutes these
@@ -1063,6 +1174,32 @@ int surf_scene_bvh_depths(const surf_scene* scene, uint32_t* tlas_depth, uint32_
 }
 
 void surf_scene_destroy(surf_scene* scene) { delete scene; }
+
+struct surf_mesh { surf::Mesh mesh; };
+
+int surf_obj_load(const char* path, uint32_t threads, surf_mesh** out) {
+    if (!path || !out) return SURF_ERR_INVALID;
+    *out = nullptr;
+    try {
+        auto m = std::make_unique<surf_mesh>();
+        m->mesh = surf::Mesh(path, threads ? threads : surf::defaultBuildThreads());
+        *out = m.release();
+    } catch (const std::exception& e) {
+        fprintf(stderr, "surf_obj_load: %s\n", e.what());
+        return SURF_ERR_IO;
+    }
+    return SURF_OK;
+}
+
+int surf_mesh_data(const surf_mesh* m, const surf_triangle** triangles, const surf_tri_extension** tri_ext, uint32_t* count) {
+    if (!m || !triangles || !tri_ext || !count) return SURF_ERR_INVALID;
+    *triangles = reinterpret_cast<const surf_triangle*>(m->mesh.triangles.data());
+    *tri_ext = reinterpret_cast<const surf_tri_extension*>(m->mesh.triExtensions.data());
+    *count = (uint32_t)m->mesh.triangles.size();
+    return SURF_OK;
+}
+
+void surf_mesh_destroy(surf_mesh* m) { delete m; }
 
 int surf_bvh_build(const surf_triangle* triangles, uint32_t count, uint32_t threads, uint32_t* indices_out,
                    surf_bvh_node* nodes_out, uint32_t* nodes_used) {

@@ -114,6 +114,9 @@ def load() -> C.CDLL:
         "surf_scene_bvh_depths": ([P, C.POINTER(U32), C.POINTER(U32)], I32),
         "surf_scene_destroy": ([P], None),
         "surf_bvh_build": ([P, U32, U32, P, P, C.POINTER(U32)], I32),
+        "surf_obj_load": ([C.c_char_p, U32, C.POINTER(P)], I32),
+        "surf_mesh_data": ([P, C.POINTER(P), C.POINTER(P), C.POINTER(U32)], I32),
+        "surf_mesh_destroy": ([P], None),
         "surf_ref_sinf": ([F], F), "surf_ref_cosf": ([F], F), "surf_ref_expf": ([F], F),
     }
     for name, (args, res) in sig.items():
@@ -198,6 +201,23 @@ class Scene:
             self.close()
         except Exception:
             pass
+
+
+def obj_load(path: str, threads: int = 0) -> tuple[np.ndarray, np.ndarray]:
+    """Mesh(path) (mesh.cpp:69-154): parallel tinyobj-compatible OBJ/OBJ.GZ parse.
+    Returns ((n, 16) float32 Triangle records, (n, 20) float32 TriExtension
+    records); identical for every thread count."""
+    h = C.c_void_p()
+    _check(load().surf_obj_load(path.encode(), threads, C.byref(h)), "surf_obj_load")
+    try:
+        tp, xp, n = C.c_void_p(), C.c_void_p(), C.c_uint32()
+        _check(load().surf_mesh_data(h, C.byref(tp), C.byref(xp), C.byref(n)), "surf_mesh_data")
+        k = n.value
+        tris = np.ctypeslib.as_array(C.cast(tp, C.POINTER(C.c_float)), (k * 16,)).reshape(k, 16).copy() if k else np.zeros((0, 16), np.float32)
+        ext = np.ctypeslib.as_array(C.cast(xp, C.POINTER(C.c_float)), (k * 20,)).reshape(k, 20).copy() if k else np.zeros((0, 20), np.float32)
+    finally:
+        load().surf_mesh_destroy(h)
+    return tris, ext
 
 
 def bvh_build(triangles: np.ndarray, threads: int = 0) -> tuple[np.ndarray, np.ndarray]:
