@@ -52,6 +52,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--tail", type=str, default="", help="tuning: drain policy 'threshold,lanes_per_wave,stage_segments'")
+    ap.add_argument("--tail-coop", type=int, default=-1, help="tuning: cooperative drain when <= N paths remain")
+    ap.add_argument("--long", type=str, default="", help="tuning: long-path worker 'escape_segments,budget'")
     ap.add_argument("--persistent", type=int, default=-1, help="tuning: force the out-of-step traversal on (1) / off (0)")
     ap.add_argument("--profile-pass", type=int, default=-1,
                     help="steps re-run with per-kernel HIP events for the roofline (-1 = --steps, same composition as the timed run)")
@@ -111,6 +113,10 @@ def main():
     r = surf_amd.Renderer(scene, W, H, device=local, shard=spec)
     if args.tail:
         r.set_tail_policy(*[int(x) for x in args.tail.split(",")])
+    if args.tail_coop >= 0:
+        r.set_tail_coop(args.tail_coop)
+    if args.long:
+        r.set_long_paths(*[int(x) for x in args.long.split(",")])
     if args.persistent >= 0:
         r.set_persistent(bool(args.persistent))
     rows = len(r.rows)

@@ -332,6 +332,7 @@ public:
     /* headless additions */
     std::vector<F32> readAccumulator();           /* width*height*4 floats */
     std::vector<U32> finalizeRGBA8();             /* width*height RGBA8 words */
+    std::vector<U32> displayRGBA8();              /* finalize image through fs_quad.frag's sqrt gamma */
     surf_ctx* handle() const { return m_ctx; }
 private:
     surf_ctx* m_ctx = nullptr;

@@ -175,6 +175,10 @@ int surf_set_zero_cutoff(surf_ctx* ctx, int enabled);
  * that runs every path to its end, the default).  Results do not depend on the
  * policy.  Drains the context first. */
 int surf_set_tail_policy(surf_ctx* ctx, uint32_t threshold_paths, uint32_t lanes_per_wave, uint32_t stage_segments);
+/* Single-stage drain: run it as the cooperative tail (one path per 64-lane
+ * wave, instances in parallel lanes) when at most max_paths paths remain
+ * (0 = never).  Identical results. */
+int surf_set_tail_coop(surf_ctx* ctx, uint32_t max_paths);
 /* Long paths: a path whose next segment would be its `escape_segments`-th
  * leaves the wavefront (one segment per iteration) for a worker kernel that
  * runs concurrently on a second stream and advances it up to `budget`
@@ -220,6 +224,9 @@ int surf_read_accumulator(surf_ctx* ctx, float* rgba_rows);
 int surf_copy_accumulator_device(surf_ctx* ctx, void* dst_device);
 /* RGBA8 of acc / total samples with RgbaToU32 rounding, rows*width words. */
 int surf_finalize_rgba8(surf_ctx* ctx, uint32_t* out_rgba8);
+/* The displayed image: fs_quad.frag:22-24 (sqrt gamma) applied to the RGBA8
+ * finalize image, written as 8-bit UNORM (round to nearest even), rows*width words. */
+int surf_display_rgba8(surf_ctx* ctx, uint32_t* out_rgba8);
 int surf_get_stats(surf_ctx* ctx, surf_stats* out);
 int surf_synchronize(surf_ctx* ctx);
 
@@ -254,6 +261,13 @@ int surf_scene_camera(const surf_scene* scene, uint32_t width, uint32_t height, 
 /* Deepest root-to-leaf edge counts of the TLAS and of all BLASes. */
 int surf_scene_bvh_depths(const surf_scene* scene, uint32_t* tlas_depth, uint32_t* max_blas_depth);
 void surf_scene_destroy(surf_scene* scene);
+
+/* Image files for an RGBA8 image (R in the low byte, as surf_finalize_rgba8 /
+ * surf_display_rgba8 write it), rows top to bottom: binary PPM (P6, alpha
+ * dropped) or PNG (8-bit RGBA, zlib).  The reference only presents to a
+ * swapchain; these are its on-disk equivalent. */
+int surf_write_ppm(const char* path, uint32_t width, uint32_t height, const uint32_t* rgba8);
+int surf_write_png(const char* path, uint32_t width, uint32_t height, const uint32_t* rgba8);
 
 /* Mesh::Mesh(path) (sources/mesh.cpp:69-154, tinyobjloader triangulate=true):
  * .obj or .obj.gz parsed in parallel chunks (threads = 0: default count).  The

@@ -586,8 +586,11 @@ template <bool LDS>
 __global__ __launch_bounds__(kBlock, SURF_TRACE_WAVES) void k_extend(DevScene S, Pool cur, float4* __restrict__ hitTUV,
                                                    uint32_t* __restrict__ hitInst, const Counters* C, int par, uint32_t stackWords) {
     extern __shared__ uint32_t lds[];
-    const TraceTables Tt = traceTables<LDS>(S, lds, stackWords);
     const uint32_t n = C->nIn[par];
+    /* blocks past the pool exit before staging: a small pool (the drain) costs
+     * what it traces, not the fixed grid's LDS staging */
+    if (blockIdx.x * blockDim.x >= n) return;
+    const TraceTables Tt = traceTables<LDS>(S, lds, stackWords);
     const uint32_t stride = blockDim.x;
     uint32_t* stk = lds + threadIdx.x;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
@@ -979,6 +982,7 @@ __global__ __launch_bounds__(kBlock, SURF_SHADE_WAVES) void k_shade(DevScene S, 
                                                   const uint32_t* __restrict__ hitInst, ShadowQ Q,
                                                   float4* __restrict__ rad, uint32_t* __restrict__ frameDone,
                                                   uint32_t npx, uint32_t window, Counters* C, int par, LongQueues LQ) {
+    if (blockIdx.x * blockDim.x >= C->nIn[par]) return;     /* nothing to shade in this block */
     __shared__ DevInstance sInst[LDS_TABLES ? kLdsInst : 1];
     __shared__ DevMaterial sMat[LDS_TABLES ? kLdsMats : 1];
     __shared__ uint2 sLights[LDS_TABLES ? kLdsLights : 1];
@@ -1053,8 +1057,9 @@ template <bool LDS>
 __global__ __launch_bounds__(kBlock, SURF_TRACE_WAVES) void k_connect(DevScene S, ShadowQ Q, float4* __restrict__ rad, Counters* C, int par,
                                                     uint32_t stackWords) {
     extern __shared__ uint32_t lds[];
-    const TraceTables Tt = traceTables<LDS>(S, lds, stackWords);
     const uint32_t n = (uint32_t)(C->app[par] >> 32);
+    if (blockIdx.x * blockDim.x >= n) return;               /* no shadow rays for this block */
+    const TraceTables Tt = traceTables<LDS>(S, lds, stackWords);
     const uint32_t stride = blockDim.x;
     uint32_t* stk = lds + threadIdx.x;
     unsigned long long cUn = 0;
@@ -1357,6 +1362,33 @@ __global__ __launch_bounds__(kBlock) void k_finalize(const float4* __restrict__ 
     const float4 a = acc[p];
     out[p] = packChannel((a.x * inv) * 255.0f) | (packChannel((a.y * inv) * 255.0f) << 8) |
              (packChannel((a.z * inv) * 255.0f) << 16) | (packChannel((a.w * inv) * 255.0f) << 24);
+}
+
+/* Display step (row f2): fs_quad.frag:22-24 samples the RGBA8 finalize image
+ * (UNORM: c/255) and writes sqrt(c/255) to an 8-bit UNORM target; the target's
+ * float->UNORM8 conversion is taken as round-to-nearest-even with saturation
+ * (packChannel).  Fused with k_finalize's packing. */
+__device__ __forceinline__ uint32_t displayChannel(uint32_t c8) {
+    return packChannel(sqrtf((float)c8 / 255.0f) * 255.0f);
+}
+__global__ __launch_bounds__(kBlock) void k_display(const float4* __restrict__ acc, uint32_t* __restrict__ out,
+                                                    uint32_t npx, float inv) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= npx) return;
+    const float4 a = acc[p];
+    out[p] = displayChannel(packChannel((a.x * inv) * 255.0f)) | (displayChannel(packChannel((a.y * inv) * 255.0f)) << 8) |
+             (displayChannel(packChannel((a.z * inv) * 255.0f)) << 16) | (displayChannel(packChannel((a.w * inv) * 255.0f)) << 24);
+}
+
+/* Per-pixel term of the Lumen energy (renderer.cpp:191-201): (r/N + g/N) + b/N.
+ * The sum over pixels is the reference's serial float sum, done on the host
+ * in pixel order from these terms (a parallel float sum would round differently). */
+__global__ __launch_bounds__(kBlock) void k_energy_terms(const float4* __restrict__ acc, float* __restrict__ out,
+                                                         uint32_t npx, float inv) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= npx) return;
+    const float4 a = acc[p];
+    out[p] = ((a.x * inv) + (a.y * inv)) + (a.z * inv);
 }
 
 /* Traversal entry points for kernel-level parity tests. */

@@ -69,4 +69,10 @@ std::vector<U32> WaveFrontRenderer::finalizeRGBA8() {
     return out;
 }
 
+std::vector<U32> WaveFrontRenderer::displayRGBA8() {
+    std::vector<U32> out((size_t)m_resolution.width * m_resolution.height);
+    check(surf_display_rgba8(m_ctx, out.data()), m_ctx, "surf_display_rgba8");
+    return out;
+}
+
 }  // namespace surf

@@ -1175,6 +1175,70 @@ int surf_scene_bvh_depths(const surf_scene* scene, uint32_t* tlas_depth, uint32_
 
 void surf_scene_destroy(surf_scene* scene) { delete scene; }
 
+int surf_write_ppm(const char* path, uint32_t width, uint32_t height, const uint32_t* rgba8) {
+    if (!path || !rgba8 || width == 0 || height == 0) return SURF_ERR_INVALID;
+    FILE* f = fopen(path, "wb");
+    if (!f) return SURF_ERR_IO;
+    fprintf(f, "P6\n%u %u\n255\n", width, height);
+    std::vector<unsigned char> row((size_t)width * 3);
+    bool ok = true;
+    for (uint32_t y = 0; y < height && ok; ++y) {
+        for (uint32_t x = 0; x < width; ++x) {
+            const uint32_t p = rgba8[(size_t)y * width + x];
+            row[3 * x] = (unsigned char)(p & 0xffu);
+            row[3 * x + 1] = (unsigned char)((p >> 8) & 0xffu);
+            row[3 * x + 2] = (unsigned char)((p >> 16) & 0xffu);
+        }
+        ok = fwrite(row.data(), 1, row.size(), f) == row.size();
+    }
+    return (fclose(f) == 0 && ok) ? SURF_OK : SURF_ERR_IO;
+}
+
+int surf_write_png(const char* path, uint32_t width, uint32_t height, const uint32_t* rgba8) {
+    if (!path || !rgba8 || width == 0 || height == 0) return SURF_ERR_INVALID;
+    /* scanlines: filter byte 0 + RGBA bytes (R from the low byte) */
+    const size_t stride = (size_t)width * 4 + 1;
+    std::vector<unsigned char> raw(stride * height);
+    for (uint32_t y = 0; y < height; ++y) {
+        unsigned char* r = &raw[stride * y];
+        r[0] = 0;
+        for (uint32_t x = 0; x < width; ++x) {
+            const uint32_t p = rgba8[(size_t)y * width + x];
+            r[1 + 4 * x] = (unsigned char)(p & 0xffu);
+            r[2 + 4 * x] = (unsigned char)((p >> 8) & 0xffu);
+            r[3 + 4 * x] = (unsigned char)((p >> 16) & 0xffu);
+            r[4 + 4 * x] = (unsigned char)(p >> 24);
+        }
+    }
+    uLongf zlen = compressBound((uLong)raw.size());
+    std::vector<unsigned char> z(zlen);
+    if (compress2(z.data(), &zlen, raw.data(), (uLong)raw.size(), 6) != Z_OK) return SURF_ERR_IO;
+    FILE* f = fopen(path, "wb");
+    if (!f) return SURF_ERR_IO;
+    bool ok = true;
+    auto put = [&](const void* p, size_t n) { ok = ok && fwrite(p, 1, n, f) == n; };
+    auto be32 = [](uint32_t v, unsigned char* b) { b[0] = (unsigned char)(v >> 24); b[1] = (unsigned char)(v >> 16); b[2] = (unsigned char)(v >> 8); b[3] = (unsigned char)v; };
+    auto chunk = [&](const char* type, const unsigned char* data, size_t n) {
+        unsigned char b[4];
+        be32((uint32_t)n, b); put(b, 4);
+        put(type, 4);
+        if (n) put(data, n);
+        uLong crc = crc32(0L, Z_NULL, 0);
+        crc = crc32(crc, reinterpret_cast<const Bytef*>(type), 4);
+        if (n) crc = crc32(crc, data, (uInt)n);
+        be32((uint32_t)crc, b); put(b, 4);
+    };
+    static const unsigned char sig[8] = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1a, '\n'};
+    put(sig, 8);
+    unsigned char ihdr[13];
+    be32(width, ihdr); be32(height, ihdr + 4);
+    ihdr[8] = 8; ihdr[9] = 6; ihdr[10] = 0; ihdr[11] = 0; ihdr[12] = 0;    /* 8-bit RGBA, deflate, no interlace */
+    chunk("IHDR", ihdr, 13);
+    chunk("IDAT", z.data(), zlen);
+    chunk("IEND", nullptr, 0);
+    return (fclose(f) == 0 && ok) ? SURF_OK : SURF_ERR_IO;
+}
+
 struct surf_mesh { surf::Mesh mesh; };
 
 int surf_obj_load(const char* path, uint32_t threads, surf_mesh** out) {

@@ -103,6 +103,8 @@ struct surf_ctx {
     Pool surv[2]{};                /* drain survivors, ping-pong between stages */
     uint32_t survCap = 0;
     uint32_t coopMax = 0;          /* survivors handled by the cooperative tail (one path per wave) */
+    uint32_t coopAll = 0;
+    int drainReplays = 1;          /* graph replays per host poll while draining (SURF_DRAIN_REPLAYS) */          /* single-stage drain: cooperative tail when <= this many paths (surf_set_tail_coop) */
     bool coopEligible = false;     /* single-leaf TLAS of <= 64 instances, LDS tables */
     int traceMode = 0;             /* surf_trace_closest/_any: 0 one ray per lane, 1 one ray per wave */
     bool persistent = false;       /* out-of-step lanes with per-wave ray ranges: measured 4x slower */
@@ -292,7 +294,8 @@ int allocWavefront(surf_ctx* c) {
     if (hipGetDeviceProperties(&prop, c->device) == hipSuccess && prop.multiProcessorCount > 0) cus = prop.multiProcessorCount;
     const uint64_t maxBlocks = (cap + kBlock - 1) / kBlock;
     c->gridWork = (uint32_t)std::min<uint64_t>(maxBlocks, (uint64_t)cus * 8);
-    c->coopMax = (uint32_t)cus * 12;    /* 3 waves per SIMD of the tail kernels (launch bounds) */
+    c->coopMax = (uint32_t)cus * 12;
+    if (const char* e = std::getenv("SURF_DRAIN_REPLAYS")) c->drainReplays = std::max(1, std::atoi(e));    /* 3 waves per SIMD of the tail kernels (launch bounds) */
     c->longGrid = (uint32_t)cus;        /* one k_long wave per CU: the wavefront keeps the rest */
     c->gridRegen = (uint32_t)std::min<uint64_t>(maxBlocks, (uint64_t)cus * 8);
     c->allocated = true;
@@ -545,7 +548,7 @@ int runTail(surf_ctx* c) {
             const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
             std::fprintf(stderr, "[surf tail] stage %d: %u paths at %.2f ms\n", stage, cnt, ms);
         }
-        if (c->coopEligible && c->tailBudget && cnt <= c->coopMax) {
+        if (c->coopEligible && ((c->tailBudget && cnt <= c->coopMax) || (!c->tailBudget && cnt <= c->coopAll))) {
             const size_t lds = traversalLds(c, 64) + (size_t)stackWords(c, 64) * sizeof(float);
             hipLaunchKernelGGL(k_tail_coop<true>, dim3(cnt), dim3(64), lds, c->stream, c->S, in, cnt, c->rad, c->frameDone,
                                c->npx, c->window, c->ctr, stackWords(c, 64), firstCounted);
@@ -598,12 +601,22 @@ int pump(surf_ctx* c, bool drain) {
         if (drain && c->accFrames >= c->targetFrames) return SURF_OK;
         const bool starved = issued >= c->pushedLimit;     /* nothing more may be issued right now */
         const uint64_t accBefore = c->accFrames;
+        static const bool dbgDrain = std::getenv("SURF_DEBUG_DRAIN") != nullptr;   /* diagnostics: drain timeline */
+        if (dbgDrain && starved) {
+            static auto tS = std::chrono::steady_clock::now();
+            std::fprintf(stderr, "[surf drain] replay %llu: %u in flight at %.3f ms\n", (unsigned long long)c->replay, inflight,
+                         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tS).count());
+        }
         if (starved && inflight > 0 && inflight <= tailThreshold(c)) {
             if ((rc = runTail(c))) return rc;
         } else if (starved && inflight == 0) {
             /* every issued sample finished: accumulating re-opens the window */
-        } else if ((rc = advance(c))) {
-            return rc;
+        } else {
+            /* draining (nothing left to issue): several replays per host poll --
+             * the per-replay poll, not the kernels, is what a small pool pays */
+            const int reps = starved ? c->drainReplays : 1;
+            for (int k = 0; k < reps; ++k)
+                if ((rc = advance(c))) return rc;
         }
         if ((rc = syncAndAccumulate(c))) return rc;
         if (starved && inflight == 0 && c->accFrames == accBefore)
@@ -796,6 +809,15 @@ int surf_set_tail_policy(surf_ctx* c, uint32_t threshold_paths, uint32_t lanes_p
     c->tailPaths = threshold_paths;
     c->tailLanes = lanes_per_wave;
     c->tailBudget = stage_segments;
+    return SURF_OK;
+}
+
+int surf_set_tail_coop(surf_ctx* c, uint32_t max_paths) {
+    if (!c) return fail(nullptr, SURF_ERR_INVALID, "ctx is NULL");
+    SURF_CHECK(c, hipSetDevice(c->device));
+    const int rc = endStream(c);
+    if (rc) return rc;
+    c->coopAll = max_paths;
     return SURF_OK;
 }
 
@@ -1165,6 +1187,22 @@ int surf_finalize_rgba8(surf_ctx* c, uint32_t* out) {
     return SURF_OK;
 }
 
+int surf_display_rgba8(surf_ctx* c, uint32_t* out) {
+    if (!c || !out) return SURF_ERR_INVALID;
+    if (c->totalSamples == 0) return fail(c, SURF_ERR_INVALID, "nothing rendered since the last clear");
+    SURF_CHECK(c, hipSetDevice(c->device));
+    int rc = allocWavefront(c);
+    if (rc) return rc;
+    if ((rc = ensureDrained(c))) return rc;
+    const float inv = 1.0f / (float)c->totalSamples;
+    hipLaunchKernelGGL(k_display, dim3((c->npx + kBlock - 1) / kBlock), dim3(kBlock), 0, c->stream, (const float4*)c->acc,
+                       c->dOutRGBA, c->npx, inv);
+    SURF_CHECK(c, hipGetLastError());
+    SURF_CHECK(c, hipMemcpyAsync(out, c->dOutRGBA, (size_t)c->npx * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+    SURF_CHECK(c, hipStreamSynchronize(c->stream));
+    return SURF_OK;
+}
+
 int surf_get_stats(surf_ctx* c, surf_stats* out) {
     if (!c || !out) return SURF_ERR_INVALID;
     int rc = ensureDrained(c);
@@ -1180,12 +1218,19 @@ int surf_get_stats(surf_ctx* c, surf_stats* out) {
     s.stack_depth = c->stackDepth;
     s.pool_capacity = c->capacity;
     if (c->totalSamples) {
-        /* Lumen energy, renderer.cpp:191-201 (serial sum of r+g+b of acc/N) */
-        std::vector<float> acc((size_t)c->npx * 4);
-        if ((rc = surf_read_accumulator(c, acc.data()))) return rc;
+        /* Lumen energy, renderer.cpp:191-201: per-pixel terms on the GPU
+         * (k_energy_terms), then the reference's serial sum in pixel order */
+        if ((rc = allocWavefront(c))) return rc;
         const float inv = 1.0f / (float)c->totalSamples;
+        float* terms = reinterpret_cast<float*>(c->dOutRGBA);          /* npx words, reused */
+        hipLaunchKernelGGL(k_energy_terms, dim3((c->npx + kBlock - 1) / kBlock), dim3(kBlock), 0, c->stream,
+                           (const float4*)c->acc, terms, c->npx, inv);
+        SURF_CHECK(c, hipGetLastError());
+        std::vector<float> h(c->npx);
+        SURF_CHECK(c, hipMemcpyAsync(h.data(), terms, (size_t)c->npx * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+        SURF_CHECK(c, hipStreamSynchronize(c->stream));
         float e = 0.0f;
-        for (size_t p = 0; p < c->npx; ++p) e = e + (((acc[4 * p] * inv) + (acc[4 * p + 1] * inv)) + (acc[4 * p + 2] * inv));
+        for (size_t p = 0; p < c->npx; ++p) e = e + h[p];
         s.energy = e;
     }
     *out = s;

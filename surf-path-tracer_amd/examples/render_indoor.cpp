@@ -6,10 +6,11 @@
  * application builds them, with RenderContext holding a HIP device instead of
  * a Vulkan context and no UIManager.
  *
- * usage: render_indoor ASSETS_DIR WIDTH HEIGHT FRAMES OUT.ppm
+ * usage: render_indoor ASSETS_DIR WIDTH HEIGHT FRAMES OUT.(ppm|png)
  * Prints the reference's per-frame line (ms, Mrays/s, samples, Lumen) and
- * writes the image as the reference presents it: acc / samples, then sqrt
- * (fs_quad.frag:12-13, gamma 2), 8 bits per channel.
+ * writes the image as the reference presents it: the RGBA8 finalize image
+ * (wavefront_finalize.comp) through fs_quad.frag's sqrt gamma, 8 bits per
+ * channel (displayRGBA8), as PPM or PNG by extension.
  */
 #include "surf/surf_host.hpp"
 
@@ -25,7 +26,7 @@ using namespace surf;
 
 int main(int argc, char** argv) {
     if (argc < 6) {
-        std::fprintf(stderr, "usage: %s ASSETS_DIR WIDTH HEIGHT FRAMES OUT.ppm\n", argv[0]);
+        std::fprintf(stderr, "usage: %s ASSETS_DIR WIDTH HEIGHT FRAMES OUT.(ppm|png)\n", argv[0]);
         return 2;
     }
     const std::string dir = argv[1];
@@ -82,20 +83,11 @@ int main(int argc, char** argv) {
                         renderer.config().samplesPerFrame, info.energy);
         }
 
-        const std::vector<F32> acc = renderer.readAccumulator();
-        FILE* out = std::fopen(argv[5], "wb");
-        if (!out) { std::perror(argv[5]); return 1; }
-        std::fprintf(out, "P6\n%u %u\n255\n", W, H);
-        std::vector<unsigned char> row((size_t)W * 3);
-        for (U32 y = 0; y < H; ++y) {
-            for (U32 x = 0; x < W; ++x)
-                for (int c = 0; c < 3; ++c) {
-                    const float v = std::sqrt(acc[4 * ((size_t)y * W + x) + c] / (float)frames);
-                    row[3 * (size_t)x + c] = (unsigned char)(v >= 1.0f ? 255 : (v <= 0.0f ? 0 : (int)(v * 255.0f + 0.5f)));
-                }
-            std::fwrite(row.data(), 1, row.size(), out);
-        }
-        std::fclose(out);
+        const std::vector<U32> img = renderer.displayRGBA8();
+        const std::string path = argv[5];
+        const bool png = path.size() > 4 && path.compare(path.size() - 4, 4, ".png") == 0;
+        const int rc = png ? surf_write_png(path.c_str(), W, H, img.data()) : surf_write_ppm(path.c_str(), W, H, img.data());
+        if (rc != SURF_OK) { std::fprintf(stderr, "cannot write %s\n", path.c_str()); return 1; }
     } catch (const std::exception& e) {
         std::fprintf(stderr, "render_indoor: %s\n", e.what());
         return 1;

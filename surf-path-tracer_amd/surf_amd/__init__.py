@@ -96,7 +96,7 @@ def load() -> C.CDLL:
         "surf_destroy": ([P], None), "surf_last_error": ([P], C.c_char_p),
         "surf_shard_rows": ([P, P, C.POINTER(U32)], I32),
         "surf_set_pool_capacity": ([P, U32], I32), "surf_set_frame_batch": ([P, U32], I32),
-        "surf_set_profiling": ([P, I32], I32), "surf_set_zero_cutoff": ([P, I32], I32), "surf_set_trace_mode": ([P, I32], I32), "surf_set_persistent": ([P, I32], I32), "surf_set_long_paths": ([P, U32, U32], I32), "surf_set_tail_policy": ([P, U32, U32, U32], I32),
+        "surf_set_profiling": ([P, I32], I32), "surf_set_zero_cutoff": ([P, I32], I32), "surf_set_trace_mode": ([P, I32], I32), "surf_set_persistent": ([P, I32], I32), "surf_set_long_paths": ([P, U32, U32], I32), "surf_set_tail_policy": ([P, U32, U32, U32], I32), "surf_set_tail_coop": ([P, U32], I32),
         "surf_debug_capped": ([P, P, U32, C.POINTER(C.c_uint64)], I32),
         "surf_upload_scene": ([P, C.POINTER(SceneDesc)], I32),
         "surf_set_camera": ([P, P], I32),
@@ -115,6 +115,8 @@ def load() -> C.CDLL:
         "surf_scene_destroy": ([P], None),
         "surf_bvh_build": ([P, U32, U32, P, P, C.POINTER(U32)], I32),
         "surf_obj_load": ([C.c_char_p, U32, C.POINTER(P)], I32),
+        "surf_write_ppm": ([C.c_char_p, U32, U32, P], I32), "surf_write_png": ([C.c_char_p, U32, U32, P], I32),
+        "surf_display_rgba8": ([P, P], I32),
         "surf_mesh_data": ([P, C.POINTER(P), C.POINTER(P), C.POINTER(U32)], I32),
         "surf_mesh_destroy": ([P], None),
         "surf_ref_sinf": ([F], F), "surf_ref_cosf": ([F], F), "surf_ref_expf": ([F], F),
@@ -201,6 +203,15 @@ class Scene:
             self.close()
         except Exception:
             pass
+
+
+def write_image(path: str, rgba8: np.ndarray) -> None:
+    """Writes an (H, W) uint32 RGBA8 image (R in the low byte) as PNG or, for a
+    .ppm path, binary PPM (alpha dropped)."""
+    img = np.ascontiguousarray(rgba8, dtype=np.uint32)
+    h, w = img.shape
+    fn = load().surf_write_ppm if path.lower().endswith(".ppm") else load().surf_write_png
+    _check(fn(path.encode(), w, h, _ptr(img)), "surf_write_image")
 
 
 def obj_load(path: str, threads: int = 0) -> tuple[np.ndarray, np.ndarray]:
@@ -312,6 +323,10 @@ class Renderer:
         _check(load().surf_set_tail_policy(self._h, threshold_paths, lanes_per_wave, stage_segments), "surf_set_tail_policy",
                self._h)
 
+    def set_tail_coop(self, max_paths: int):
+        """Single-stage drain as the cooperative tail when <= max_paths paths remain (0 = never)."""
+        _check(load().surf_set_tail_coop(self._h, max_paths), "surf_set_tail_coop", self._h)
+
     def set_long_paths(self, escape_segments: int = 64, budget: int = 64):
         """Paths reaching escape_segments move to the concurrent long-path worker (0 = off)."""
         _check(load().surf_set_long_paths(self._h, escape_segments, budget), "surf_set_long_paths", self._h)
@@ -347,6 +362,12 @@ class Renderer:
     def finalize_rgba8(self) -> np.ndarray:
         out = np.zeros((len(self.rows), self.width), dtype=np.uint32)
         _check(load().surf_finalize_rgba8(self._h, _ptr(out)), "surf_finalize_rgba8", self._h)
+        return out
+
+    def display_rgba8(self) -> np.ndarray:
+        """The displayed image: fs_quad.frag's sqrt gamma on the RGBA8 finalize image."""
+        out = np.zeros((len(self.rows), self.width), dtype=np.uint32)
+        _check(load().surf_display_rgba8(self._h, _ptr(out)), "surf_display_rgba8", self._h)
         return out
 
     def stats(self) -> dict:

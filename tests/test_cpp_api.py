@@ -1,22 +1,28 @@
 """The drop-in C++ API end to end: examples/render_indoor.cpp builds the scene,
 BVHs, camera and WaveFrontRenderer exactly as the reference's main.cpp does
-(sources/main.cpp:141-442) and writes the presented image (sqrt gamma,
-fs_quad.frag:12-13).  Its pixels must equal the same presentation of the CPU
-oracle's accumulator, bit for bit."""
+(sources/main.cpp:141-442) and writes the presented image (the RGBA8 finalize
+image through fs_quad.frag's sqrt gamma).  Its pixels must equal the same
+presentation of the CPU oracle's accumulator, bit for bit."""
 import os
 import subprocess
 
 import numpy as np
 import pytest
 
+import oracle
+
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EXE = os.path.join(REPO, "surf-path-tracer_amd", "build", "render_indoor")
 
 
 def present(acc, frames):
-    v = np.sqrt(acc[..., :3] / np.float32(frames)).astype(np.float32)
-    q = np.where(v >= 1.0, 255, np.where(v <= 0.0, 0, (v * np.float32(255.0) + np.float32(0.5)).astype(np.int32)))
-    return q.astype(np.uint8)
+    """wavefront_finalize.comp + RgbaToU32 (oracle), then fs_quad.frag: sqrt of
+    the UNORM8 value, back to UNORM8 (round to nearest even)."""
+    h, w = acc.shape[:2]
+    rgba = oracle.finalize_rgba8(acc, np.float32(1.0) / np.float32(frames))
+    ch = np.stack([(rgba >> (8 * k)) & 0xFF for k in range(3)], 1).astype(np.float32)
+    g = np.rint(np.sqrt(ch / np.float32(255.0)) * np.float32(255.0)).clip(0, 255)
+    return g.astype(np.uint8).reshape(h, w, 3)
 
 
 def read_ppm(path):

@@ -193,7 +193,12 @@ def test_finalize_rgba8_matches_oracle(product_scene):
     e = np.float32(0.0)
     for p in acc.reshape(-1, 4) * (np.float32(1.0) / np.float32(F)):
         e = np.float32(e + np.float32(np.float32(p[0] + p[1]) + p[2]))
-    assert st["energy"] == pytest.approx(float(e), rel=1e-6)
+    assert np.float32(st["energy"]) == e, "Lumen energy: serial pixel-order sum (renderer.cpp:191-201)"
+    # display step (fs_quad.frag:22-24): sqrt of the UNORM8 finalize image, back to UNORM8
+    disp = r.display_rgba8().reshape(-1)
+    ch = np.stack([(want >> (8 * k)) & 0xFF for k in range(4)], 1).astype(np.float32)
+    g = np.rint(np.sqrt(ch / np.float32(255.0)) * np.float32(255.0)).clip(0, 255).astype(np.uint32)
+    assert np.array_equal(disp, g[:, 0] | (g[:, 1] << 8) | (g[:, 2] << 16) | (g[:, 3] << 24))
 
 
 def test_cutoff_off_matches_reference_counts(oracle_scene, product_scene):

@@ -6,10 +6,11 @@ import sys
 sys.path.insert(0, "/root/repo"); sys.path.insert(0, "/root/repo/surf-path-tracer_amd")
 import numpy as np
 
+VARIANT = 0 if "--indoor" in sys.argv else 1
 if "--make" in sys.argv:
     import oracle
-    s = oracle.OracleScene(variant=1)
-    (eo, ed), _ = s.record_rays(1280, 720, 0, 0, 1280 * 720 // 8, max_ext=1_500_000, max_shadow=10)
+    s = oracle.OracleScene(variant=VARIANT)
+    (eo, ed), _ = s.record_rays(1280, 720, 0, 0, 1280 * 720 // (8 if VARIANT else 2), max_ext=1_500_000, max_shadow=10)
     n, t = s.trace_visits(eo, ed)
     cost = n.sum(1).astype(np.int64)
     np.savez("/root/repo/gpurun_in_c5.npz", o=eo, d=ed, cost=cost)
@@ -24,8 +25,9 @@ order = np.argsort(cost)
 n = len(o)
 sets = {"all": np.arange(n), "drop1%": np.sort(order[: int(n * 0.99)]), "drop0.1%": np.sort(order[: int(n * 0.999)]),
         "top1%": np.sort(order[int(n * 0.99):]), "half": np.arange(n // 2), "quarter": np.arange(n // 4),
-        "sixteenth": np.arange(n // 16), "by-cost": order, "shuffled": np.random.default_rng(1).permutation(n)}
-s = surf_amd.Scene.indoor(variant=1)
+        "sixteenth": np.arange(n // 16), "by-cost": order, "shuffled": np.random.default_rng(1).permutation(n),
+        "by-dir-octant+origin": np.lexsort((np.round(o[:, 0] * 2), np.round(o[:, 1] * 2), np.round(o[:, 2] * 2), (d > 0) @ np.array([1, 2, 4])))}
+s = surf_amd.Scene.indoor(variant=VARIANT)
 r = surf_amd.Renderer(s, 64, 64)
 import time
 for k in range(2):
