@@ -128,6 +128,7 @@ typedef struct {
     float    energy;           /* sum of acc.rgb / samples over the shard ("Lumen", renderer.cpp:191-201) */
     uint32_t max_segments;     /* longest path seen (extension rays), diagnostics */
     uint64_t tail_survivors;   /* drain paths still alive after the tail's first stage */
+    uint64_t long_paths;       /* paths finished by the long-path worker (surf_set_long_paths) */
 } surf_stats;
 
 typedef struct surf_ctx surf_ctx;       /* one per HIP device */
@@ -170,21 +171,25 @@ int surf_set_zero_cutoff(surf_ctx* ctx, int enabled);
 /* Drain policy: when no new sample may be issued and at most `threshold_paths`
  * paths are in flight, the tail kernel finishes them in stages: each stage
  * runs `lanes_per_wave` paths per 64-lane wave for up to `stage_segments`
- * segments; once few paths remain, the cooperative tail runs each on a whole
- * wave (0 = automatic for the first two; stage_segments 0 = a single stage
- * that runs every path to its end, the default).  Results do not depend on the
- * policy.  Drains the context first. */
+ * segments and hands the survivors to the next; once at most the
+ * surf_set_tail_coop limit remain, the cooperative tail runs each on a whole
+ * wave (0 = automatic for the first two; stage_segments 0 = a single lane
+ * stage to the end; default 16).  Results do not depend on the policy.
+ * Drains the context first. */
 int surf_set_tail_policy(surf_ctx* ctx, uint32_t threshold_paths, uint32_t lanes_per_wave, uint32_t stage_segments);
-/* Single-stage drain: run it as the cooperative tail (one path per 64-lane
- * wave, instances in parallel lanes) when at most max_paths paths remain
- * (0 = never).  Identical results. */
+/* Drain paths handed to the cooperative tail (one path per 64-lane wave, the
+ * lanes-as-planes traversal; default 20000, 0 = never).  Identical results. */
 int surf_set_tail_coop(surf_ctx* ctx, uint32_t max_paths);
 /* Long paths: a path whose next segment would be its `escape_segments`-th
- * leaves the wavefront (one segment per iteration) for a worker kernel that
- * runs concurrently on a second stream and advances it up to `budget`
- * segments per graph replay (default off; escape_segments 0 = off).
- * Results do not depend on it.  Drains the context first. */
-int surf_set_long_paths(surf_ctx* ctx, uint32_t escape_segments, uint32_t budget);
+ * leaves the wavefront (which advances a path one segment per iteration, i.e.
+ * per ~4 kernel launches over the whole pool) through a device ring for a
+ * worker kernel that runs concurrently on a second stream and advances each
+ * of its paths one segment per loop iteration.  Worker launches are queued
+ * back to back, each living `lifetime_us` (0 = 10 ms) and handing unfinished
+ * paths to the next; the escaping bounce's shadow ray travels with the path,
+ * so radiance is added in the reference's order.  Results do not depend on it
+ * (escape_segments 0 = off).  Drains the context first. */
+int surf_set_long_paths(surf_ctx* ctx, uint32_t escape_segments, uint32_t lifetime_us);
 /* Diagnostics: how many paths the segment cap ended in the current sample
  * stream, and the sample ids (frame slot * shard pixels + pixel) of the first
  * min(count, 64, max). */

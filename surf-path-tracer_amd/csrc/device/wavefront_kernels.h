@@ -40,6 +40,9 @@ constexpr int kBlock = 256;
 #ifndef SURF_SHADE_WAVES
 #define SURF_SHADE_WAVES 3
 #endif
+#ifndef SURF_SEG_TIMING
+#define SURF_SEG_TIMING 0
+#endif
 #ifndef SURF_TRACE_WAVES
 #define SURF_TRACE_WAVES 1
 #endif
@@ -96,11 +99,24 @@ struct DevCamera {
 };
 
 struct Pool { float4* o; float4* d; float4* T; };
-/* Long paths (the reference's Russian roulette keeps some alive for thousands
- * of segments): k_shade moves a path that reaches Counters::longThresh
- * segments to an escape queue; k_long, running concurrently with the
- * wavefront on a second stream, advances them many segments per graph replay. */
-struct LongQueues { Pool esc[3]; Pool lp[2]; };
+/* Long paths (the reference's Russian roulette keeps ~0.04% of paths alive for
+ * hundreds to thousands of segments): the wavefront advances a path one
+ * segment per phase, so a path reaching Counters::longThresh segments leaves
+ * it through this ring for k_long, a worker running concurrently on a second
+ * stream that advances each of its paths one segment per iteration.  Entry i
+ * lives in slot i & (cap - 1): the path record plus the shadow ray of the
+ * escaping bounce, which the worker resolves first (radiance order).
+ * Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility): the producer
+ * writes the record with agent-scope (sc1) stores, waits for them, then
+ * publishes seq[slot] = i + 1 with an agent atomic store; the consumer polls
+ * seq with an agent load, then an agent acquire, then reads the record. */
+struct LongRing {
+    float4 *o, *d, *T;        /* path (Pool layout) */
+    float4 *so, *sd, *sc;     /* pending shadow ray (ShadowQ layout); sc.w = 1 when present */
+    uint32_t* seq;
+    Pool park;                /* one slot per worker lane: path held when a worker's lifetime ends */
+    uint32_t* parkFlag;
+};
 /* Where a path that used up its segment budget goes. */
 struct Sink { Pool q; uint32_t* n; uint32_t cap; };
 struct ShadowQ { float4* o; float4* d; float4* c; };
@@ -117,23 +133,27 @@ struct Counters {
     uint32_t survN;                  /* k_tail survivors appended (may exceed survCap) */
     uint32_t survCap;
     uint32_t longThresh;             /* a continuation with this many segments escapes the wavefront (0 = off) */
-    uint32_t eSel;                   /* escape queue k_shade appends to (host rotates it per graph replay) */
-    uint32_t eN[3];                  /* escapes appended to queue q (may exceed eCap) */
-    uint32_t eCap;
-    uint32_t lpN[2];                 /* long-path pool sizes (k_long output, may exceed lpCap) */
-    uint32_t lpCap;
-    uint32_t _pad2;
+    uint32_t ringCap;                /* long-path ring slots (power of two) */
+    /* ring words each on a 128-B line of their own: the workers poll them, and
+     * must not share a line with the wavefront's per-block atomics above */
+    alignas(128) uint32_t ringTail;  /* entries reserved by k_shade (agent atomics, mod 2^32) */
+    alignas(128) uint32_t ringHead;  /* entries claimed by k_long */
+    alignas(128) uint32_t closing;   /* set by k_close: the wavefront will escape no more paths */
+    uint32_t parkedN;                /* worker lanes holding a parked path */
+    alignas(128) uint32_t _pad2;
     unsigned long long issued[2];    /* stream samples issued, per parity */
     unsigned long long limit;        /* host-written issue limit (frame window) */
     unsigned long long baseFrame;    /* absolute frame index of stream frame 0 */
-    unsigned long long ev[8];        /* ext, hit, cont, shadow, acc, unocc, tail paths, capped paths */
+    unsigned long long ev[16];       /* ext, hit, cont, shadow, acc, unocc, tail paths, capped paths, long paths */
     uint32_t capped[64];             /* sample ids of the first paths ended by the segment cap (diagnostics) */
     /* event counts striped over kStripes cache lines (block b adds to stripe
      * b % kStripes): a counter shared by every block of a launch serializes its
      * atomics (~12 ns each, measured); totals = ev + sum over stripes */
     unsigned long long evS[32][16];
+    unsigned long long dbg[8];       /* SURF_SEG_TIMING builds: k_tail_coop cycles (extend, shade, connect, segments) */
 };
 constexpr uint32_t kStripes = 32;    /* frameDone and event-count stripes */
+constexpr int kEvents = 9;           /* event kinds counted (ev / evS index) */
 
 /* Where a stream sample lives: radiance slot sid = (frame % window) * npx + pixel. */
 struct StreamGeom {
@@ -542,6 +562,151 @@ __device__ __forceinline__ bool traceAnyCoop(const DevScene& S, const TraceTable
         occ = instanceTrace<true>(S, Tt.inst[Tt.order[lane]], o, d, depth, u, v, prim, stk, stride, 0u);
     }
     return __ballot(occ) != 0ull;
+}
+
+/* ------------------------------------------------- one ray per wave, lanes as planes
+ * For the last long paths of a drain (whose single-path segment latency is
+ * what the drain waits for): every lane holds the same ray and the wave walks
+ * the reference's DFS itself -- same boxes, same near/far order, same pruning,
+ * same leaf order -- with the work of one node visit spread over lanes:
+ *   lanes 0..11 each load one bound of the node record (box b = l / 6,
+ *   axis a = (l % 6) / 2, side s = l & 1), lanes 12 / 13 its leftFirst / count;
+ *   (bound - o_a) * rd_a for all 12 planes is one multiply;
+ *   the reference's ternary min/max (same operand order, so NaN/inf cases
+ *   stay bit-identical) run on lane pairs and lane triples via DPP moves;
+ *   near/far, the stack (one VGPR, entry k in lane k) and the loop are scalar;
+ *   a leaf's triangles are tested in parallel lanes and accepted in index order.
+ * The DFS is the same sequence of decisions as blasTrace, so results equal
+ * traceScene's bit for bit (also for any-hit).  Needs all 64 lanes active, a
+ * single-leaf TLAS and a stack depth <= 64. */
+template <int CTRL>
+__device__ __forceinline__ float dppMov(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+constexpr int kDppSwap1 = 0xB1;             /* quad_perm [1,0,3,2]: lane l <- l ^ 1 */
+constexpr int kDppShr2 = 0x112, kDppShr4 = 0x114;   /* row_shr: lane l <- l - n (within 16) */
+
+__device__ __forceinline__ uint32_t planeDword(uint32_t l) {
+    if (l < 12u) return (l / 6u) * 8u + (l & 1u) * 4u + ((l % 6u) >> 1);
+    return l == 12u ? 3u : (l == 13u ? 7u : 0u);
+}
+__device__ __forceinline__ float pick3(V3 v, uint32_t a) { return a == 0u ? v.x : (a == 1u ? v.y : v.z); }
+
+/* Both children's slab distances from this lane's bound v (lanes 0..11):
+ * dn = box 0 (left child), df = box 1 (right), kFarAway on a miss (slab()). */
+__device__ __forceinline__ void slabPair(float v, float oA, float rdA, float depth, float& d0, float& d1) {
+    const float t = (v - oA) * rdA;
+    const float tp = dppMov<kDppSwap1>(t);
+    const float t0a = tmin(t, tp), t1a = tmax(t, tp);          /* even lanes: (lo, hi) of one axis */
+    const float t0x = dppMov<kDppShr4>(t0a), t0y = dppMov<kDppShr2>(t0a);
+    const float t1x = dppMov<kDppShr4>(t1a), t1y = dppMov<kDppShr2>(t1a);
+    const float m0 = tmax(tmax(t0x, t0y), t0a);                /* lane 6b+4: t0a is the z axis */
+    const float m1 = tmin(tmin(t1x, t1y), t1a);
+    const float dist = (m1 >= m0 && m0 < depth && m1 > 0.0f) ? m0 : kFarAway;
+    d0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dist), 4));
+    d1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dist), 10));
+}
+
+/* Triangles [lf, lf + cnt) of a BLAS leaf, one per lane, accepted in index order. */
+template <bool ANY>
+__device__ __forceinline__ bool leafWave(const float4* tri, uint32_t lf, uint32_t cnt, V3 o, V3 d, float& depth,
+                                         float& hu, float& hv, uint32_t& hprim) {
+    bool any = false;
+    const uint32_t lane = __lane_id();
+    for (uint32_t b = 0; b < cnt; b += 64u) {
+        const uint32_t k = b + lane;
+        float t = depth, u = 0.0f, v = 0.0f;
+        uint32_t prim = 0;
+        bool h = false;
+        if (k < cnt) {
+            const float4* tp = tri + 3u * (lf + k);
+            const float4 a = tp[0], e1 = tp[1], e2 = tp[2];
+            prim = f2u(a.w);
+            h = triHit(xyz(a), xyz(e1), xyz(e2), o, d, t, u, v);
+        }
+        unsigned long long m = __ballot(h);
+        if (ANY) { if (m) return true; continue; }
+        while (m) {
+            const int j = __ffsll((long long)m) - 1;
+            m &= m - 1ull;
+            const float tj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t), j));
+            if (tj < depth) {
+                depth = tj;
+                hu = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(u), j));
+                hv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
+                hprim = (uint32_t)__builtin_amdgcn_readlane((int)prim, j);
+                any = true;
+            }
+        }
+    }
+    return any;
+}
+
+template <bool ANY>
+__device__ __forceinline__ bool blasWave(const DevScene& S, const TraceInst& I, V3 o, V3 d, float& depth, float& hu, float& hv,
+                                         uint32_t& hprim) {
+    const uint32_t lane = __lane_id();
+    const uint32_t nodeOff = I.meta.x;
+    const float4* tri = S.tris + 3u * I.meta.y;
+    const uint32_t rlf = f2u(I.r0.w), rcnt = f2u(I.r1.w);
+    if (rcnt != 0u) return leafWave<ANY>(tri, rlf, rcnt, o, d, depth, hu, hv, hprim);
+    const V3 rd = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    const uint32_t dw = planeDword(lane), ax = lane < 12u ? (lane % 6u) >> 1 : 0u;
+    const float oA = pick3(o, ax), rdA = pick3(rd, ax);
+    /* root: never box-tested (bvh.cpp:131); its children's boxes are in its record */
+    float dn, df;
+    slabPair(reinterpret_cast<const float*>(&I.r0)[dw], oA, rdA, depth, dn, df);
+    uint32_t cn = nodeOff + rlf, cf = cn + 1u;
+    if (dn > df) { const float t = dn; dn = df; df = t; const uint32_t c = cn; cn = cf; cf = c; }
+    if (dn == kFarAway) return false;
+    uint32_t stk = 0, sp = 0, node = cn;
+    if (df != kFarAway) { stk = lane == sp ? cf : stk; ++sp; }
+    bool any = false;
+    for (;;) {
+        const float v = reinterpret_cast<const float*>(S.nodes + 4u * node)[dw];
+        const uint32_t lf = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(v), 12);
+        const uint32_t cnt = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(v), 13);
+        if (cnt != 0u) {
+            if (leafWave<ANY>(tri, lf, cnt, o, d, depth, hu, hv, hprim)) {
+                if (ANY) return true;
+                any = true;
+            }
+            if (sp == 0u) break;
+            node = (uint32_t)__builtin_amdgcn_readlane((int)stk, (int)--sp);
+            continue;
+        }
+        slabPair(v, oA, rdA, depth, dn, df);
+        cn = nodeOff + lf; cf = cn + 1u;
+        if (dn > df) { const float t = dn; dn = df; df = t; const uint32_t c = cn; cn = cf; cf = c; }
+        if (dn == kFarAway) {
+            if (sp == 0u) break;
+            node = (uint32_t)__builtin_amdgcn_readlane((int)stk, (int)--sp);
+        } else {
+            node = cn;
+            if (df != kFarAway) { stk = lane == sp ? cf : stk; ++sp; }
+        }
+    }
+    return any;
+}
+
+/* BvhTLAS::intersect / intersectAny over a single-leaf TLAS (bvh.cpp:654-778). */
+template <bool ANY>
+__device__ __forceinline__ bool traceWave(const DevScene& S, const TraceTables& Tt, V3 o, V3 d, float& depth, float& hu,
+                                          float& hv, uint32_t& hinst, uint32_t& hprim) {
+    bool any = false;
+    for (uint32_t k = 0; k < S.tlasLeafCount; ++k) {
+        const uint32_t ii = Tt.order[k];
+        const TraceInst& I = Tt.inst[ii];
+        V3 oo = mk3(rowDot(I.m0, o.x, o.y, o.z, 1.0f), rowDot(I.m1, o.x, o.y, o.z, 1.0f), rowDot(I.m2, o.x, o.y, o.z, 1.0f));
+        if (!I.meta.z) oo = divs(oo, rowDot(I.m3, o.x, o.y, o.z, 1.0f));
+        const V3 dd = mk3(rowDot(I.m0, d.x, d.y, d.z, 0.0f), rowDot(I.m1, d.x, d.y, d.z, 0.0f), rowDot(I.m2, d.x, d.y, d.z, 0.0f));
+        if (blasWave<ANY>(S, I, oo, dd, depth, hu, hv, hprim)) {
+            if (ANY) return true;
+            any = true;
+            hinst = ii;
+        }
+    }
+    return any;
 }
 
 /* --------------------------------------------------------------- wave helpers */
@@ -964,6 +1129,57 @@ __device__ __forceinline__ void shadePath(const DevScene& S, const ShadeTables& 
     }
 }
 
+/* ---------------------------------------------------------- long-path ring
+ * Agent-scope (sc1) stores: the bytes leave the XCD's L2 for the coherent
+ * fabric, so a k_long wave on another XCD reads them after its acquire. */
+__device__ __forceinline__ void stAgent(float4* p, float4 v) {
+    uint32_t* q = reinterpret_cast<uint32_t*>(p);
+    __hip_atomic_store(q + 0, __float_as_uint(v.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(q + 1, __float_as_uint(v.y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(q + 2, __float_as_uint(v.z), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(q + 3, __float_as_uint(v.w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ldAgent(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+/* Wave-level escape (every lane of the wave calls it): reserves ring entries
+ * for the lanes with `want` set -- as many as fit, the rest stay in the
+ * wavefront -- and publishes their path + pending shadow ray.  Returns whether
+ * this lane's path left. */
+template <class ShadeOutT>
+__device__ __forceinline__ bool escapeLong(Counters* C, const LongRing& LR, bool want, const ShadeOutT& r) {
+    const unsigned long long m = __ballot(want);
+    if (!m) return false;
+    uint32_t base = 0, n = 0;
+    if (laneId() == 0) {
+        const uint32_t need = (uint32_t)__popcll(m), cap = C->ringCap;
+        uint32_t t = ldAgent(&C->ringTail);
+        for (;;) {
+            /* head only grows, so a stale head under-estimates the room */
+            const uint32_t room = cap - (t - ldAgent(&C->ringHead));
+            n = need < room ? need : room;
+            if (n == 0u) break;
+            const uint32_t prev = atomicCAS(&C->ringTail, t, t + n);
+            if (prev == t) { base = t; break; }
+            t = prev;
+        }
+    }
+    base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
+    n = (uint32_t)__builtin_amdgcn_readfirstlane((int)n);
+    const uint32_t rank = rankBelow(m);
+    const bool esc = want && rank < n;
+    const uint32_t i = base + rank, k = i & (C->ringCap - 1u);
+    if (esc) {
+        stAgent(&LR.o[k], r.o); stAgent(&LR.d[k], r.d); stAgent(&LR.T[k], r.T);
+        stAgent(&LR.so[k], r.so); stAgent(&LR.sd[k], r.sd);
+        stAgent(&LR.sc[k], make_float4(r.sc.x, r.sc.y, r.sc.z, r.shadow ? 1.0f : 0.0f));
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (esc) __hip_atomic_store(&LR.seq[k], i + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return esc;
+}
+
 /* Frame completion: one atomic per distinct frame slot in the wave (lanes of a
  * wave almost always share one frame). */
 __device__ __forceinline__ void frameDoneAdd(uint32_t* frameDone, bool done, uint32_t slot) {
@@ -981,7 +1197,7 @@ template <bool LDS_TABLES>
 __global__ __launch_bounds__(kBlock, SURF_SHADE_WAVES) void k_shade(DevScene S, Pool cur, Pool nxt, const float4* __restrict__ hitTUV,
                                                   const uint32_t* __restrict__ hitInst, ShadowQ Q,
                                                   float4* __restrict__ rad, uint32_t* __restrict__ frameDone,
-                                                  uint32_t npx, uint32_t window, Counters* C, int par, LongQueues LQ) {
+                                                  uint32_t npx, uint32_t window, Counters* C, int par, LongRing LR) {
     if (blockIdx.x * blockDim.x >= C->nIn[par]) return;     /* nothing to shade in this block */
     __shared__ DevInstance sInst[LDS_TABLES ? kLdsInst : 1];
     __shared__ DevMaterial sMat[LDS_TABLES ? kLdsMats : 1];
@@ -997,8 +1213,7 @@ __global__ __launch_bounds__(kBlock, SURF_SHADE_WAVES) void k_shade(DevScene S, 
     __shared__ uint32_t sBase[2][2];
     const uint32_t n = C->nIn[par];
     const uint32_t maxSeg = C->maxSeg, zeroCutoff = C->zeroCutoff;
-    const uint32_t longThresh = C->longThresh, eSel = C->eSel % 3u, eCap = C->eCap;
-    const Pool eq = LQ.esc[eSel];
+    const uint32_t longThresh = C->longThresh;
     const uint32_t wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
     uint32_t it = 0;
     unsigned long long cHit = 0, cCont = 0, cSh = 0, cAcc = 0;
@@ -1015,13 +1230,10 @@ __global__ __launch_bounds__(kBlock, SURF_SHADE_WAVES) void k_shade(DevScene S, 
             shadePath(S, Tb, o4, ldS(&cur.d[i]), ldS(&cur.T[i]), ldS(&hitTUV[i]), ldSu(&hitInst[i]), maxSeg, zeroCutoff, r);
             if (r.addRad) addRadiance(rad, f2u(o4.w), r.radd);
         }
-        /* a path reaching longThresh segments leaves for the k_long worker */
-        bool esc = false;
-        if (r.cont && longThresh != 0u && r.seg + 1u >= longThresh) {
-            const uint32_t k = atomicAdd(&C->eN[eSel], 1u);
-            if (k < eCap) { eq.o[k] = r.o; eq.d[k] = r.d; eq.T[k] = r.T; esc = true; }
-        }
-        const unsigned long long mCont = __ballot(r.cont && !esc), mSh = __ballot(r.shadow);
+        /* a path reaching longThresh segments leaves for the k_long worker,
+         * taking this bounce's shadow ray with it */
+        const bool esc = longThresh != 0u && escapeLong(C, LR, r.cont && r.seg + 1u >= longThresh, r);
+        const unsigned long long mCont = __ballot(r.cont && !esc), mSh = __ballot(r.shadow && !esc);
         if (laneId() == 0) { sWave[it][wv][0] = (uint32_t)__popcll(mCont); sWave[it][wv][1] = (uint32_t)__popcll(mSh); }
         __syncthreads();
         if (threadIdx.x == 0) {
@@ -1036,7 +1248,7 @@ __global__ __launch_bounds__(kBlock, SURF_SHADE_WAVES) void k_shade(DevScene S, 
         jc += rankBelow(mCont);
         js += rankBelow(mSh);
         if (r.cont && !esc) { stS(&nxt.o[jc], r.o); stS(&nxt.d[jc], r.d); stS(&nxt.T[jc], r.T); }
-        if (r.shadow) { stS(&Q.o[js], r.so); stS(&Q.d[js], r.sd); stS(&Q.c[js], r.sc); }
+        if (r.shadow && !esc) { stS(&Q.o[js], r.so); stS(&Q.d[js], r.sd); stS(&Q.c[js], r.sc); }
         /* a path that ends here may still have this phase's shadow ray pending:
          * connect runs before the host reads frameDone (end of the phase). */
         frameDoneAdd(frameDone + (blockIdx.x % kStripes) * window, active && !r.cont, slot);
@@ -1047,7 +1259,7 @@ __global__ __launch_bounds__(kBlock, SURF_SHADE_WAVES) void k_shade(DevScene S, 
         }
         cHit += (unsigned long long)__popcll(__ballot(r.hitGeom));
         cCont += (unsigned long long)__popcll(__ballot(r.cont));
-        cSh += (unsigned long long)__popcll(mSh);
+        cSh += (unsigned long long)__popcll(__ballot(r.shadow));
         cAcc += (unsigned long long)__popcll(__ballot(r.accd));
     }
     blockCount<4>(C, {1, 2, 3, 4}, {cHit, cCont, cSh, cAcc});
@@ -1233,13 +1445,39 @@ __global__ __launch_bounds__(64, 3) void k_tail(DevScene S, Pool cur, uint32_t n
             lds + threadIdx.x, blockDim.x, firstCounted);
 }
 
-/* Long-path worker (second stream, concurrent with a graph replay): advances
- * every path of lp[in] and of escape queue `es` by up to `budget` segments;
- * paths still alive go to lp[out].  Grid-stride over both inputs. */
+/* Radiance add of the long-path worker: rad[sid] += c per channel, bit-exact
+ * (an IEEE f32 add in the ALU, installed by compare-and-swap).  The worker is
+ * the path's only writer, so the swap succeeds at once; it only has to be an
+ * agent-scope atomic because the worker runs beside the wavefront kernels,
+ * which write other samples of the same cache lines. */
+__device__ __forceinline__ void addExact(float* p, float c) {
+    unsigned int* u = reinterpret_cast<unsigned int*>(p);
+    unsigned int old = ldAgent(u);
+    for (;;) {
+        const unsigned int nv = __float_as_uint(__uint_as_float(old) + c);
+        const unsigned int prev = atomicCAS(u, old, nv);
+        if (prev == old) return;
+        old = prev;
+    }
+}
+__device__ __forceinline__ void addRadianceAtomic(float4* rad, uint32_t sid, V3 c) {
+    float* r = reinterpret_cast<float*>(rad + sid);
+    addExact(r + 0, c.x); addExact(r + 1, c.y); addExact(r + 2, c.z);
+}
+
+/* Long-path worker (stream 2, concurrent with the wavefront's graph replays):
+ * every lane owns at most one path and advances it one segment per iteration
+ * -- extend, shade, shadow ray, the wavefront kernels' device functions --
+ * instead of one segment per wavefront phase.  An idle lane claims the next
+ * published ring entry (resolving the escaping bounce's shadow ray first).
+ * The launch lives `lifetime` ticks of the 100 MHz clock: then each lane parks
+ * its path in its park slot (the next launch, same grid, resumes it) and the
+ * wave exits; a wave also exits when the host has closed the ring and it is
+ * empty.  No wave ever waits on another, so every launch ends. */
 template <bool LDS_TABLES>
-__global__ __launch_bounds__(64, 3) void k_long(DevScene S, LongQueues LQ, uint32_t in, uint32_t es, float4* __restrict__ rad,
+__global__ __launch_bounds__(64, 2) void k_long(DevScene S, LongRing LR, float4* __restrict__ rad,
                                              uint32_t* __restrict__ frameDone, uint32_t npx, uint32_t window, Counters* C,
-                                             uint32_t stackWords, uint32_t budget) {
+                                             uint32_t stackWords, unsigned long long lifetime) {
     extern __shared__ uint32_t lds[];
     const TraceTables Tt = traceTables<LDS_TABLES>(S, lds, stackWords);
     __shared__ DevInstance sInst[LDS_TABLES ? kLdsInst : 1];
@@ -1250,14 +1488,138 @@ __global__ __launch_bounds__(64, 3) void k_long(DevScene S, LongQueues LQ, uint3
         stageTables(S, sInst, sMat, sLights);
         Tb = ShadeTables{sInst, sMat, sLights};
     }
-    const uint32_t nLp = min(C->lpN[in], C->lpCap), nEs = min(C->eN[es], C->eCap);
-    const Sink sink{LQ.lp[in ^ 1u], &C->lpN[in ^ 1u], C->lpCap};
-    for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < nLp + nEs; v += gridDim.x * blockDim.x) {
-        const Pool& src = v < nLp ? LQ.lp[in] : LQ.esc[es];
-        const uint32_t k = v < nLp ? v : v - nLp;
-        runPath(S, Tt, Tb, src.o[k], src.d[k], src.T[k], budget, sink, rad, frameDone, npx, window, C, lds + threadIdx.x,
-                blockDim.x, 0u);
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    const uint32_t lane = threadIdx.x, gl = blockIdx.x * 64u + lane;
+    uint32_t* stk = lds + threadIdx.x;
+    const uint32_t stride = blockDim.x;
+    const uint32_t maxSeg = C->maxSeg, zeroCutoff = C->zeroCutoff, mask = C->ringCap - 1u;
+    unsigned long long* ev = C->evS[blockIdx.x % kStripes];
+    uint32_t* fd = frameDone + (blockIdx.x % kStripes) * window;
+    /* lane state: the path and its event counts since it was claimed / resumed */
+    bool active = LR.parkFlag[gl] != 0u;      /* written by the previous launch (stream order) */
+    float4 o4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), d4 = o4, T4 = o4, so = o4, sd = o4, sc = o4;
+    if (active) { o4 = LR.park.o[gl]; d4 = LR.park.d[gl]; T4 = LR.park.T[gl]; LR.parkFlag[gl] = 0u; }
+    {
+        const unsigned long long m = __ballot(active);
+        if (lane == 0 && m) atomicSub(&C->parkedN, (uint32_t)__popcll(m));
     }
+    uint32_t nExt = 0, nHit = 0, nCont = 0, nSh = 0, nAcc = 0, nUn = 0;
+    bool pend = false;
+    for (;;) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > lifetime) break;
+        /* ---- claim: idle lanes take the next published entries, in order */
+        const unsigned long long idle = __ballot(!active);
+        if (idle) {
+            uint32_t h = 0, t = 0;
+            if (lane == 0) { h = ldAgent(&C->ringHead); t = ldAgent(&C->ringTail); }
+            h = (uint32_t)__builtin_amdgcn_readfirstlane((int)h);
+            t = (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
+            const uint32_t nIdle = (uint32_t)__popcll(idle);
+            const uint32_t avail = (t - h) < nIdle ? (t - h) : nIdle;
+            if (avail) {
+                const uint32_t rank = rankBelow(idle);
+                const bool want = !active && rank < avail;
+                const bool pub = want && ldAgent(&LR.seq[(h + rank) & mask]) == h + rank + 1u;
+                const unsigned long long notPub = __ballot(want && !pub);
+                const uint32_t n = notPub ? (uint32_t)__popcll(idle & ((notPub & (~notPub + 1ull)) - 1ull)) : avail;
+                if (n) {
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    const bool take = want && rank < n;
+                    float4 a0 = o4, a1 = d4, a2 = T4, a3 = so, a4 = sd, a5 = sc;
+                    if (take) {
+                        const uint32_t k = (h + rank) & mask;
+                        a0 = LR.o[k]; a1 = LR.d[k]; a2 = LR.T[k]; a3 = LR.so[k]; a4 = LR.sd[k]; a5 = LR.sc[k];
+                    }
+                    /* the entries are read before the head moves past them: a
+                     * producer reuses slot k only once head > index */
+                    uint32_t ok = 0;
+                    if (lane == 0) ok = atomicCAS(&C->ringHead, h, h + n) == h ? 1u : 0u;
+                    ok = (uint32_t)__builtin_amdgcn_readfirstlane((int)ok);
+                    if (ok && take) {
+                        active = true;
+                        o4 = a0; d4 = a1; T4 = a2; so = a3; sd = a4; sc = a5;
+                        pend = a5.w != 0.0f;
+                    }
+                }
+            }
+        }
+        if (!__ballot(active)) {
+            uint32_t done = 0;
+            if (lane == 0) done = ldAgent(&C->closing) && ldAgent(&C->ringHead) == ldAgent(&C->ringTail);
+            if (__builtin_amdgcn_readfirstlane((int)done)) break;
+            /* idle: normal priority, poll every ~8k cycles */
+            __builtin_amdgcn_s_setprio(0);
+            __builtin_amdgcn_s_sleep(127);
+            continue;
+        }
+        /* a wave with paths runs at the highest issue priority: the SIMD's
+         * wavefront waves (throughput work) take the cycles it leaves, so a
+         * long path's segment latency stays near the unloaded latency */
+        __builtin_amdgcn_s_setprio(3);
+        if (!active) continue;
+        /* ---- one segment of each active lane's path */
+        if (pend) {
+            /* the escaping bounce's shadow ray (its n_shadow was counted by k_shade) */
+            pend = false;
+            float sdep = so.w, su = 0.0f, sv = 0.0f;
+            uint32_t si = kUnset, sp = kUnset;
+            if (!traceScene<true>(S, Tt, xyz(so), xyz(sd), sdep, su, sv, si, sp, stk, stride)) {
+                addRadianceAtomic(rad, f2u(sd.w), xyz(sc));
+                ++nUn; ++nAcc;
+            }
+        }
+        float depth = kFarAway, u = 0.0f, v = 0.0f;
+        uint32_t inst = kUnset, prim = kUnset;
+        const bool hit = traceScene<false>(S, Tt, xyz(o4), xyz(d4), depth, u, v, inst, prim, stk, stride);
+        ++nExt;
+        ShadeOut r;
+        shadePath(S, Tb, o4, d4, T4, make_float4(depth, u, v, u2f(prim)), hit ? inst : kUnset, maxSeg, zeroCutoff, r);
+        if (r.addRad) addRadianceAtomic(rad, f2u(o4.w), r.radd);
+        nHit += r.hitGeom; nAcc += r.accd;
+        if (r.shadow) {
+            ++nSh;
+            float sdep = r.so.w, su = 0.0f, sv = 0.0f;
+            uint32_t si = kUnset, sp = kUnset;
+            if (!traceScene<true>(S, Tt, xyz(r.so), xyz(r.sd), sdep, su, sv, si, sp, stk, stride)) {
+                addRadianceAtomic(rad, f2u(r.sd.w), xyz(r.sc));
+                ++nUn; ++nAcc;
+            }
+        }
+        if (r.capped) {
+            const unsigned long long k = atomicAdd(&C->ev[7], 1ull);
+            if (k < 64) C->capped[k] = f2u(o4.w);
+        }
+        if (r.cont) {
+            ++nCont;
+            o4 = r.o; d4 = r.d; T4 = r.T;
+            continue;
+        }
+        /* path finished: its radiance adds have returned, so completion follows them */
+        atomicMax(&C->segMax, r.seg);
+        atomicAdd(&fd[f2u(o4.w) / npx], 1u);
+        atomicAdd(&ev[0], (unsigned long long)nExt); atomicAdd(&ev[1], (unsigned long long)nHit);
+        atomicAdd(&ev[2], (unsigned long long)nCont); atomicAdd(&ev[3], (unsigned long long)nSh);
+        atomicAdd(&ev[4], (unsigned long long)nAcc); atomicAdd(&ev[5], (unsigned long long)nUn);
+        atomicAdd(&ev[8], 1ull);
+        nExt = nHit = nCont = nSh = nAcc = nUn = 0;
+        active = false;
+    }
+    /* lifetime over (or ring closed and empty): park what is still running */
+    if (active) {
+        LR.park.o[gl] = o4; LR.park.d[gl] = d4; LR.park.T[gl] = T4;
+        LR.parkFlag[gl] = 1u;
+        atomicAdd(&ev[0], (unsigned long long)nExt); atomicAdd(&ev[1], (unsigned long long)nHit);
+        atomicAdd(&ev[2], (unsigned long long)nCont); atomicAdd(&ev[3], (unsigned long long)nSh);
+        atomicAdd(&ev[4], (unsigned long long)nAcc); atomicAdd(&ev[5], (unsigned long long)nUn);
+    }
+    const unsigned long long m = __ballot(active);
+    if (lane == 0 && m) atomicAdd(&C->parkedN, (uint32_t)__popcll(m));
+}
+
+/* Closes the long-path ring for the rest of the stream (no k_shade will run
+ * before the next stream): idle workers may exit once it is empty. */
+__global__ void k_close(Counters* C) {
+    if (threadIdx.x == 0) __hip_atomic_store(&C->closing, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 /* Cooperative tail: one path per 64-lane wave (block), for the few very long
@@ -1267,7 +1629,7 @@ __global__ __launch_bounds__(64, 3) void k_long(DevScene S, LongQueues LQ, uint3
  * inputs, same results, no broadcast), shadow ray any-hit in parallel lanes;
  * lane 0 does the writes.  Identical results to k_tail.  LDS: traversal stack,
  * box-distance stack (stackWords words each), then the trace tables. */
-template <bool LDS_TABLES>
+template <bool LDS_TABLES, bool WAVE>
 __global__ __launch_bounds__(64, 3) void k_tail_coop(DevScene S, Pool cur, uint32_t n, float4* __restrict__ rad,
                                                   uint32_t* __restrict__ frameDone, uint32_t npx, uint32_t window, Counters* C,
                                                   uint32_t stackWords, uint32_t firstCounted) {
@@ -1291,22 +1653,50 @@ __global__ __launch_bounds__(64, 3) void k_tail_coop(DevScene S, Pool cur, uint3
     float4 o4 = cur.o[i], d4 = cur.d[i], T4 = cur.T[i];
     const uint32_t slot = f2u(o4.w) / npx;
     unsigned long long nExt = 0, nHit = 0, nCont = 0, nSh = 0, nAcc = 0, nUn = 0;
+#if SURF_SEG_TIMING
+    unsigned long long cyc[3] = {0, 0, 0};
+#endif
     for (;;) {
         float depth = kFarAway, u = 0.0f, v = 0.0f;
         uint32_t inst = kUnset, prim = kUnset;
-        const bool hit = traceSceneCoop(S, Tt, xyz(o4), xyz(d4), depth, u, v, inst, prim, stk, astk, stride);
+#if SURF_SEG_TIMING
+        const unsigned long long c0 = __builtin_readcyclecounter();
+#endif
+        const bool hit = WAVE ? traceWave<false>(S, Tt, xyz(o4), xyz(d4), depth, u, v, inst, prim)
+                              : traceSceneCoop(S, Tt, xyz(o4), xyz(d4), depth, u, v, inst, prim, stk, astk, stride);
         ++nExt;
         ShadeOut r;
+#if SURF_SEG_TIMING
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        const unsigned long long c1 = __builtin_readcyclecounter();
+#endif
         shadePath(S, Tb, o4, d4, T4, make_float4(depth, u, v, u2f(prim)), hit ? inst : kUnset, maxSeg, zeroCutoff, r);
         if (lead && r.addRad) addRadiance(rad, f2u(o4.w), r.radd);
+#if SURF_SEG_TIMING
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        const unsigned long long c2 = __builtin_readcyclecounter();
+#endif
         nHit += r.hitGeom; nAcc += r.accd;
         if (r.shadow) {
             ++nSh;
-            if (!traceAnyCoop(S, Tt, xyz(r.so), xyz(r.sd), r.so.w, stk, stride)) {
+            bool occ;
+            if (WAVE) {
+                float sdep = r.so.w, su = 0.0f, sv = 0.0f;
+                uint32_t si = kUnset, sp = kUnset;
+                occ = traceWave<true>(S, Tt, xyz(r.so), xyz(r.sd), sdep, su, sv, si, sp);
+            } else {
+                occ = traceAnyCoop(S, Tt, xyz(r.so), xyz(r.sd), r.so.w, stk, stride);
+            }
+            if (!occ) {
                 if (lead) addRadiance(rad, f2u(r.sd.w), xyz(r.sc));
                 ++nUn; ++nAcc;
             }
         }
+#if SURF_SEG_TIMING
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        const unsigned long long c3 = __builtin_readcyclecounter();
+        cyc[0] += c1 - c0; cyc[1] += c2 - c1; cyc[2] += c3 - c2;
+#endif
         if (lead && r.capped) {
             const unsigned long long k = atomicAdd(&C->ev[7], 1ull);
             if (k < 64) C->capped[k] = f2u(o4.w);
@@ -1326,6 +1716,10 @@ __global__ __launch_bounds__(64, 3) void k_tail_coop(DevScene S, Pool cur, uint3
         atomicAdd(&ev[0], nExt - (unsigned long long)firstCounted); atomicAdd(&ev[1], nHit); atomicAdd(&ev[2], nCont);
         atomicAdd(&ev[3], nSh); atomicAdd(&ev[4], nAcc); atomicAdd(&ev[5], nUn);
         atomicAdd(&ev[6], 1ull);
+#if SURF_SEG_TIMING
+        atomicAdd(&C->dbg[0], cyc[0]); atomicAdd(&C->dbg[1], cyc[1]); atomicAdd(&C->dbg[2], cyc[2]);
+        atomicAdd(&C->dbg[3], nExt); atomicAdd(&C->dbg[4], nSh);
+#endif
     }
 }
 
@@ -1424,6 +1818,7 @@ __global__ __launch_bounds__(kBlock) void k_trace_any(DevScene S, const float* _
 /* Cooperative traversal entry points (one ray per 64-lane block): the same
  * results as k_trace_closest / k_trace_any, exposed for parity tests and
  * latency measurements of the cooperative tail's traversal. */
+template <bool WAVE>
 __global__ __launch_bounds__(64) void k_trace_closest_coop(DevScene S, const float* __restrict__ o, const float* __restrict__ d,
                                                            uint32_t n, float4* __restrict__ tuv, uint2* __restrict__ ip,
                                                            uint32_t stackWords) {
@@ -1433,14 +1828,16 @@ __global__ __launch_bounds__(64) void k_trace_closest_coop(DevScene S, const flo
     if (i >= n) return;
     float depth = kFarAway, u = 0.0f, v = 0.0f;
     uint32_t inst = kUnset, prim = kUnset;
-    const bool hit = traceSceneCoop(S, Tt, mk3(o[3 * i], o[3 * i + 1], o[3 * i + 2]), mk3(d[3 * i], d[3 * i + 1], d[3 * i + 2]),
-                                    depth, u, v, inst, prim, lds + threadIdx.x,
-                                    reinterpret_cast<float*>(lds + stackWords) + threadIdx.x, blockDim.x);
+    const V3 ro = mk3(o[3 * i], o[3 * i + 1], o[3 * i + 2]), rdir = mk3(d[3 * i], d[3 * i + 1], d[3 * i + 2]);
+    const bool hit = WAVE ? traceWave<false>(S, Tt, ro, rdir, depth, u, v, inst, prim)
+                          : traceSceneCoop(S, Tt, ro, rdir, depth, u, v, inst, prim, lds + threadIdx.x,
+                                           reinterpret_cast<float*>(lds + stackWords) + threadIdx.x, blockDim.x);
     if (threadIdx.x == 0) {
         tuv[i] = make_float4(depth, hit ? u : 0.0f, hit ? v : 0.0f, 0.0f);
         ip[i] = make_uint2(hit ? inst : kUnset, hit ? prim : kUnset);
     }
 }
+template <bool WAVE>
 __global__ __launch_bounds__(64) void k_trace_any_coop(DevScene S, const float* __restrict__ o, const float* __restrict__ d,
                                                        const float* __restrict__ tmaxv, uint32_t n, uint8_t* __restrict__ occ,
                                                        uint32_t stackWords) {
@@ -1448,8 +1845,15 @@ __global__ __launch_bounds__(64) void k_trace_any_coop(DevScene S, const float* 
     const TraceTables Tt = stageTrace(S, lds, stackWords);
     const uint32_t i = blockIdx.x;
     if (i >= n) return;
-    const bool oc = traceAnyCoop(S, Tt, mk3(o[3 * i], o[3 * i + 1], o[3 * i + 2]), mk3(d[3 * i], d[3 * i + 1], d[3 * i + 2]),
-                                 tmaxv[i], lds + threadIdx.x, blockDim.x);
+    const V3 ro = mk3(o[3 * i], o[3 * i + 1], o[3 * i + 2]), rdir = mk3(d[3 * i], d[3 * i + 1], d[3 * i + 2]);
+    bool oc;
+    if (WAVE) {
+        float depth = tmaxv[i], u = 0.0f, v = 0.0f;
+        uint32_t inst = kUnset, prim = kUnset;
+        oc = traceWave<true>(S, Tt, ro, rdir, depth, u, v, inst, prim);
+    } else {
+        oc = traceAnyCoop(S, Tt, ro, rdir, tmaxv[i], lds + threadIdx.x, blockDim.x);
+    }
     if (threadIdx.x == 0) occ[i] = oc ? 1 : 0;
 }
 

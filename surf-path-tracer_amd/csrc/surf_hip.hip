@@ -32,6 +32,7 @@ namespace {
 constexpr int kPhasesPerGraph = 8;          /* even: parity returns to 0 after a replay */
 constexpr uint32_t kMaxStack = 120;          /* LDS stack entries per ray (block 256 -> 120 KiB max) */
 constexpr uint64_t kMaxIterations = 1ull << 22;  /* safety net: a path longer than this is a bug */
+constexpr uint32_t kDefaultLifetimeUs = 10000;   /* k_long launch lifetime */
 
 std::mutex gErrMutex;
 std::string gLastError;
@@ -99,24 +100,26 @@ struct surf_ctx {
     bool zeroCutoff = true;        /* radiance-neutral early end of T == 0 paths */
     uint64_t pushedLimit = 0;
     uint32_t tailPaths = 0;        /* drain policy (surf_set_tail_policy), 0 = automatic */
-    uint32_t tailBudget = 0;       /* per-stage segment budget of the drain tail (0 = one stage: measured fastest) */
+    uint32_t tailBudget = 16;      /* per-stage segment budget of the drain tail (0 = one stage); 16: measured fastest */
     Pool surv[2]{};                /* drain survivors, ping-pong between stages */
     uint32_t survCap = 0;
     uint32_t coopMax = 0;          /* survivors handled by the cooperative tail (one path per wave) */
-    uint32_t coopAll = 0;
-    int drainReplays = 1;          /* graph replays per host poll while draining (SURF_DRAIN_REPLAYS) */          /* single-stage drain: cooperative tail when <= this many paths (surf_set_tail_coop) */
+    uint32_t coopAll = 20000;      /* drain paths left to the cooperative (one path per wave) tail (surf_set_tail_coop) */
+    int drainReplays = 1;          /* graph replays per host poll while draining (SURF_DRAIN_REPLAYS) */
     bool coopEligible = false;     /* single-leaf TLAS of <= 64 instances, LDS tables */
     int traceMode = 0;             /* surf_trace_closest/_any: 0 one ray per lane, 1 one ray per wave */
     bool persistent = false;       /* out-of-step lanes with per-wave ray ranges: measured 4x slower */
-    /* long paths: escape queues + long-path pools, advanced by k_long on stream2 */
-    uint32_t longThresh = 0;       /* escape length (surf_set_long_paths; 0 = off: measured slower) */
-    uint32_t longBudget = 64;      /* segments per path per k_long launch */
-    uint32_t longGrid = 0;         /* k_long workgroups (64 lanes) */
+    /* long paths: ring + k_long worker launches on stream2 (surf_set_long_paths) */
+    uint32_t longThresh = 0;       /* escape length (0 = off) */
+    unsigned long long longLifetime = 0;   /* worker launch lifetime, 100 MHz ticks */
+    uint32_t longGrid = 0;         /* k_long waves (64 lanes each) */
+    uint32_t ringCap = 0;
     hipStream_t stream2 = nullptr;
-    hipEvent_t evG[3] = {}, evL[3] = {};
-    LongQueues LQ{};
-    uint32_t eCap = 0, lpCap = 0;
-    uint64_t replay = 0;           /* graph replays of the current stream */
+    static constexpr int kWorkerQueue = 2;   /* worker launches kept queued on stream2 */
+    hipEvent_t evW[kWorkerQueue] = {};
+    uint64_t wLaunched = 0, wRetired = 0;    /* worker launches of this context */
+    bool closed = false;           /* k_close issued for the current stream */
+    LongRing LR{};
     uint32_t tailLanes = 0;
     uint32_t segMaxBase = 0;       /* longest path of finished streams */
 
@@ -128,7 +131,7 @@ struct surf_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipEvent_t pev[kPhasesPerGraph * 4 + 1] = {};
     surf_stats stats{};
-    unsigned long long evBase[8] = {};   /* event counts of finished streams since the last clear */
+    unsigned long long evBase[kEvents] = {};   /* event counts of finished streams since the last clear */
 };
 
 #define SURF_CHECK(ctx, call)                                                             \
@@ -241,8 +244,11 @@ int upload(surf_ctx* c, const std::vector<T>& host, const T** devOut) {
 int allocWavefront(surf_ctx* c) {
     if (c->allocated) return SURF_OK;
     if (c->capacity == 0) {
-        /* default: ~4 frames of paths in flight keeps 256 CUs busy, bounded at 4M paths */
-        const uint64_t want = (uint64_t)c->npx * 4;
+        /* default: ~4 full frames of paths in flight, bounded at 4M paths.  Sized
+         * from the whole frame, not the shard: a row shard of G GPUs keeps the
+         * same pool, so its stream needs ~G times fewer wavefront phases (each
+         * phase pays launch and poll latency however few paths it holds). */
+        const uint64_t want = (uint64_t)c->width * c->height * 4;
         c->capacity = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(want, 65536), 1u << 22);
     }
     if (c->window == 0) {
@@ -257,18 +263,27 @@ int allocWavefront(surf_ctx* c) {
         if ((rc = devAlloc(c, c->wfAllocs, &c->pool[p].d, cap))) return rc;
         if ((rc = devAlloc(c, c->wfAllocs, &c->pool[p].T, cap))) return rc;
     }
-    c->eCap = (uint32_t)std::min<size_t>(std::max<size_t>(cap / 32, 4096), 1u << 18);
-    c->lpCap = (uint32_t)std::min<size_t>(std::max<size_t>(cap / 8, 4096), 1u << 20);
-    for (int q = 0; q < 3; ++q) {
-        if ((rc = devAlloc(c, c->wfAllocs, &c->LQ.esc[q].o, c->eCap))) return rc;
-        if ((rc = devAlloc(c, c->wfAllocs, &c->LQ.esc[q].d, c->eCap))) return rc;
-        if ((rc = devAlloc(c, c->wfAllocs, &c->LQ.esc[q].T, c->eCap))) return rc;
-    }
-    for (int q = 0; q < 2; ++q) {
-        if ((rc = devAlloc(c, c->wfAllocs, &c->LQ.lp[q].o, c->lpCap))) return rc;
-        if ((rc = devAlloc(c, c->wfAllocs, &c->LQ.lp[q].d, c->lpCap))) return rc;
-        if ((rc = devAlloc(c, c->wfAllocs, &c->LQ.lp[q].T, c->lpCap))) return rc;
-    }
+    /* grid: 8 workgroups of 256 per CU saturate the 256-CU chip; grid-stride beyond */
+    int cus = 256;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, c->device) == hipSuccess && prop.multiProcessorCount > 0) cus = prop.multiProcessorCount;
+    /* long-path ring: a power of two >= capacity / 4 (<= 1M entries, 96 B each);
+     * when it is full a path simply stays in the wavefront */
+    c->ringCap = 1u << 12;
+    while (c->ringCap < std::min<size_t>(cap / 4, 1u << 20)) c->ringCap <<= 1;
+    c->longGrid = (uint32_t)cus;        /* one worker wave per CU: up to 64 x CUs long paths at once */
+    if (const char* e = std::getenv("SURF_LONG_WAVES")) c->longGrid = (uint32_t)std::max(1, std::atoi(e));
+    float4** ring[6] = {&c->LR.o, &c->LR.d, &c->LR.T, &c->LR.so, &c->LR.sd, &c->LR.sc};
+    for (auto q : ring)
+        if ((rc = devAlloc(c, c->wfAllocs, q, c->ringCap))) return rc;
+    if ((rc = devAlloc(c, c->wfAllocs, &c->LR.seq, c->ringCap))) return rc;
+    const size_t parkSlots = (size_t)c->longGrid * 64;
+    if ((rc = devAlloc(c, c->wfAllocs, &c->LR.park.o, parkSlots))) return rc;
+    if ((rc = devAlloc(c, c->wfAllocs, &c->LR.park.d, parkSlots))) return rc;
+    if ((rc = devAlloc(c, c->wfAllocs, &c->LR.park.T, parkSlots))) return rc;
+    if ((rc = devAlloc(c, c->wfAllocs, &c->LR.parkFlag, parkSlots))) return rc;
+    SURF_CHECK(c, hipMemset(c->LR.seq, 0, (size_t)c->ringCap * sizeof(uint32_t)));
+    SURF_CHECK(c, hipMemset(c->LR.parkFlag, 0, parkSlots * sizeof(uint32_t)));
     c->survCap = (uint32_t)std::min<size_t>(std::max<size_t>(cap / 16, 4096), 1u << 18);
     for (int q = 0; q < 2; ++q) {
         if ((rc = devAlloc(c, c->wfAllocs, &c->surv[q].o, c->survCap))) return rc;
@@ -288,15 +303,10 @@ int allocWavefront(surf_ctx* c) {
         hipHostMalloc((void**)&c->hFrameDone, (size_t)kStripes * c->window * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess)
         return fail(c, SURF_ERR_OOM, "hipHostMalloc of the counter block failed");
     for (auto& e : c->pev) SURF_CHECK(c, hipEventCreate(&e));
-    /* grid: 8 workgroups of 256 per CU saturate the 256-CU chip; grid-stride beyond */
-    int cus = 256;
-    hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, c->device) == hipSuccess && prop.multiProcessorCount > 0) cus = prop.multiProcessorCount;
     const uint64_t maxBlocks = (cap + kBlock - 1) / kBlock;
     c->gridWork = (uint32_t)std::min<uint64_t>(maxBlocks, (uint64_t)cus * 8);
     c->coopMax = (uint32_t)cus * 12;
     if (const char* e = std::getenv("SURF_DRAIN_REPLAYS")) c->drainReplays = std::max(1, std::atoi(e));    /* 3 waves per SIMD of the tail kernels (launch bounds) */
-    c->longGrid = (uint32_t)cus;        /* one k_long wave per CU: the wavefront keeps the rest */
     c->gridRegen = (uint32_t)std::min<uint64_t>(maxBlocks, (uint64_t)cus * 8);
     c->allocated = true;
     return SURF_OK;
@@ -322,10 +332,10 @@ void launchPhase(surf_ctx* c, int par, hipEvent_t* ev) {
     if (ev) (void)hipEventRecord(ev[1], c->stream);
     if (c->ldsTables)
         hipLaunchKernelGGL(k_shade<true>, dim3(c->gridWork), dim3(kBlock), 0, c->stream, c->S, c->pool[par], c->pool[par ^ 1],
-                           c->hitTUV, (const uint32_t*)c->hitInst, c->Q, c->rad, c->frameDone, c->npx, c->window, c->ctr, par, c->LQ);
+                           c->hitTUV, (const uint32_t*)c->hitInst, c->Q, c->rad, c->frameDone, c->npx, c->window, c->ctr, par, c->LR);
     else
         hipLaunchKernelGGL(k_shade<false>, dim3(c->gridWork), dim3(kBlock), 0, c->stream, c->S, c->pool[par], c->pool[par ^ 1],
-                           c->hitTUV, (const uint32_t*)c->hitInst, c->Q, c->rad, c->frameDone, c->npx, c->window, c->ctr, par, c->LQ);
+                           c->hitTUV, (const uint32_t*)c->hitInst, c->Q, c->rad, c->frameDone, c->npx, c->window, c->ctr, par, c->LR);
     if (ev) (void)hipEventRecord(ev[2], c->stream);
     if (c->ldsTables)
         hipLaunchKernelGGL(k_connect<true>, dim3(c->gridWork), dim3(kBlock), lds, c->stream, c->S, c->Q, c->rad, c->ctr, par, sw);
@@ -349,19 +359,22 @@ int buildGraph(surf_ctx* c) {
 
 /* ---- sample stream ------------------------------------------------------ */
 int startStream(surf_ctx* c, uint64_t baseFrame, uint32_t maxSeg) {
+    SURF_CHECK(c, hipStreamSynchronize(c->stream2));     /* no worker of an older stream still runs */
     Counters h{};
     h.maxSeg = maxSeg;
     h.zeroCutoff = c->zeroCutoff ? 1u : 0u;
     h.baseFrame = baseFrame;
     h.survCap = c->survCap;
     h.longThresh = c->longThresh;
-    h.eCap = c->eCap;
-    h.lpCap = c->lpCap;
+    h.ringCap = c->ringCap;
     *c->hctr = h;
     SURF_CHECK(c, hipMemcpyAsync(c->ctr, c->hctr, sizeof(Counters), hipMemcpyHostToDevice, c->stream));
     SURF_CHECK(c, hipMemsetAsync(c->frameDone, 0, (size_t)kStripes * c->window * sizeof(uint32_t), c->stream));
+    /* ring sequence words restart with the entry counters (a stale seq could equal a new index + 1) */
+    SURF_CHECK(c, hipMemsetAsync(c->LR.seq, 0, (size_t)c->ringCap * sizeof(uint32_t), c->stream));
+    /* parked paths belong to the old stream, which ended drained: none remain */
     c->streamActive = true;
-    c->replay = 0;
+    c->closed = false;
     c->baseFrame = baseFrame;
     c->targetFrames = 0;
     c->accFrames = 0;
@@ -391,8 +404,8 @@ uint64_t framePaths(const surf_ctx* c, uint32_t slot) {
 }
 
 /* Event totals of the current stream: plain counters + the block stripes. */
-void streamEvents(const Counters& h, unsigned long long out[8]) {
-    for (int k = 0; k < 8; ++k) {
+void streamEvents(const Counters& h, unsigned long long out[kEvents]) {
+    for (int k = 0; k < kEvents; ++k) {
         out[k] = h.ev[k];
         for (uint32_t s = 0; s < kStripes; ++s) out[k] += h.evS[s][k];
     }
@@ -422,35 +435,7 @@ int syncAndAccumulate(surf_ctx* c) {
 
 /* One unit of forward progress: kPhasesPerGraph phases (graph replay, or
  * direct launches with per-kernel events when profiling). */
-/* k_long for replay j (j >= 1), on stream2 after graph j-1 (whose escapes it
- * consumes): lp[j%2] + esc[(j-1)%3] -> lp[(j+1)%2]. */
-int launchLong(surf_ctx* c, uint64_t j) {
-    const uint32_t in = (uint32_t)(j & 1u), es = (uint32_t)((j - 1) % 3);
-    SURF_CHECK(c, hipStreamWaitEvent(c->stream2, c->evG[(j - 1) % 3], 0));
-    SURF_CHECK(c, hipMemsetAsync(&c->ctr->lpN[in ^ 1u], 0, sizeof(uint32_t), c->stream2));
-    const size_t lds = traversalLds(c, 64);
-    if (c->ldsTables)
-        hipLaunchKernelGGL(k_long<true>, dim3(c->longGrid), dim3(64), lds, c->stream2, c->S, c->LQ, in, es, c->rad, c->frameDone,
-                           c->npx, c->window, c->ctr, stackWords(c, 64), c->longBudget);
-    else
-        hipLaunchKernelGGL(k_long<false>, dim3(c->longGrid), dim3(64), lds, c->stream2, c->S, c->LQ, in, es, c->rad, c->frameDone,
-                           c->npx, c->window, c->ctr, stackWords(c, 64), c->longBudget);
-    SURF_CHECK(c, hipGetLastError());
-    SURF_CHECK(c, hipEventRecord(c->evL[j % 3], c->stream2));
-    return SURF_OK;
-}
-
 int advance(surf_ctx* c) {
-    const uint64_t j = c->replay;
-    const bool lng = c->longThresh != 0;
-    if (lng) {
-        /* esc[j%3] is free once k_long(j-2) -- its last reader -- has finished */
-        if (j >= 2) SURF_CHECK(c, hipStreamWaitEvent(c->stream, c->evL[(j - 2) % 3], 0));
-        c->hctr->eSel = (uint32_t)(j % 3);
-        c->hctr->eN[j % 3] = 0;
-        SURF_CHECK(c, hipMemcpyAsync(&c->ctr->eSel, &c->hctr->eSel, sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
-        SURF_CHECK(c, hipMemcpyAsync(&c->ctr->eN[j % 3], &c->hctr->eN[j % 3], sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
-    }
     if (c->profiling) {
         for (int ph = 0; ph < kPhasesPerGraph; ++ph) launchPhase(c, ph & 1, &c->pev[4 * ph]);
         SURF_CHECK(c, hipGetLastError());
@@ -464,17 +449,65 @@ int advance(surf_ctx* c) {
     } else {
         SURF_CHECK(c, hipGraphLaunch(c->graphExec, c->stream));
     }
-    if (lng) {
-        SURF_CHECK(c, hipEventRecord(c->evG[j % 3], c->stream));
-        if (j >= 1) {
-            const int rc = launchLong(c, j);
-            if (rc) return rc;
-        }
-    }
-    c->replay = j + 1;
     c->stats.iterations += kPhasesPerGraph;
     if (c->stats.iterations > kMaxIterations)
         return fail(c, SURF_ERR_LIMIT, "wavefront did not drain after " + std::to_string(c->stats.iterations) + " iterations");
+    return SURF_OK;
+}
+
+/* ---- long-path worker ----------------------------------------------------
+ * k_long launches are queued on stream2, kWorkerQueue at a time, so one is
+ * always resident while the stream may escape paths; each lives
+ * longLifetime and hands its unfinished paths to the next through the park
+ * slots.  Once the ring is closed (drain), launches continue only while the
+ * last finished launch left work behind. */
+void retireWorkers(surf_ctx* c) {
+    while (c->wRetired < c->wLaunched && hipEventQuery(c->evW[c->wRetired % surf_ctx::kWorkerQueue]) == hipSuccess)
+        ++c->wRetired;
+}
+
+int launchWorker(surf_ctx* c) {
+    const size_t lds = traversalLds(c, 64);
+    if (c->ldsTables)
+        hipLaunchKernelGGL(k_long<true>, dim3(c->longGrid), dim3(64), lds, c->stream2, c->S, c->LR, c->rad, c->frameDone,
+                           c->npx, c->window, c->ctr, stackWords(c, 64), c->longLifetime);
+    else
+        hipLaunchKernelGGL(k_long<false>, dim3(c->longGrid), dim3(64), lds, c->stream2, c->S, c->LR, c->rad, c->frameDone,
+                           c->npx, c->window, c->ctr, stackWords(c, 64), c->longLifetime);
+    SURF_CHECK(c, hipGetLastError());
+    SURF_CHECK(c, hipEventRecord(c->evW[c->wLaunched % surf_ctx::kWorkerQueue], c->stream2));
+    ++c->wLaunched;
+    return SURF_OK;
+}
+
+/* Work the worker still owes, from a counter copy taken after every launch
+ * finished (hctr is then consistent with the device). */
+bool longWorkLeft(const surf_ctx* c) {
+    return c->hctr->ringHead != c->hctr->ringTail || c->hctr->parkedN != 0u;
+}
+
+int maintainWorkers(surf_ctx* c) {
+    if (!c->longThresh) return SURF_OK;
+    retireWorkers(c);
+    if (!c->closed) {
+        while (c->wLaunched - c->wRetired < (uint64_t)surf_ctx::kWorkerQueue)
+            if (int rc = launchWorker(c)) return rc;
+        return SURF_OK;
+    }
+    if (c->wLaunched != c->wRetired) return SURF_OK;
+    /* all launches done: a fresh copy of the counters says whether any is owed */
+    SURF_CHECK(c, hipMemcpyAsync(c->hctr, c->ctr, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
+    SURF_CHECK(c, hipStreamSynchronize(c->stream));
+    if (longWorkLeft(c)) return launchWorker(c);
+    return SURF_OK;
+}
+
+/* Drain: the wavefront is empty and nothing more will be issued. */
+int closeRing(surf_ctx* c) {
+    if (!c->longThresh || c->closed) return SURF_OK;
+    hipLaunchKernelGGL(k_close, dim3(1), dim3(64), 0, c->stream, c->ctr);
+    SURF_CHECK(c, hipGetLastError());
+    c->closed = true;
     return SURF_OK;
 }
 
@@ -498,42 +531,15 @@ void launchTail(surf_ctx* c, Pool in, uint32_t n, uint32_t lpw, uint32_t firstCo
  * reference's Russian-roulette survivors that run for thousands of segments),
  * the cooperative tail runs each on a whole wave, which cuts the latency of a
  * segment -- the quantity the last paths of a drain are bound by. */
-/* Drain: the long paths still held by k_long's pool and by the last replay's
- * escape queue join pool 0, so the staged tail finishes one population.  They
- * have not had their next extension ray counted (regen counts pool paths'). */
-int mergeLongPaths(surf_ctx* c) {
-    if (c->longThresh == 0 || c->replay == 0) return SURF_OK;
-    SURF_CHECK(c, hipStreamSynchronize(c->stream2));
-    SURF_CHECK(c, hipMemcpyAsync(c->hctr, c->ctr, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
-    SURF_CHECK(c, hipStreamSynchronize(c->stream));
-    const uint64_t j = c->replay;                       /* k_long(j-1) wrote lp[j%2]; esc[(j-1)%3] unconsumed */
-    const uint32_t lpIdx = (uint32_t)(j & 1u), es = (uint32_t)((j - 1) % 3);
-    const uint32_t nLp = j >= 2 ? std::min(c->hctr->lpN[lpIdx], c->lpCap) : 0u;
-    const uint32_t nE = std::min(c->hctr->eN[es], c->eCap);
-    uint32_t at = c->hctr->nIn[0];
-    if ((uint64_t)at + nLp + nE > c->capacity) return fail(c, SURF_ERR_LIMIT, "long paths exceed the pool at drain");
-    auto append = [&](const Pool& src, uint32_t n) -> int {
-        if (!n) return SURF_OK;
-        SURF_CHECK(c, hipMemcpyAsync(c->pool[0].o + at, src.o, n * sizeof(float4), hipMemcpyDeviceToDevice, c->stream));
-        SURF_CHECK(c, hipMemcpyAsync(c->pool[0].d + at, src.d, n * sizeof(float4), hipMemcpyDeviceToDevice, c->stream));
-        SURF_CHECK(c, hipMemcpyAsync(c->pool[0].T + at, src.T, n * sizeof(float4), hipMemcpyDeviceToDevice, c->stream));
-        at += n;
-        return SURF_OK;
-    };
-    int rc;
-    if ((rc = append(c->LQ.lp[lpIdx], nLp)) || (rc = append(c->LQ.esc[es], nE))) return rc;
-    c->evBase[0] += (uint64_t)nLp + nE;                 /* runTail counts their first extension as already counted */
-    c->hctr->nIn[0] = at;
-    c->hctr->lpN[0] = c->hctr->lpN[1] = 0;
-    c->hctr->eN[0] = c->hctr->eN[1] = c->hctr->eN[2] = 0;
-    SURF_CHECK(c, hipMemcpyAsync(c->ctr, c->hctr, sizeof(Counters), hipMemcpyHostToDevice, c->stream));
-    c->replay = 0;                                      /* no k_long work left; a later replay restarts the ring */
-    return SURF_OK;
+/* Cooperative drain with the lanes-as-planes wave traversal (traceWave):
+ * single-leaf TLAS, stack in one VGPR's 64 lanes (SURF_COOP_WAVE=0: the
+ * instance-parallel variant instead, for comparison). */
+bool waveEligible(const surf_ctx* c) {
+    static const bool off = [] { const char* e = std::getenv("SURF_COOP_WAVE"); return e && e[0] == '0'; }();
+    return !off && c->coopEligible && c->stackDepth <= 64;
 }
 
 int runTail(surf_ctx* c) {
-    int rc0 = mergeLongPaths(c);
-    if (rc0) return rc0;
     const uint32_t n = c->hctr->nIn[0];
     if (n == 0) return SURF_OK;
     if (c->profiling) SURF_CHECK(c, hipEventRecord(c->pev[0], c->stream));
@@ -548,10 +554,14 @@ int runTail(surf_ctx* c) {
             const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
             std::fprintf(stderr, "[surf tail] stage %d: %u paths at %.2f ms\n", stage, cnt, ms);
         }
-        if (c->coopEligible && ((c->tailBudget && cnt <= c->coopMax) || (!c->tailBudget && cnt <= c->coopAll))) {
-            const size_t lds = traversalLds(c, 64) + (size_t)stackWords(c, 64) * sizeof(float);
-            hipLaunchKernelGGL(k_tail_coop<true>, dim3(cnt), dim3(64), lds, c->stream, c->S, in, cnt, c->rad, c->frameDone,
-                               c->npx, c->window, c->ctr, stackWords(c, 64), firstCounted);
+        if (c->coopEligible && cnt <= c->coopAll) {
+            /* the wave traversal keeps no stack in LDS: only the trace tables */
+            if (waveEligible(c))
+                hipLaunchKernelGGL((k_tail_coop<true, true>), dim3(cnt), dim3(64), traversalLds(c, 64) - (size_t)stackWords(c, 64) * sizeof(uint32_t),
+                                   c->stream, c->S, in, cnt, c->rad, c->frameDone, c->npx, c->window, c->ctr, 0u, firstCounted);
+            else
+                hipLaunchKernelGGL((k_tail_coop<true, false>), dim3(cnt), dim3(64), traversalLds(c, 64) + (size_t)stackWords(c, 64) * sizeof(float),
+                                   c->stream, c->S, in, cnt, c->rad, c->frameDone, c->npx, c->window, c->ctr, stackWords(c, 64), firstCounted);
             SURF_CHECK(c, hipGetLastError());
             c->stats.tail_survivors += cnt;
             break;
@@ -578,6 +588,16 @@ int runTail(surf_ctx* c) {
         float t; (void)hipEventElapsedTime(&t, c->pev[0], c->pev[1]);
         c->stats.ms_tail += t;
     }
+#if SURF_SEG_TIMING
+    if (dbg) {
+        SURF_CHECK(c, hipMemcpyAsync(c->hctr, c->ctr, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
+        SURF_CHECK(c, hipStreamSynchronize(c->stream));
+        const unsigned long long* g = c->hctr->dbg;
+        const double ns = (double)std::max(1ull, g[3]);
+        std::fprintf(stderr, "[surf tail] coop cycles per segment: extend %.0f shade %.0f connect %.0f (%llu segments, %llu shadow)\n",
+                     g[0] / ns, g[1] / ns, g[2] / ns, g[3], g[4]);
+    }
+#endif
     /* pool 0 is now empty: the next phase starts from regen's refill */
     c->hctr->nIn[0] = 0;
     SURF_CHECK(c, hipMemcpyAsync(&c->ctr->nIn[0], &c->hctr->nIn[0], sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
@@ -595,22 +615,31 @@ int pump(surf_ctx* c, bool drain) {
     const uint64_t target = c->targetFrames * (uint64_t)c->npx;
     for (;;) {
         const uint64_t issued = c->hctr->issued[0];
-        /* k_long's paths count as in flight until the drain merges them */
-        const uint32_t inflight = c->hctr->nIn[0] + ((c->longThresh && c->replay) ? 1u : 0u);
+        const uint32_t inflight = c->hctr->nIn[0];        /* wavefront pool (the long-path worker holds the rest) */
         if (!drain && issued >= target) return SURF_OK;
         if (drain && c->accFrames >= c->targetFrames) return SURF_OK;
+        if ((rc = maintainWorkers(c))) return rc;
         const bool starved = issued >= c->pushedLimit;     /* nothing more may be issued right now */
         const uint64_t accBefore = c->accFrames;
         static const bool dbgDrain = std::getenv("SURF_DEBUG_DRAIN") != nullptr;   /* diagnostics: drain timeline */
         if (dbgDrain && starved) {
             static auto tS = std::chrono::steady_clock::now();
-            std::fprintf(stderr, "[surf drain] replay %llu: %u in flight at %.3f ms\n", (unsigned long long)c->replay, inflight,
+            std::fprintf(stderr, "[surf drain] iteration %llu: %u in flight, ring %u..%u, %llu/%llu frames at %.3f ms\n",
+                         (unsigned long long)c->stats.iterations, inflight, c->hctr->ringHead, c->hctr->ringTail,
+                         (unsigned long long)c->accFrames, (unsigned long long)c->targetFrames,
                          std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tS).count());
         }
+        bool waited = false;
         if (starved && inflight > 0 && inflight <= tailThreshold(c)) {
             if ((rc = runTail(c))) return rc;
         } else if (starved && inflight == 0) {
-            /* every issued sample finished: accumulating re-opens the window */
+            /* every wavefront path finished: accumulating re-opens the window;
+             * frames still open wait for the long-path worker */
+            if (drain && (rc = closeRing(c))) return rc;
+            if (c->wLaunched != c->wRetired) {
+                SURF_CHECK(c, hipEventSynchronize(c->evW[c->wRetired % surf_ctx::kWorkerQueue]));
+                waited = true;
+            }
         } else {
             /* draining (nothing left to issue): several replays per host poll --
              * the per-replay poll, not the kernels, is what a small pool pays */
@@ -619,7 +648,8 @@ int pump(surf_ctx* c, bool drain) {
                 if ((rc = advance(c))) return rc;
         }
         if ((rc = syncAndAccumulate(c))) return rc;
-        if (starved && inflight == 0 && c->accFrames == accBefore)
+        const bool workerOwes = c->longThresh && (!c->closed || c->wLaunched != c->wRetired || longWorkLeft(c));
+        if (starved && inflight == 0 && c->accFrames == accBefore && !waited && !workerOwes)
             return fail(c, SURF_ERR_HIP, "sample stream stalled: pool empty but frames incomplete");
     }
 }
@@ -648,9 +678,9 @@ int endStream(surf_ctx* c) {
     if (rc) return rc;
     if (c->stream2) SURF_CHECK(c, hipStreamSynchronize(c->stream2));
     if (c->streamActive) {
-        unsigned long long e[8];
+        unsigned long long e[kEvents];
         streamEvents(*c->hctr, e);
-        for (int k = 0; k < 8; ++k) c->evBase[k] += e[k];
+        for (int k = 0; k < kEvents; ++k) c->evBase[k] += e[k];
         c->segMaxBase = std::max(c->segMaxBase, c->hctr->segMax);
     }
     c->streamActive = false;
@@ -689,9 +719,7 @@ int createCtx(int dev, uint32_t w, uint32_t h, std::vector<uint32_t> rows, surf_
     c->npx = (uint32_t)(w * c->rows.size());
     bool evOk = true;
     if (hipSetDevice(dev) == hipSuccess) {
-        for (int k = 0; k < 3; ++k)
-            evOk = evOk && hipEventCreateWithFlags(&c->evG[k], hipEventDisableTiming) == hipSuccess &&
-                   hipEventCreateWithFlags(&c->evL[k], hipEventDisableTiming) == hipSuccess;
+        for (auto& e : c->evW) evOk = evOk && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
     }
     if (!evOk || hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
@@ -738,6 +766,8 @@ int surf_create_sharded(int dev, uint32_t w, uint32_t h, uint32_t shard, uint32_
 void surf_destroy(surf_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
+    /* long-path workers end within their lifetime; nothing may be freed under them */
+    if (c->stream2) (void)hipStreamSynchronize(c->stream2);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     destroyGraph(c);
     freeList(c->sceneAllocs);
@@ -752,10 +782,7 @@ void surf_destroy(surf_ctx* c) {
     if (c->stream2) (void)hipStreamSynchronize(c->stream2);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->stream2) (void)hipStreamDestroy(c->stream2);
-    for (int k = 0; k < 3; ++k) {
-        if (c->evG[k]) (void)hipEventDestroy(c->evG[k]);
-        if (c->evL[k]) (void)hipEventDestroy(c->evL[k]);
-    }
+    for (auto& e : c->evW) if (e) (void)hipEventDestroy(e);
     delete c;
 }
 
@@ -821,17 +848,16 @@ int surf_set_tail_coop(surf_ctx* c, uint32_t max_paths) {
     return SURF_OK;
 }
 
-int surf_set_long_paths(surf_ctx* c, uint32_t escape_segments, uint32_t budget) {
+int surf_set_long_paths(surf_ctx* c, uint32_t escape_segments, uint32_t lifetime_us) {
     if (!c) return fail(nullptr, SURF_ERR_INVALID, "ctx is NULL");
-    if (escape_segments != 0 && budget == 0) return fail(c, SURF_ERR_INVALID, "budget must be > 0");
     SURF_CHECK(c, hipSetDevice(c->device));
     const int rc = endStream(c);
     if (rc) return rc;
     c->longThresh = escape_segments;
-    c->longBudget = budget;
+    /* s_memrealtime ticks at 100 MHz; one launch lives at most 1 s */
+    c->longLifetime = 100ull * std::min<uint32_t>(lifetime_us ? lifetime_us : kDefaultLifetimeUs, 1000000u);
     return SURF_OK;
 }
-
 int surf_set_persistent(surf_ctx* c, int enabled) {
     if (!c) return fail(nullptr, SURF_ERR_INVALID, "ctx is NULL");
     SURF_CHECK(c, hipSetDevice(c->device));
@@ -844,8 +870,9 @@ int surf_set_persistent(surf_ctx* c, int enabled) {
 
 int surf_set_trace_mode(surf_ctx* c, int mode) {
     if (!c) return fail(nullptr, SURF_ERR_INVALID, "ctx is NULL");
-    if (mode != 0 && mode != 1) return fail(c, SURF_ERR_INVALID, "trace mode must be 0 or 1");
-    if (mode == 1 && !c->coopEligible) return fail(c, SURF_ERR_INVALID, "cooperative traversal needs a single-leaf TLAS of <= 64 instances");
+    if (mode < 0 || mode > 2) return fail(c, SURF_ERR_INVALID, "trace mode must be 0, 1 or 2");
+    if (mode >= 1 && !c->coopEligible) return fail(c, SURF_ERR_INVALID, "cooperative traversal needs a single-leaf TLAS of <= 64 instances");
+    if (mode == 2 && c->stackDepth > 64) return fail(c, SURF_ERR_INVALID, "wave traversal keeps its stack in 64 lanes: BVH too deep");
     c->traceMode = mode;
     return SURF_OK;
 }
@@ -1208,12 +1235,13 @@ int surf_get_stats(surf_ctx* c, surf_stats* out) {
     int rc = ensureDrained(c);
     if (rc) return rc;
     surf_stats s = c->stats;
-    unsigned long long ev[8];
-    unsigned long long cur[8] = {};
+    unsigned long long ev[kEvents];
+    unsigned long long cur[kEvents] = {};
     if (c->streamActive && c->hctr) streamEvents(*c->hctr, cur);
-    for (int k = 0; k < 8; ++k) ev[k] = c->evBase[k] + cur[k];
+    for (int k = 0; k < kEvents; ++k) ev[k] = c->evBase[k] + cur[k];
     s.n_ext = ev[0]; s.n_hit = ev[1]; s.n_cont = ev[2]; s.n_shadow = ev[3]; s.n_acc = ev[4]; s.n_unocc = ev[5];
     s.tail_paths = ev[6];
+    s.long_paths = ev[8];
     s.max_segments = std::max(c->segMaxBase, (c->streamActive && c->hctr) ? c->hctr->segMax : 0u);
     s.stack_depth = c->stackDepth;
     s.pool_capacity = c->capacity;
@@ -1260,7 +1288,10 @@ int surf_trace_closest(surf_ctx* c, uint32_t n, const float* o, const float* d, 
     (void)hipMemcpyAsync(dO, o, 12 * (size_t)n, hipMemcpyHostToDevice, c->stream);
     (void)hipMemcpyAsync(dD, d, 12 * (size_t)n, hipMemcpyHostToDevice, c->stream);
     if (c->traceMode == 1)
-        hipLaunchKernelGGL(k_trace_closest_coop, dim3(n), dim3(64), traversalLds(c, 64) + (size_t)stackWords(c, 64) * sizeof(float),
+        hipLaunchKernelGGL(k_trace_closest_coop<false>, dim3(n), dim3(64), traversalLds(c, 64) + (size_t)stackWords(c, 64) * sizeof(float),
+                           c->stream, c->S, (const float*)dO, (const float*)dD, n, dT, dI, stackWords(c, 64));
+    else if (c->traceMode == 2)
+        hipLaunchKernelGGL(k_trace_closest_coop<true>, dim3(n), dim3(64), traversalLds(c, 64) + (size_t)stackWords(c, 64) * sizeof(float),
                            c->stream, c->S, (const float*)dO, (const float*)dD, n, dT, dI, stackWords(c, 64));
     else if (c->ldsTables)
         hipLaunchKernelGGL(k_trace_closest<true>, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), traversalLds(c, kBlock), c->stream,
@@ -1292,8 +1323,9 @@ int surf_trace_any(surf_ctx* c, uint32_t n, const float* o, const float* d, cons
     (void)hipMemcpyAsync(dO, o, 12 * (size_t)n, hipMemcpyHostToDevice, c->stream);
     (void)hipMemcpyAsync(dD, d, 12 * (size_t)n, hipMemcpyHostToDevice, c->stream);
     (void)hipMemcpyAsync(dM, tm, 4 * (size_t)n, hipMemcpyHostToDevice, c->stream);
-    if (c->traceMode == 1)
-        hipLaunchKernelGGL(k_trace_any_coop, dim3(n), dim3(64), traversalLds(c, 64), c->stream, c->S, (const float*)dO,
+    if (c->traceMode == 1 || c->traceMode == 2)
+        hipLaunchKernelGGL(c->traceMode == 2 ? k_trace_any_coop<true> : k_trace_any_coop<false>, dim3(n), dim3(64),
+                           traversalLds(c, 64), c->stream, c->S, (const float*)dO,
                            (const float*)dD, (const float*)dM, n, dR, stackWords(c, 64));
     else if (c->ldsTables)
         hipLaunchKernelGGL(k_trace_any<true>, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), traversalLds(c, kBlock), c->stream,

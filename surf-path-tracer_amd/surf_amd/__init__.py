@@ -64,6 +64,7 @@ class Stats(C.Structure):
         ("launches_extend", C.c_uint64),
         ("stack_depth", C.c_uint32), ("pool_capacity", C.c_uint32),
         ("energy", C.c_float), ("max_segments", C.c_uint32), ("tail_survivors", C.c_uint64),
+        ("long_paths", C.c_uint64),
     ]
 
     def as_dict(self) -> dict:
@@ -327,9 +328,10 @@ class Renderer:
         """Single-stage drain as the cooperative tail when <= max_paths paths remain (0 = never)."""
         _check(load().surf_set_tail_coop(self._h, max_paths), "surf_set_tail_coop", self._h)
 
-    def set_long_paths(self, escape_segments: int = 64, budget: int = 64):
-        """Paths reaching escape_segments move to the concurrent long-path worker (0 = off)."""
-        _check(load().surf_set_long_paths(self._h, escape_segments, budget), "surf_set_long_paths", self._h)
+    def set_long_paths(self, escape_segments: int = 24, lifetime_us: int = 0):
+        """Paths reaching escape_segments move to the concurrent long-path worker (0 = off);
+        lifetime_us: life of one worker launch (0 = default)."""
+        _check(load().surf_set_long_paths(self._h, escape_segments, lifetime_us), "surf_set_long_paths", self._h)
 
     def set_persistent(self, on: bool):
         """Out-of-step (persistent) wavefront traversal on/off (identical results)."""

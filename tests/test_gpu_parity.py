@@ -30,7 +30,7 @@ def l2_report(a, b):
     return float(np.sqrt((per ** 2).mean())), float(per.max()), float((per > 1e-3).mean())
 
 
-@pytest.mark.parametrize("mode", [0, 1], ids=["lane-per-ray", "wave-per-ray"])
+@pytest.mark.parametrize("mode", [0, 1, 2], ids=["lane-per-ray", "wave-per-ray", "wave-lanes-as-planes"])
 def test_closest_hit_records_bitexact(oracle_scene, product_scene, mode):
     W = H = 96
     (eo, ed), (so, sd, st) = oracle_scene.record_rays(W, H, 0, 0, W * H)
@@ -51,7 +51,7 @@ def test_closest_hit_records_bitexact(oracle_scene, product_scene, mode):
     assert (gpu[3] != UNSET).mean() > 0.9
 
 
-@pytest.mark.parametrize("mode", [0, 1], ids=["lane-per-ray", "wave-per-ray"])
+@pytest.mark.parametrize("mode", [0, 1, 2], ids=["lane-per-ray", "wave-per-ray", "wave-lanes-as-planes"])
 def test_any_hit_bitexact(oracle_scene, product_scene, mode):
     W = H = 96
     _, (so, sd, st) = oracle_scene.record_rays(W, H, 1, 0, W * H)
@@ -119,6 +119,45 @@ def test_drain_policies_bitexact(oracle_scene, product_scene, policy):
     _assert_bitexact(g, c2, f"drain policy {policy}")
     _assert_counts(st, cnt)
     r0.close()
+
+
+@pytest.mark.parametrize("escape,lifetime_us", [(2, 0), (4, 300), (24, 0), (3, 50)],
+                         ids=["escape2", "escape4-short-life", "escape24", "escape3-park-heavy"])
+def test_long_path_worker_bitexact(oracle_scene, product_scene, escape, lifetime_us):
+    """Paths escaping the wavefront to the concurrent long-path worker (device
+    ring hand-off, shadow ray carried along, lanes parked and resumed across
+    worker launches) give the oracle's radiance and event counts bit for bit.
+    escape 2/3 pushes most paths through the ring, so it wraps many times."""
+    W, H, F = 128, 96, 6
+    r = surf_amd.Renderer(product_scene, W, H, pool_capacity=8192)
+    r.set_long_paths(escape, lifetime_us)
+    r.render(2, 0, 0)
+    r.render(F - 2, 2, 0)                 # the stream (and the worker) spans render calls
+    g = r.accumulator()
+    st = r.stats()
+    oracle.set_zero_cutoff(True)
+    try:
+        c2, cnt, _ = oracle_scene.render(W, H, F)
+    finally:
+        oracle.set_zero_cutoff(False)
+    _assert_bitexact(g, c2, f"long-path worker escape={escape}")
+    _assert_counts(st, cnt)
+    assert st["long_paths"] > 0, "no path went through the worker"
+    r.close()
+
+
+def test_long_path_worker_full_frame(oracle_scene, product_scene):
+    """1280x720 with the worker on: a band of rows against the oracle.  (Escape
+    at 6 segments: with two frames the drain tail takes over after ~12 phases.)"""
+    W, H, F = 1280, 720, 2
+    r = surf_amd.Renderer(product_scene, W, H)
+    r.set_long_paths(6, 0)
+    r.render(F, 0, 0)
+    g = r.accumulator()
+    st = r.stats()
+    c, _, _ = oracle_scene.render(W, H, F, rows=(340, 348))
+    _assert_bitexact(g[340:348], c, "1280x720 rows 340..347, worker on")
+    assert st["long_paths"] > 0
 
 
 def test_render_c1_256x256x16_bitexact(oracle_scene, product_scene):
