@@ -45,7 +45,8 @@ def parse():
     ap.add_argument("--height", type=int, default=720)
     ap.add_argument("--frames-per-step", type=int, default=16)
     ap.add_argument("--max-segments", type=int, default=0, help="0 = unbounded + RR (C3); 8 = C2")
-    ap.add_argument("--row-block", type=int, default=16)
+    ap.add_argument("--row-block", type=int, default=1,
+                    help="rows per interleaved shard block (1 spreads the long-path-heavy rows over all GPUs)")
     ap.add_argument("--scene", choices=["indoor", "c5"], default="indoor",
                     help="indoor = bundled scene (C2/C3); c5 = +648-Suzanne 10.2M-triangle lattice BLAS (C5)")
     ap.add_argument("--cpu-frames", type=int, default=48, help="frames of the CPU baseline sample (full frame)")

@@ -182,14 +182,13 @@ int surf_set_tail_policy(surf_ctx* ctx, uint32_t threshold_paths, uint32_t lanes
 int surf_set_tail_coop(surf_ctx* ctx, uint32_t max_paths);
 /* Long paths: a path whose next segment would be its `escape_segments`-th
  * leaves the wavefront (which advances a path one segment per iteration, i.e.
- * per ~4 kernel launches over the whole pool) through a device ring for a
- * worker kernel that runs concurrently on a second stream and advances each
- * of its paths one segment per loop iteration.  Worker launches are queued
- * back to back, each living `lifetime_us` (0 = 10 ms) and handing unfinished
- * paths to the next; the escaping bounce's shadow ray travels with the path,
- * so radiance is added in the reference's order.  Results do not depend on it
- * (escape_segments 0 = off).  Drains the context first. */
-int surf_set_long_paths(surf_ctx* ctx, uint32_t escape_segments, uint32_t lifetime_us);
+ * per ~4 kernel launches over the whole pool) for the long pool, which a
+ * second chain of the phase graph advances `segments_per_phase` segments per
+ * phase, beside the wavefront kernels; the escaping bounce's shadow ray
+ * travels with the path, so radiance is added in the reference's order.
+ * Results do not depend on it (escape_segments 0 = off).  Drains the context
+ * first. */
+int surf_set_long_paths(surf_ctx* ctx, uint32_t escape_segments, uint32_t segments_per_phase);
 /* Diagnostics: how many paths the segment cap ended in the current sample
  * stream, and the sample ids (frame slot * shard pixels + pixel) of the first
  * min(count, 64, max). */

@@ -101,21 +101,19 @@ struct DevCamera {
 struct Pool { float4* o; float4* d; float4* T; };
 /* Long paths (the reference's Russian roulette keeps ~0.04% of paths alive for
  * hundreds to thousands of segments): the wavefront advances a path one
- * segment per phase, so a path reaching Counters::longThresh segments leaves
- * it through this ring for k_long, a worker running concurrently on a second
- * stream that advances each of its paths one segment per iteration.  Entry i
- * lives in slot i & (cap - 1): the path record plus the shadow ray of the
- * escaping bounce, which the worker resolves first (radiance order).
- * Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility): the producer
- * writes the record with agent-scope (sc1) stores, waits for them, then
- * publishes seq[slot] = i + 1 with an agent atomic store; the consumer polls
- * seq with an agent load, then an agent acquire, then reads the record. */
-struct LongRing {
-    float4 *o, *d, *T;        /* path (Pool layout) */
-    float4 *so, *sd, *sc;     /* pending shadow ray (ShadowQ layout); sc.w = 1 when present */
-    uint32_t* seq;
-    Pool park;                /* one slot per worker lane: path held when a worker's lifetime ends */
-    uint32_t* parkFlag;
+ * segment per phase (~1.8 ms at 1280x720), so by the end of a stream tens of
+ * thousands of them are still in flight.  A path reaching Counters::longThresh
+ * segments therefore leaves the wavefront: k_shade appends it -- with the
+ * shadow ray of that bounce, resolved first so radiance is added in the
+ * reference's order -- to escape queue esc[phase % 4], and k_long, a second
+ * chain of the phase graph that runs beside the wavefront kernels, advances
+ * every long path up to Counters::longBudget segments per phase
+ * (lp[phase & 1] + esc[(phase - 1) % 4] -> lp[(phase + 1) & 1]). */
+struct EscQ { float4 *o, *d, *T, *so, *sd, *sc; };   /* path + pending shadow ray (sc.w = 1 when present) */
+struct LongPools {
+    Pool lp[2];
+    EscQ esc[4];
+    uint32_t lpCap, escCap;
 };
 /* Where a path that used up its segment budget goes. */
 struct Sink { Pool q; uint32_t* n; uint32_t cap; };
@@ -133,14 +131,12 @@ struct Counters {
     uint32_t survN;                  /* k_tail survivors appended (may exceed survCap) */
     uint32_t survCap;
     uint32_t longThresh;             /* a continuation with this many segments escapes the wavefront (0 = off) */
-    uint32_t ringCap;                /* long-path ring slots (power of two) */
-    /* ring words each on a 128-B line of their own: the workers poll them, and
-     * must not share a line with the wavefront's per-block atomics above */
-    alignas(128) uint32_t ringTail;  /* entries reserved by k_shade (agent atomics, mod 2^32) */
-    alignas(128) uint32_t ringHead;  /* entries claimed by k_long */
-    alignas(128) uint32_t closing;   /* set by k_close: the wavefront will escape no more paths */
-    uint32_t parkedN;                /* worker lanes holding a parked path */
-    alignas(128) uint32_t _pad2;
+    uint32_t longBudget;             /* segments per long path per k_long step */
+    uint32_t lpN[2];                 /* long pools (k_long appends; may exceed lpCap only by refusal) */
+    uint32_t escN[4];                /* escape queues (k_shade appends) */
+    uint32_t lpDone;                 /* k_long blocks finished (last one resets its inputs' counts) */
+    uint32_t longPop;                /* long paths in flight (escaped, not finished) <= lpCap */
+    uint32_t _pad2[2];
     unsigned long long issued[2];    /* stream samples issued, per parity */
     unsigned long long limit;        /* host-written issue limit (frame window) */
     unsigned long long baseFrame;    /* absolute frame index of stream frame 0 */
@@ -1129,54 +1125,42 @@ __device__ __forceinline__ void shadePath(const DevScene& S, const ShadeTables& 
     }
 }
 
-/* ---------------------------------------------------------- long-path ring
- * Agent-scope (sc1) stores: the bytes leave the XCD's L2 for the coherent
- * fabric, so a k_long wave on another XCD reads them after its acquire. */
-__device__ __forceinline__ void stAgent(float4* p, float4 v) {
-    uint32_t* q = reinterpret_cast<uint32_t*>(p);
-    __hip_atomic_store(q + 0, __float_as_uint(v.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(q + 1, __float_as_uint(v.y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(q + 2, __float_as_uint(v.z), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(q + 3, __float_as_uint(v.w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 __device__ __forceinline__ uint32_t ldAgent(const uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+/* Path-count bound of the long pools: k_shade reserves population before it
+ * escapes a path (the rest of the wave's candidates stay in the wavefront). */
+__device__ __forceinline__ uint32_t reserveLong(Counters* C, uint32_t want, uint32_t cap) {
+    const uint32_t old = atomicAdd(&C->longPop, want);
+    const uint32_t room = old >= cap ? 0u : cap - old;
+    const uint32_t got = want < room ? want : room;
+    if (got < want) atomicSub(&C->longPop, want - got);
+    return got;
+}
 
-/* Wave-level escape (every lane of the wave calls it): reserves ring entries
- * for the lanes with `want` set -- as many as fit, the rest stay in the
- * wavefront -- and publishes their path + pending shadow ray.  Returns whether
- * this lane's path left. */
+/* ---------------------------------------------------------- long-path escape
+ * Wave-level append of the lanes with `want` set to escape queue q (one
+ * atomic per wave); lanes beyond the queue's capacity stay in the wavefront.
+ * Every lane of the wave calls it.  Returns whether this lane's path left. */
 template <class ShadeOutT>
-__device__ __forceinline__ bool escapeLong(Counters* C, const LongRing& LR, bool want, const ShadeOutT& r) {
+__device__ __forceinline__ bool escapeLong(Counters* C, const LongPools& LP, uint32_t q, bool want, const ShadeOutT& r) {
     const unsigned long long m = __ballot(want);
     if (!m) return false;
-    uint32_t base = 0, n = 0;
+    uint32_t base = 0, got = 0;
     if (laneId() == 0) {
-        const uint32_t need = (uint32_t)__popcll(m), cap = C->ringCap;
-        uint32_t t = ldAgent(&C->ringTail);
-        for (;;) {
-            /* head only grows, so a stale head under-estimates the room */
-            const uint32_t room = cap - (t - ldAgent(&C->ringHead));
-            n = need < room ? need : room;
-            if (n == 0u) break;
-            const uint32_t prev = atomicCAS(&C->ringTail, t, t + n);
-            if (prev == t) { base = t; break; }
-            t = prev;
-        }
+        got = reserveLong(C, (uint32_t)__popcll(m), LP.lpCap);
+        if (got) base = atomicAdd(&C->escN[q], got);
     }
     base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
-    n = (uint32_t)__builtin_amdgcn_readfirstlane((int)n);
+    got = (uint32_t)__builtin_amdgcn_readfirstlane((int)got);
     const uint32_t rank = rankBelow(m);
-    const bool esc = want && rank < n;
-    const uint32_t i = base + rank, k = i & (C->ringCap - 1u);
+    const uint32_t k = base + rank;
+    const bool esc = want && rank < got;        /* escCap == lpCap >= population: k < escCap */
     if (esc) {
-        stAgent(&LR.o[k], r.o); stAgent(&LR.d[k], r.d); stAgent(&LR.T[k], r.T);
-        stAgent(&LR.so[k], r.so); stAgent(&LR.sd[k], r.sd);
-        stAgent(&LR.sc[k], make_float4(r.sc.x, r.sc.y, r.sc.z, r.shadow ? 1.0f : 0.0f));
+        const EscQ& E = LP.esc[q];
+        E.o[k] = r.o; E.d[k] = r.d; E.T[k] = r.T; E.so[k] = r.so; E.sd[k] = r.sd;
+        E.sc[k] = make_float4(r.sc.x, r.sc.y, r.sc.z, r.shadow ? 1.0f : 0.0f);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (esc) __hip_atomic_store(&LR.seq[k], i + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return esc;
 }
 
@@ -1197,7 +1181,7 @@ template <bool LDS_TABLES>
 __global__ __launch_bounds__(kBlock, SURF_SHADE_WAVES) void k_shade(DevScene S, Pool cur, Pool nxt, const float4* __restrict__ hitTUV,
                                                   const uint32_t* __restrict__ hitInst, ShadowQ Q,
                                                   float4* __restrict__ rad, uint32_t* __restrict__ frameDone,
-                                                  uint32_t npx, uint32_t window, Counters* C, int par, LongRing LR) {
+                                                  uint32_t npx, uint32_t window, Counters* C, int par, LongPools LP, uint32_t escQ) {
     if (blockIdx.x * blockDim.x >= C->nIn[par]) return;     /* nothing to shade in this block */
     __shared__ DevInstance sInst[LDS_TABLES ? kLdsInst : 1];
     __shared__ DevMaterial sMat[LDS_TABLES ? kLdsMats : 1];
@@ -1232,7 +1216,7 @@ __global__ __launch_bounds__(kBlock, SURF_SHADE_WAVES) void k_shade(DevScene S, 
         }
         /* a path reaching longThresh segments leaves for the k_long worker,
          * taking this bounce's shadow ray with it */
-        const bool esc = longThresh != 0u && escapeLong(C, LR, r.cont && r.seg + 1u >= longThresh, r);
+        const bool esc = longThresh != 0u && escapeLong(C, LP, escQ, r.cont && r.seg + 1u >= longThresh, r);
         const unsigned long long mCont = __ballot(r.cont && !esc), mSh = __ballot(r.shadow && !esc);
         if (laneId() == 0) { sWave[it][wv][0] = (uint32_t)__popcll(mCont); sWave[it][wv][1] = (uint32_t)__popcll(mSh); }
         __syncthreads();
@@ -1465,161 +1449,129 @@ __device__ __forceinline__ void addRadianceAtomic(float4* rad, uint32_t sid, V3 
     addExact(r + 0, c.x); addExact(r + 1, c.y); addExact(r + 2, c.z);
 }
 
-/* Long-path worker (stream 2, concurrent with the wavefront's graph replays):
- * every lane owns at most one path and advances it one segment per iteration
- * -- extend, shade, shadow ray, the wavefront kernels' device functions --
- * instead of one segment per wavefront phase.  An idle lane claims the next
- * published ring entry (resolving the escaping bounce's shadow ray first).
- * The launch lives `lifetime` ticks of the 100 MHz clock: then each lane parks
- * its path in its park slot (the next launch, same grid, resumes it) and the
- * wave exits; a wave also exits when the host has closed the ring and it is
- * empty.  No wave ever waits on another, so every launch ends. */
+/* Long-path step (the second chain of the phase graph, running beside the
+ * wavefront kernels): every path of lp[in] and of escape queue eq advances up
+ * to Counters::longBudget segments in its lane (extend -> shade -> shadow ray,
+ * the wavefront kernels' device functions); paths still alive are appended to
+ * lp[in ^ 1].  An escaped path first resolves the shadow ray of the bounce it
+ * escaped on.  Radiance adds are compare-and-swap (this kernel runs beside
+ * wavefront kernels that write other samples of the same cache lines).  The
+ * last block to finish resets the counts of the queues it consumed. */
 template <bool LDS_TABLES>
-__global__ __launch_bounds__(64, 2) void k_long(DevScene S, LongRing LR, float4* __restrict__ rad,
-                                             uint32_t* __restrict__ frameDone, uint32_t npx, uint32_t window, Counters* C,
-                                             uint32_t stackWords, unsigned long long lifetime) {
+__global__ __launch_bounds__(kBlock, 2) void k_long(DevScene S, LongPools LP, float4* __restrict__ rad,
+                                                 uint32_t* __restrict__ frameDone, uint32_t npx, uint32_t window,
+                                                 Counters* C, uint32_t in, uint32_t eq, uint32_t stackWords) {
     extern __shared__ uint32_t lds[];
-    const TraceTables Tt = traceTables<LDS_TABLES>(S, lds, stackWords);
     __shared__ DevInstance sInst[LDS_TABLES ? kLdsInst : 1];
     __shared__ DevMaterial sMat[LDS_TABLES ? kLdsMats : 1];
     __shared__ uint2 sLights[LDS_TABLES ? kLdsLights : 1];
-    ShadeTables Tb{S.inst, S.mats, S.lights};
-    if (LDS_TABLES) {
-        stageTables(S, sInst, sMat, sLights);
-        Tb = ShadeTables{sInst, sMat, sLights};
-    }
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    const uint32_t lane = threadIdx.x, gl = blockIdx.x * 64u + lane;
-    uint32_t* stk = lds + threadIdx.x;
-    const uint32_t stride = blockDim.x;
-    const uint32_t maxSeg = C->maxSeg, zeroCutoff = C->zeroCutoff, mask = C->ringCap - 1u;
-    unsigned long long* ev = C->evS[blockIdx.x % kStripes];
-    uint32_t* fd = frameDone + (blockIdx.x % kStripes) * window;
-    /* lane state: the path and its event counts since it was claimed / resumed */
-    bool active = LR.parkFlag[gl] != 0u;      /* written by the previous launch (stream order) */
-    float4 o4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), d4 = o4, T4 = o4, so = o4, sd = o4, sc = o4;
-    if (active) { o4 = LR.park.o[gl]; d4 = LR.park.d[gl]; T4 = LR.park.T[gl]; LR.parkFlag[gl] = 0u; }
-    {
-        const unsigned long long m = __ballot(active);
-        if (lane == 0 && m) atomicSub(&C->parkedN, (uint32_t)__popcll(m));
-    }
-    uint32_t nExt = 0, nHit = 0, nCont = 0, nSh = 0, nAcc = 0, nUn = 0;
-    bool pend = false;
-    for (;;) {
-        if (__builtin_amdgcn_s_memrealtime() - t0 > lifetime) break;
-        /* ---- claim: idle lanes take the next published entries, in order */
-        const unsigned long long idle = __ballot(!active);
-        if (idle) {
-            uint32_t h = 0, t = 0;
-            if (lane == 0) { h = ldAgent(&C->ringHead); t = ldAgent(&C->ringTail); }
-            h = (uint32_t)__builtin_amdgcn_readfirstlane((int)h);
-            t = (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
-            const uint32_t nIdle = (uint32_t)__popcll(idle);
-            const uint32_t avail = (t - h) < nIdle ? (t - h) : nIdle;
-            if (avail) {
-                const uint32_t rank = rankBelow(idle);
-                const bool want = !active && rank < avail;
-                const bool pub = want && ldAgent(&LR.seq[(h + rank) & mask]) == h + rank + 1u;
-                const unsigned long long notPub = __ballot(want && !pub);
-                const uint32_t n = notPub ? (uint32_t)__popcll(idle & ((notPub & (~notPub + 1ull)) - 1ull)) : avail;
-                if (n) {
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                    const bool take = want && rank < n;
-                    float4 a0 = o4, a1 = d4, a2 = T4, a3 = so, a4 = sd, a5 = sc;
-                    if (take) {
-                        const uint32_t k = (h + rank) & mask;
-                        a0 = LR.o[k]; a1 = LR.d[k]; a2 = LR.T[k]; a3 = LR.so[k]; a4 = LR.sd[k]; a5 = LR.sc[k];
-                    }
-                    /* the entries are read before the head moves past them: a
-                     * producer reuses slot k only once head > index */
-                    uint32_t ok = 0;
-                    if (lane == 0) ok = atomicCAS(&C->ringHead, h, h + n) == h ? 1u : 0u;
-                    ok = (uint32_t)__builtin_amdgcn_readfirstlane((int)ok);
-                    if (ok && take) {
-                        active = true;
-                        o4 = a0; d4 = a1; T4 = a2; so = a3; sd = a4; sc = a5;
-                        pend = a5.w != 0.0f;
+    const uint32_t nL = min(C->lpN[in], LP.lpCap), nE = min(C->escN[eq], LP.escCap), n = nL + nE;
+    if (blockIdx.x * blockDim.x < n) {
+        __builtin_amdgcn_s_setprio(2);     /* latency work beside the wavefront's throughput kernels */
+        const TraceTables Tt = traceTables<LDS_TABLES>(S, lds, stackWords);
+        ShadeTables Tb{S.inst, S.mats, S.lights};
+        if (LDS_TABLES) {
+            stageTables(S, sInst, sMat, sLights);
+            Tb = ShadeTables{sInst, sMat, sLights};
+        }
+        uint32_t* stk = lds + threadIdx.x;
+        const uint32_t stride = blockDim.x;
+        const uint32_t maxSeg = C->maxSeg, zeroCutoff = C->zeroCutoff, budget = C->longBudget;
+        const Pool src = LP.lp[in], dst = LP.lp[in ^ 1u];
+        const EscQ E = LP.esc[eq];
+        uint32_t* fd = frameDone + (blockIdx.x % kStripes) * window;
+        unsigned long long cExt = 0, cHit = 0, cCont = 0, cSh = 0, cAcc = 0, cUn = 0, cFin = 0;
+        for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
+            const uint32_t v = base + threadIdx.x;
+            const bool active = v < n;
+            float4 o4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), d4 = o4, T4 = o4;
+            bool alive = false;
+            uint32_t nExt = 0, nHit = 0, nCont = 0, nSh = 0, nAcc = 0, nUn = 0;
+            if (active) {
+                alive = true;
+                if (v < nL) {
+                    o4 = src.o[v]; d4 = src.d[v]; T4 = src.T[v];
+                } else {
+                    const uint32_t k = v - nL;
+                    o4 = E.o[k]; d4 = E.d[k]; T4 = E.T[k];
+                    const float4 sc = E.sc[k];
+                    if (sc.w != 0.0f) {
+                        /* the escaping bounce's shadow ray (n_shadow counted by k_shade) */
+                        const float4 so = E.so[k], sd = E.sd[k];
+                        float sdep = so.w, su = 0.0f, sv = 0.0f;
+                        uint32_t si = kUnset, sp = kUnset;
+                        if (!traceScene<true>(S, Tt, xyz(so), xyz(sd), sdep, su, sv, si, sp, stk, stride)) {
+                            addRadianceAtomic(rad, f2u(sd.w), xyz(sc));
+                            ++nUn; ++nAcc;
+                        }
                     }
                 }
+                for (uint32_t sgm = 0; sgm < budget; ++sgm) {
+                    float depth = kFarAway, u = 0.0f, vv = 0.0f;
+                    uint32_t inst = kUnset, prim = kUnset;
+                    const bool hit = traceScene<false>(S, Tt, xyz(o4), xyz(d4), depth, u, vv, inst, prim, stk, stride);
+                    ++nExt;
+                    ShadeOut r;
+                    shadePath(S, Tb, o4, d4, T4, make_float4(depth, u, vv, u2f(prim)), hit ? inst : kUnset, maxSeg, zeroCutoff, r);
+                    if (r.addRad) addRadianceAtomic(rad, f2u(o4.w), r.radd);
+                    nHit += r.hitGeom; nAcc += r.accd;
+                    if (r.shadow) {
+                        ++nSh;
+                        float sdep = r.so.w, su = 0.0f, sv = 0.0f;
+                        uint32_t si = kUnset, sp = kUnset;
+                        if (!traceScene<true>(S, Tt, xyz(r.so), xyz(r.sd), sdep, su, sv, si, sp, stk, stride)) {
+                            addRadianceAtomic(rad, f2u(r.sd.w), xyz(r.sc));
+                            ++nUn; ++nAcc;
+                        }
+                    }
+                    if (r.capped) {
+                        const unsigned long long kc = atomicAdd(&C->ev[7], 1ull);
+                        if (kc < 64) C->capped[kc] = f2u(o4.w);
+                    }
+                    if (!r.cont) {
+                        atomicMax(&C->segMax, r.seg);
+                        alive = false;
+                        break;
+                    }
+                    ++nCont;
+                    o4 = r.o; d4 = r.d; T4 = r.T;
+                }
             }
-        }
-        if (!__ballot(active)) {
-            uint32_t done = 0;
-            if (lane == 0) done = ldAgent(&C->closing) && ldAgent(&C->ringHead) == ldAgent(&C->ringTail);
-            if (__builtin_amdgcn_readfirstlane((int)done)) break;
-            /* idle: normal priority, poll every ~8k cycles */
-            __builtin_amdgcn_s_setprio(0);
-            __builtin_amdgcn_s_sleep(127);
-            continue;
-        }
-        /* a wave with paths runs at the highest issue priority: the SIMD's
-         * wavefront waves (throughput work) take the cycles it leaves, so a
-         * long path's segment latency stays near the unloaded latency */
-        __builtin_amdgcn_s_setprio(3);
-        if (!active) continue;
-        /* ---- one segment of each active lane's path */
-        if (pend) {
-            /* the escaping bounce's shadow ray (its n_shadow was counted by k_shade) */
-            pend = false;
-            float sdep = so.w, su = 0.0f, sv = 0.0f;
-            uint32_t si = kUnset, sp = kUnset;
-            if (!traceScene<true>(S, Tt, xyz(so), xyz(sd), sdep, su, sv, si, sp, stk, stride)) {
-                addRadianceAtomic(rad, f2u(sd.w), xyz(sc));
-                ++nUn; ++nAcc;
+            /* survivors to the other long pool (one atomic per wave; the
+             * population is bounded by lpCap where k_shade escapes) */
+            const unsigned long long mA = __ballot(alive);
+            if (mA) {
+                const uint32_t j = waveAppend(&C->lpN[in ^ 1u], mA);
+                if (alive) { dst.o[j] = o4; dst.d[j] = d4; dst.T[j] = T4; }
             }
+            const bool fin = active && !alive;
+            frameDoneAdd(fd, fin, f2u(o4.w) / npx);
+            const unsigned long long mF = __ballot(fin);
+            if (laneId() == 0 && mF) atomicSub(&C->longPop, (uint32_t)__popcll(mF));
+            cExt += nExt; cHit += nHit; cCont += nCont; cSh += nSh; cAcc += nAcc; cUn += nUn; cFin += fin;
         }
-        float depth = kFarAway, u = 0.0f, v = 0.0f;
-        uint32_t inst = kUnset, prim = kUnset;
-        const bool hit = traceScene<false>(S, Tt, xyz(o4), xyz(d4), depth, u, v, inst, prim, stk, stride);
-        ++nExt;
-        ShadeOut r;
-        shadePath(S, Tb, o4, d4, T4, make_float4(depth, u, v, u2f(prim)), hit ? inst : kUnset, maxSeg, zeroCutoff, r);
-        if (r.addRad) addRadianceAtomic(rad, f2u(o4.w), r.radd);
-        nHit += r.hitGeom; nAcc += r.accd;
-        if (r.shadow) {
-            ++nSh;
-            float sdep = r.so.w, su = 0.0f, sv = 0.0f;
-            uint32_t si = kUnset, sp = kUnset;
-            if (!traceScene<true>(S, Tt, xyz(r.so), xyz(r.sd), sdep, su, sv, si, sp, stk, stride)) {
-                addRadianceAtomic(rad, f2u(r.sd.w), xyz(r.sc));
-                ++nUn; ++nAcc;
-            }
+        /* per-lane totals -> one atomic per counter per wave */
+        unsigned long long* ev = C->evS[blockIdx.x % kStripes];
+        const unsigned long long vals[7] = {cExt, cHit, cCont, cSh, cAcc, cUn, cFin};
+        const int idx[7] = {0, 1, 2, 3, 4, 5, 8};
+#pragma unroll
+        for (int q = 0; q < 7; ++q) {
+            unsigned long long t = vals[q];
+            for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off);
+            if (laneId() == 0 && t) atomicAdd(&ev[idx[q]], t);
         }
-        if (r.capped) {
-            const unsigned long long k = atomicAdd(&C->ev[7], 1ull);
-            if (k < 64) C->capped[k] = f2u(o4.w);
-        }
-        if (r.cont) {
-            ++nCont;
-            o4 = r.o; d4 = r.d; T4 = r.T;
-            continue;
-        }
-        /* path finished: its radiance adds have returned, so completion follows them */
-        atomicMax(&C->segMax, r.seg);
-        atomicAdd(&fd[f2u(o4.w) / npx], 1u);
-        atomicAdd(&ev[0], (unsigned long long)nExt); atomicAdd(&ev[1], (unsigned long long)nHit);
-        atomicAdd(&ev[2], (unsigned long long)nCont); atomicAdd(&ev[3], (unsigned long long)nSh);
-        atomicAdd(&ev[4], (unsigned long long)nAcc); atomicAdd(&ev[5], (unsigned long long)nUn);
-        atomicAdd(&ev[8], 1ull);
-        nExt = nHit = nCont = nSh = nAcc = nUn = 0;
-        active = false;
     }
-    /* lifetime over (or ring closed and empty): park what is still running */
-    if (active) {
-        LR.park.o[gl] = o4; LR.park.d[gl] = d4; LR.park.T[gl] = T4;
-        LR.parkFlag[gl] = 1u;
-        atomicAdd(&ev[0], (unsigned long long)nExt); atomicAdd(&ev[1], (unsigned long long)nHit);
-        atomicAdd(&ev[2], (unsigned long long)nCont); atomicAdd(&ev[3], (unsigned long long)nSh);
-        atomicAdd(&ev[4], (unsigned long long)nAcc); atomicAdd(&ev[5], (unsigned long long)nUn);
+    /* last block out resets the consumed queues' counts (k_long(ph + 1) and
+     * k_shade(ph + 3) come after this launch in the graph) */
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        if (atomicAdd(&C->lpDone, 1u) == gridDim.x - 1u) {
+            atomicExch(&C->lpN[in], 0u);
+            atomicExch(&C->escN[eq], 0u);
+            atomicExch(&C->lpDone, 0u);
+        }
     }
-    const unsigned long long m = __ballot(active);
-    if (lane == 0 && m) atomicAdd(&C->parkedN, (uint32_t)__popcll(m));
-}
-
-/* Closes the long-path ring for the rest of the stream (no k_shade will run
- * before the next stream): idle workers may exit once it is empty. */
-__global__ void k_close(Counters* C) {
-    if (threadIdx.x == 0) __hip_atomic_store(&C->closing, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 /* Cooperative tail: one path per 64-lane wave (block), for the few very long

@@ -32,7 +32,6 @@ namespace {
 constexpr int kPhasesPerGraph = 8;          /* even: parity returns to 0 after a replay */
 constexpr uint32_t kMaxStack = 120;          /* LDS stack entries per ray (block 256 -> 120 KiB max) */
 constexpr uint64_t kMaxIterations = 1ull << 22;  /* safety net: a path longer than this is a bug */
-constexpr uint32_t kDefaultLifetimeUs = 10000;   /* k_long launch lifetime */
 
 std::mutex gErrMutex;
 std::string gLastError;
@@ -109,17 +108,12 @@ struct surf_ctx {
     bool coopEligible = false;     /* single-leaf TLAS of <= 64 instances, LDS tables */
     int traceMode = 0;             /* surf_trace_closest/_any: 0 one ray per lane, 1 one ray per wave */
     bool persistent = false;       /* out-of-step lanes with per-wave ray ranges: measured 4x slower */
-    /* long paths: ring + k_long worker launches on stream2 (surf_set_long_paths) */
+    /* long paths: escape queues + long pools, advanced by the k_long chain of the graph (surf_set_long_paths) */
     uint32_t longThresh = 0;       /* escape length (0 = off) */
-    unsigned long long longLifetime = 0;   /* worker launch lifetime, 100 MHz ticks */
-    uint32_t longGrid = 0;         /* k_long waves (64 lanes each) */
-    uint32_t ringCap = 0;
-    hipStream_t stream2 = nullptr;
-    static constexpr int kWorkerQueue = 2;   /* worker launches kept queued on stream2 */
-    hipEvent_t evW[kWorkerQueue] = {};
-    uint64_t wLaunched = 0, wRetired = 0;    /* worker launches of this context */
-    bool closed = false;           /* k_close issued for the current stream */
-    LongRing LR{};
+    uint32_t longBudget = 8;       /* segments per long path per phase */
+    hipStream_t stream2 = nullptr; /* the k_long branch while the graph is captured */
+    hipEvent_t evFork = nullptr, evShade[kPhasesPerGraph] = {}, evLong[kPhasesPerGraph] = {};
+    LongPools LP{};
     uint32_t tailLanes = 0;
     uint32_t segMaxBase = 0;       /* longest path of finished streams */
 
@@ -267,23 +261,20 @@ int allocWavefront(surf_ctx* c) {
     int cus = 256;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, c->device) == hipSuccess && prop.multiProcessorCount > 0) cus = prop.multiProcessorCount;
-    /* long-path ring: a power of two >= capacity / 4 (<= 1M entries, 96 B each);
-     * when it is full a path simply stays in the wavefront */
-    c->ringCap = 1u << 12;
-    while (c->ringCap < std::min<size_t>(cap / 4, 1u << 20)) c->ringCap <<= 1;
-    c->longGrid = (uint32_t)cus;        /* one worker wave per CU: up to 64 x CUs long paths at once */
-    if (const char* e = std::getenv("SURF_LONG_WAVES")) c->longGrid = (uint32_t)std::max(1, std::atoi(e));
-    float4** ring[6] = {&c->LR.o, &c->LR.d, &c->LR.T, &c->LR.so, &c->LR.sd, &c->LR.sc};
-    for (auto q : ring)
-        if ((rc = devAlloc(c, c->wfAllocs, q, c->ringCap))) return rc;
-    if ((rc = devAlloc(c, c->wfAllocs, &c->LR.seq, c->ringCap))) return rc;
-    const size_t parkSlots = (size_t)c->longGrid * 64;
-    if ((rc = devAlloc(c, c->wfAllocs, &c->LR.park.o, parkSlots))) return rc;
-    if ((rc = devAlloc(c, c->wfAllocs, &c->LR.park.d, parkSlots))) return rc;
-    if ((rc = devAlloc(c, c->wfAllocs, &c->LR.park.T, parkSlots))) return rc;
-    if ((rc = devAlloc(c, c->wfAllocs, &c->LR.parkFlag, parkSlots))) return rc;
-    SURF_CHECK(c, hipMemset(c->LR.seq, 0, (size_t)c->ringCap * sizeof(uint32_t)));
-    SURF_CHECK(c, hipMemset(c->LR.parkFlag, 0, parkSlots * sizeof(uint32_t)));
+    /* long pools: the population of escaped paths is bounded by lpCap (k_shade
+     * reserves it), so each escape queue (one phase's escapes) fits in lpCap too */
+    c->LP.lpCap = c->LP.escCap = (uint32_t)std::min<size_t>(std::max<size_t>(cap / 4, 65536), 1u << 20);
+    for (int q = 0; q < 2; ++q) {
+        if ((rc = devAlloc(c, c->wfAllocs, &c->LP.lp[q].o, c->LP.lpCap))) return rc;
+        if ((rc = devAlloc(c, c->wfAllocs, &c->LP.lp[q].d, c->LP.lpCap))) return rc;
+        if ((rc = devAlloc(c, c->wfAllocs, &c->LP.lp[q].T, c->LP.lpCap))) return rc;
+    }
+    for (int q = 0; q < 4; ++q) {
+        float4** f[6] = {&c->LP.esc[q].o, &c->LP.esc[q].d, &c->LP.esc[q].T, &c->LP.esc[q].so, &c->LP.esc[q].sd, &c->LP.esc[q].sc};
+        for (auto x : f)
+            if ((rc = devAlloc(c, c->wfAllocs, x, c->LP.escCap))) return rc;
+    }
+    /* drain stages: survivors of a tail stage, ping-pong */
     c->survCap = (uint32_t)std::min<size_t>(std::max<size_t>(cap / 16, 4096), 1u << 18);
     for (int q = 0; q < 2; ++q) {
         if ((rc = devAlloc(c, c->wfAllocs, &c->surv[q].o, c->survCap))) return rc;
@@ -314,11 +305,31 @@ int allocWavefront(surf_ctx* c) {
 
 StreamGeom geom(const surf_ctx* c) { return StreamGeom{c->dRows, c->width, c->npx, c->window}; }
 
-/* One wavefront phase: extend -> shade -> connect -> regen.  With ev != null,
- * an event is recorded before each kernel and after the last (profiling). */
-void launchPhase(surf_ctx* c, int par, hipEvent_t* ev) {
+/* k_long for phase ph: lp[ph & 1] + esc[(ph - 1) % 4] -> lp[(ph + 1) & 1]. */
+void launchLong(surf_ctx* c, int ph, hipStream_t st) {
+    const uint32_t in = (uint32_t)ph & 1u, eq = ((uint32_t)ph + 3u) & 3u;
+    const size_t lds = traversalLds(c, kBlock);
+    if (c->ldsTables)
+        hipLaunchKernelGGL(k_long<true>, dim3(c->gridWork), dim3(kBlock), lds, st, c->S, c->LP, c->rad, c->frameDone, c->npx,
+                           c->window, c->ctr, in, eq, stackWords(c, kBlock));
+    else
+        hipLaunchKernelGGL(k_long<false>, dim3(c->gridWork), dim3(kBlock), lds, st, c->S, c->LP, c->rad, c->frameDone, c->npx,
+                           c->window, c->ctr, in, eq, stackWords(c, kBlock));
+}
+
+/* One wavefront phase (ph = 0..kPhasesPerGraph-1): extend -> shade -> connect
+ * -> regen, plus -- when long paths escape -- that phase's k_long step.
+ * Captured (graph): k_long(ph + 1) runs on stream2 after shade(ph), beside the
+ * rest of the chain; shade(ph) waits for k_long(ph - 3), the last reader of
+ * the escape queue it refills.  Direct launches (profiling): k_long(ph) runs
+ * first, in stream order.  With ev != null, an event is recorded before each
+ * wavefront kernel and after the last. */
+void launchPhase(surf_ctx* c, int ph, hipEvent_t* ev, bool capture) {
+    const int par = ph & 1;
     const size_t lds = traversalLds(c, kBlock);
     const uint32_t sw = stackWords(c, kBlock);
+    const bool lng = c->longThresh != 0;
+    if (lng && !capture) launchLong(c, ph, c->stream);
     if (ev) (void)hipEventRecord(ev[0], c->stream);
     if (c->persistent && c->ldsTables && c->S.tlasLeafCount > 0)
         hipLaunchKernelGGL(k_extend_p<true>, dim3(c->gridWork), dim3(kBlock), lds, c->stream, c->S, c->pool[par], c->hitTUV,
@@ -330,12 +341,22 @@ void launchPhase(surf_ctx* c, int par, hipEvent_t* ev) {
         hipLaunchKernelGGL(k_extend<false>, dim3(c->gridWork), dim3(kBlock), lds, c->stream, c->S, c->pool[par], c->hitTUV,
                            c->hitInst, (const Counters*)c->ctr, par, sw);
     if (ev) (void)hipEventRecord(ev[1], c->stream);
+    if (lng && capture && ph >= 3) (void)hipStreamWaitEvent(c->stream, c->evLong[ph - 3], 0);
+    const uint32_t escQ = (uint32_t)ph & 3u;
     if (c->ldsTables)
         hipLaunchKernelGGL(k_shade<true>, dim3(c->gridWork), dim3(kBlock), 0, c->stream, c->S, c->pool[par], c->pool[par ^ 1],
-                           c->hitTUV, (const uint32_t*)c->hitInst, c->Q, c->rad, c->frameDone, c->npx, c->window, c->ctr, par, c->LR);
+                           c->hitTUV, (const uint32_t*)c->hitInst, c->Q, c->rad, c->frameDone, c->npx, c->window, c->ctr, par,
+                           c->LP, escQ);
     else
         hipLaunchKernelGGL(k_shade<false>, dim3(c->gridWork), dim3(kBlock), 0, c->stream, c->S, c->pool[par], c->pool[par ^ 1],
-                           c->hitTUV, (const uint32_t*)c->hitInst, c->Q, c->rad, c->frameDone, c->npx, c->window, c->ctr, par, c->LR);
+                           c->hitTUV, (const uint32_t*)c->hitInst, c->Q, c->rad, c->frameDone, c->npx, c->window, c->ctr, par,
+                           c->LP, escQ);
+    if (lng && capture && ph + 1 < kPhasesPerGraph) {
+        (void)hipEventRecord(c->evShade[ph], c->stream);
+        (void)hipStreamWaitEvent(c->stream2, c->evShade[ph], 0);
+        launchLong(c, ph + 1, c->stream2);
+        (void)hipEventRecord(c->evLong[ph + 1], c->stream2);
+    }
     if (ev) (void)hipEventRecord(ev[2], c->stream);
     if (c->ldsTables)
         hipLaunchKernelGGL(k_connect<true>, dim3(c->gridWork), dim3(kBlock), lds, c->stream, c->S, c->Q, c->rad, c->ctr, par, sw);
@@ -349,8 +370,18 @@ void launchPhase(surf_ctx* c, int par, hipEvent_t* ev) {
 
 int buildGraph(surf_ctx* c) {
     if (c->graphExec) return SURF_OK;
+    const bool lng = c->longThresh != 0;
     SURF_CHECK(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-    for (int ph = 0; ph < kPhasesPerGraph; ++ph) launchPhase(c, ph & 1, nullptr);
+    if (lng) {
+        /* fork: the k_long chain on stream2, k_long(0) first (it consumes the
+         * previous replay's last escapes; replays are serialized) */
+        (void)hipEventRecord(c->evFork, c->stream);
+        (void)hipStreamWaitEvent(c->stream2, c->evFork, 0);
+        launchLong(c, 0, c->stream2);
+        (void)hipEventRecord(c->evLong[0], c->stream2);
+    }
+    for (int ph = 0; ph < kPhasesPerGraph; ++ph) launchPhase(c, ph, nullptr, true);
+    if (lng) (void)hipStreamWaitEvent(c->stream, c->evLong[kPhasesPerGraph - 1], 0);   /* join */
     hipError_t e = hipStreamEndCapture(c->stream, &c->graph);
     if (e != hipSuccess) return fail(c, SURF_ERR_HIP, std::string("graph capture: ") + hipGetErrorString(e));
     SURF_CHECK(c, hipGraphInstantiate(&c->graphExec, c->graph, nullptr, nullptr, 0));
@@ -366,15 +397,11 @@ int startStream(surf_ctx* c, uint64_t baseFrame, uint32_t maxSeg) {
     h.baseFrame = baseFrame;
     h.survCap = c->survCap;
     h.longThresh = c->longThresh;
-    h.ringCap = c->ringCap;
+    h.longBudget = c->longBudget;
     *c->hctr = h;
     SURF_CHECK(c, hipMemcpyAsync(c->ctr, c->hctr, sizeof(Counters), hipMemcpyHostToDevice, c->stream));
     SURF_CHECK(c, hipMemsetAsync(c->frameDone, 0, (size_t)kStripes * c->window * sizeof(uint32_t), c->stream));
-    /* ring sequence words restart with the entry counters (a stale seq could equal a new index + 1) */
-    SURF_CHECK(c, hipMemsetAsync(c->LR.seq, 0, (size_t)c->ringCap * sizeof(uint32_t), c->stream));
-    /* parked paths belong to the old stream, which ended drained: none remain */
     c->streamActive = true;
-    c->closed = false;
     c->baseFrame = baseFrame;
     c->targetFrames = 0;
     c->accFrames = 0;
@@ -437,7 +464,7 @@ int syncAndAccumulate(surf_ctx* c) {
  * direct launches with per-kernel events when profiling). */
 int advance(surf_ctx* c) {
     if (c->profiling) {
-        for (int ph = 0; ph < kPhasesPerGraph; ++ph) launchPhase(c, ph & 1, &c->pev[4 * ph]);
+        for (int ph = 0; ph < kPhasesPerGraph; ++ph) launchPhase(c, ph, &c->pev[4 * ph], false);
         SURF_CHECK(c, hipGetLastError());
         SURF_CHECK(c, hipEventSynchronize(c->pev[4 * (kPhasesPerGraph - 1) + 4]));
         for (int ph = 0; ph < kPhasesPerGraph; ++ph) {
@@ -452,62 +479,6 @@ int advance(surf_ctx* c) {
     c->stats.iterations += kPhasesPerGraph;
     if (c->stats.iterations > kMaxIterations)
         return fail(c, SURF_ERR_LIMIT, "wavefront did not drain after " + std::to_string(c->stats.iterations) + " iterations");
-    return SURF_OK;
-}
-
-/* ---- long-path worker ----------------------------------------------------
- * k_long launches are queued on stream2, kWorkerQueue at a time, so one is
- * always resident while the stream may escape paths; each lives
- * longLifetime and hands its unfinished paths to the next through the park
- * slots.  Once the ring is closed (drain), launches continue only while the
- * last finished launch left work behind. */
-void retireWorkers(surf_ctx* c) {
-    while (c->wRetired < c->wLaunched && hipEventQuery(c->evW[c->wRetired % surf_ctx::kWorkerQueue]) == hipSuccess)
-        ++c->wRetired;
-}
-
-int launchWorker(surf_ctx* c) {
-    const size_t lds = traversalLds(c, 64);
-    if (c->ldsTables)
-        hipLaunchKernelGGL(k_long<true>, dim3(c->longGrid), dim3(64), lds, c->stream2, c->S, c->LR, c->rad, c->frameDone,
-                           c->npx, c->window, c->ctr, stackWords(c, 64), c->longLifetime);
-    else
-        hipLaunchKernelGGL(k_long<false>, dim3(c->longGrid), dim3(64), lds, c->stream2, c->S, c->LR, c->rad, c->frameDone,
-                           c->npx, c->window, c->ctr, stackWords(c, 64), c->longLifetime);
-    SURF_CHECK(c, hipGetLastError());
-    SURF_CHECK(c, hipEventRecord(c->evW[c->wLaunched % surf_ctx::kWorkerQueue], c->stream2));
-    ++c->wLaunched;
-    return SURF_OK;
-}
-
-/* Work the worker still owes, from a counter copy taken after every launch
- * finished (hctr is then consistent with the device). */
-bool longWorkLeft(const surf_ctx* c) {
-    return c->hctr->ringHead != c->hctr->ringTail || c->hctr->parkedN != 0u;
-}
-
-int maintainWorkers(surf_ctx* c) {
-    if (!c->longThresh) return SURF_OK;
-    retireWorkers(c);
-    if (!c->closed) {
-        while (c->wLaunched - c->wRetired < (uint64_t)surf_ctx::kWorkerQueue)
-            if (int rc = launchWorker(c)) return rc;
-        return SURF_OK;
-    }
-    if (c->wLaunched != c->wRetired) return SURF_OK;
-    /* all launches done: a fresh copy of the counters says whether any is owed */
-    SURF_CHECK(c, hipMemcpyAsync(c->hctr, c->ctr, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
-    SURF_CHECK(c, hipStreamSynchronize(c->stream));
-    if (longWorkLeft(c)) return launchWorker(c);
-    return SURF_OK;
-}
-
-/* Drain: the wavefront is empty and nothing more will be issued. */
-int closeRing(surf_ctx* c) {
-    if (!c->longThresh || c->closed) return SURF_OK;
-    hipLaunchKernelGGL(k_close, dim3(1), dim3(64), 0, c->stream, c->ctr);
-    SURF_CHECK(c, hipGetLastError());
-    c->closed = true;
     return SURF_OK;
 }
 
@@ -539,12 +510,15 @@ bool waveEligible(const surf_ctx* c) {
     return !off && c->coopEligible && c->stackDepth <= 64;
 }
 
-int runTail(surf_ctx* c) {
-    const uint32_t n = c->hctr->nIn[0];
+/* longPool: finish the long pool lp[0] (the wavefront is empty and no
+ * escape is pending; their next extension ray is not counted yet), else
+ * pool 0 (regen counted each path's next extension ray). */
+int runTail(surf_ctx* c, bool longPool) {
+    const uint32_t n = longPool ? std::min(c->hctr->lpN[0], c->LP.lpCap) : c->hctr->nIn[0];
     if (n == 0) return SURF_OK;
     if (c->profiling) SURF_CHECK(c, hipEventRecord(c->pev[0], c->stream));
-    Pool in = c->pool[0];
-    uint32_t cnt = n, firstCounted = 1u;
+    Pool in = longPool ? c->LP.lp[0] : c->pool[0];
+    uint32_t cnt = n, firstCounted = longPool ? 0u : 1u;
     int buf = 0;
     static const bool dbg = std::getenv("SURF_DEBUG_TAIL") != nullptr;   /* diagnostics: per-stage log on stderr */
     auto t0 = std::chrono::steady_clock::now();
@@ -598,9 +572,17 @@ int runTail(surf_ctx* c) {
                      g[0] / ns, g[1] / ns, g[2] / ns, g[3], g[4]);
     }
 #endif
-    /* pool 0 is now empty: the next phase starts from regen's refill */
-    c->hctr->nIn[0] = 0;
-    SURF_CHECK(c, hipMemcpyAsync(&c->ctr->nIn[0], &c->hctr->nIn[0], sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+    if (longPool) {
+        /* every escaped path has finished */
+        c->hctr->lpN[0] = 0;
+        c->hctr->longPop = 0;
+        SURF_CHECK(c, hipMemcpyAsync(&c->ctr->lpN[0], &c->hctr->lpN[0], sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+        SURF_CHECK(c, hipMemcpyAsync(&c->ctr->longPop, &c->hctr->longPop, sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+    } else {
+        /* pool 0 is now empty: the next phase starts from regen's refill */
+        c->hctr->nIn[0] = 0;
+        SURF_CHECK(c, hipMemcpyAsync(&c->ctr->nIn[0], &c->hctr->nIn[0], sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+    }
     SURF_CHECK(c, hipStreamSynchronize(c->stream));
     return SURF_OK;
 }
@@ -615,31 +597,31 @@ int pump(surf_ctx* c, bool drain) {
     const uint64_t target = c->targetFrames * (uint64_t)c->npx;
     for (;;) {
         const uint64_t issued = c->hctr->issued[0];
-        const uint32_t inflight = c->hctr->nIn[0];        /* wavefront pool (the long-path worker holds the rest) */
+        /* in flight at a replay boundary: the wavefront pool, the long pool
+         * k_long(0) reads next, and the escapes of the last phase */
+        const uint32_t nW = c->hctr->nIn[0];
+        const uint32_t nL = c->longThresh ? std::min(c->hctr->lpN[0], c->LP.lpCap) : 0u;
+        const uint32_t nE = c->longThresh ? std::min(c->hctr->escN[3], c->LP.escCap) : 0u;
+        const uint64_t inflight = (uint64_t)nW + nL + nE;
         if (!drain && issued >= target) return SURF_OK;
         if (drain && c->accFrames >= c->targetFrames) return SURF_OK;
-        if ((rc = maintainWorkers(c))) return rc;
         const bool starved = issued >= c->pushedLimit;     /* nothing more may be issued right now */
         const uint64_t accBefore = c->accFrames;
         static const bool dbgDrain = std::getenv("SURF_DEBUG_DRAIN") != nullptr;   /* diagnostics: drain timeline */
         if (dbgDrain && starved) {
             static auto tS = std::chrono::steady_clock::now();
-            std::fprintf(stderr, "[surf drain] iteration %llu: %u in flight, ring %u..%u, %llu/%llu frames at %.3f ms\n",
-                         (unsigned long long)c->stats.iterations, inflight, c->hctr->ringHead, c->hctr->ringTail,
-                         (unsigned long long)c->accFrames, (unsigned long long)c->targetFrames,
+            std::fprintf(stderr, "[surf drain] iteration %llu: %u wavefront + %u long + %u escaped, %llu/%llu frames at %.3f ms\n",
+                         (unsigned long long)c->stats.iterations, nW, nL, nE, (unsigned long long)c->accFrames,
+                         (unsigned long long)c->targetFrames,
                          std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tS).count());
         }
-        bool waited = false;
-        if (starved && inflight > 0 && inflight <= tailThreshold(c)) {
-            if ((rc = runTail(c))) return rc;
+        if (starved && inflight > 0 && nW == 0 && nE == 0) {
+            /* only long paths left: the staged tail finishes them */
+            if ((rc = runTail(c, true))) return rc;
+        } else if (starved && nL == 0 && nE == 0 && nW > 0 && nW <= tailThreshold(c)) {
+            if ((rc = runTail(c, false))) return rc;
         } else if (starved && inflight == 0) {
-            /* every wavefront path finished: accumulating re-opens the window;
-             * frames still open wait for the long-path worker */
-            if (drain && (rc = closeRing(c))) return rc;
-            if (c->wLaunched != c->wRetired) {
-                SURF_CHECK(c, hipEventSynchronize(c->evW[c->wRetired % surf_ctx::kWorkerQueue]));
-                waited = true;
-            }
+            /* every issued sample finished: accumulating re-opens the window */
         } else {
             /* draining (nothing left to issue): several replays per host poll --
              * the per-replay poll, not the kernels, is what a small pool pays */
@@ -648,8 +630,7 @@ int pump(surf_ctx* c, bool drain) {
                 if ((rc = advance(c))) return rc;
         }
         if ((rc = syncAndAccumulate(c))) return rc;
-        const bool workerOwes = c->longThresh && (!c->closed || c->wLaunched != c->wRetired || longWorkLeft(c));
-        if (starved && inflight == 0 && c->accFrames == accBefore && !waited && !workerOwes)
+        if (starved && inflight == 0 && c->accFrames == accBefore)
             return fail(c, SURF_ERR_HIP, "sample stream stalled: pool empty but frames incomplete");
     }
 }
@@ -719,7 +700,9 @@ int createCtx(int dev, uint32_t w, uint32_t h, std::vector<uint32_t> rows, surf_
     c->npx = (uint32_t)(w * c->rows.size());
     bool evOk = true;
     if (hipSetDevice(dev) == hipSuccess) {
-        for (auto& e : c->evW) evOk = evOk && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+        evOk = hipEventCreateWithFlags(&c->evFork, hipEventDisableTiming) == hipSuccess;
+        for (auto& e : c->evShade) evOk = evOk && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+        for (auto& e : c->evLong) evOk = evOk && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
     }
     if (!evOk || hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
@@ -782,7 +765,9 @@ void surf_destroy(surf_ctx* c) {
     if (c->stream2) (void)hipStreamSynchronize(c->stream2);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->stream2) (void)hipStreamDestroy(c->stream2);
-    for (auto& e : c->evW) if (e) (void)hipEventDestroy(e);
+    if (c->evFork) (void)hipEventDestroy(c->evFork);
+    for (auto& e : c->evShade) if (e) (void)hipEventDestroy(e);
+    for (auto& e : c->evLong) if (e) (void)hipEventDestroy(e);
     delete c;
 }
 
@@ -848,14 +833,16 @@ int surf_set_tail_coop(surf_ctx* c, uint32_t max_paths) {
     return SURF_OK;
 }
 
-int surf_set_long_paths(surf_ctx* c, uint32_t escape_segments, uint32_t lifetime_us) {
+int surf_set_long_paths(surf_ctx* c, uint32_t escape_segments, uint32_t segments_per_phase) {
     if (!c) return fail(nullptr, SURF_ERR_INVALID, "ctx is NULL");
+    if (escape_segments != 0 && (segments_per_phase == 0 || segments_per_phase > 4096))
+        return fail(c, SURF_ERR_INVALID, "segments_per_phase must be 1..4096");
     SURF_CHECK(c, hipSetDevice(c->device));
     const int rc = endStream(c);
     if (rc) return rc;
     c->longThresh = escape_segments;
-    /* s_memrealtime ticks at 100 MHz; one launch lives at most 1 s */
-    c->longLifetime = 100ull * std::min<uint32_t>(lifetime_us ? lifetime_us : kDefaultLifetimeUs, 1000000u);
+    if (escape_segments) c->longBudget = segments_per_phase;
+    destroyGraph(c);                  /* the graph's shape (the k_long chain) changes */
     return SURF_OK;
 }
 int surf_set_persistent(surf_ctx* c, int enabled) {

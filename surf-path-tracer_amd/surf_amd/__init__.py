@@ -328,10 +328,10 @@ class Renderer:
         """Single-stage drain as the cooperative tail when <= max_paths paths remain (0 = never)."""
         _check(load().surf_set_tail_coop(self._h, max_paths), "surf_set_tail_coop", self._h)
 
-    def set_long_paths(self, escape_segments: int = 24, lifetime_us: int = 0):
-        """Paths reaching escape_segments move to the concurrent long-path worker (0 = off);
-        lifetime_us: life of one worker launch (0 = default)."""
-        _check(load().surf_set_long_paths(self._h, escape_segments, lifetime_us), "surf_set_long_paths", self._h)
+    def set_long_paths(self, escape_segments: int = 16, segments_per_phase: int = 8):
+        """Paths reaching escape_segments leave the wavefront for the long pool, advanced
+        segments_per_phase segments per phase beside it (escape_segments 0 = off)."""
+        _check(load().surf_set_long_paths(self._h, escape_segments, segments_per_phase), "surf_set_long_paths", self._h)
 
     def set_persistent(self, on: bool):
         """Out-of-step (persistent) wavefront traversal on/off (identical results)."""

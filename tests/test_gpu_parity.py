@@ -121,18 +121,18 @@ def test_drain_policies_bitexact(oracle_scene, product_scene, policy):
     r0.close()
 
 
-@pytest.mark.parametrize("escape,lifetime_us", [(2, 0), (4, 300), (24, 0), (3, 50)],
-                         ids=["escape2", "escape4-short-life", "escape24", "escape3-park-heavy"])
-def test_long_path_worker_bitexact(oracle_scene, product_scene, escape, lifetime_us):
-    """Paths escaping the wavefront to the concurrent long-path worker (device
-    ring hand-off, shadow ray carried along, lanes parked and resumed across
-    worker launches) give the oracle's radiance and event counts bit for bit.
-    escape 2/3 pushes most paths through the ring, so it wraps many times."""
+@pytest.mark.parametrize("escape,per_phase", [(2, 1), (4, 8), (24, 8), (3, 64)],
+                         ids=["escape2-1seg", "escape4-8seg", "escape24-8seg", "escape3-64seg"])
+def test_long_path_worker_bitexact(oracle_scene, product_scene, escape, per_phase):
+    """Paths escaping the wavefront to the long pool (escape queues with the
+    shadow ray carried along, the k_long chain of the phase graph, the staged
+    tail over the long pool) give the oracle's radiance and event counts bit
+    for bit.  escape 2/3 pushes most paths through the long pool."""
     W, H, F = 128, 96, 6
     r = surf_amd.Renderer(product_scene, W, H, pool_capacity=8192)
-    r.set_long_paths(escape, lifetime_us)
+    r.set_long_paths(escape, per_phase)
     r.render(2, 0, 0)
-    r.render(F - 2, 2, 0)                 # the stream (and the worker) spans render calls
+    r.render(F - 2, 2, 0)                 # the stream (and the long pool) spans render calls
     g = r.accumulator()
     st = r.stats()
     oracle.set_zero_cutoff(True)
@@ -140,18 +140,17 @@ def test_long_path_worker_bitexact(oracle_scene, product_scene, escape, lifetime
         c2, cnt, _ = oracle_scene.render(W, H, F)
     finally:
         oracle.set_zero_cutoff(False)
-    _assert_bitexact(g, c2, f"long-path worker escape={escape}")
+    _assert_bitexact(g, c2, f"long paths escape={escape} per_phase={per_phase}")
     _assert_counts(st, cnt)
-    assert st["long_paths"] > 0, "no path went through the worker"
+    assert st["long_paths"] > 0, "no path finished in the long pool"
     r.close()
 
 
 def test_long_path_worker_full_frame(oracle_scene, product_scene):
-    """1280x720 with the worker on: a band of rows against the oracle.  (Escape
-    at 6 segments: with two frames the drain tail takes over after ~12 phases.)"""
+    """1280x720 with long paths on: a band of rows against the oracle."""
     W, H, F = 1280, 720, 2
     r = surf_amd.Renderer(product_scene, W, H)
-    r.set_long_paths(6, 0)
+    r.set_long_paths(6, 8)
     r.render(F, 0, 0)
     g = r.accumulator()
     st = r.stats()

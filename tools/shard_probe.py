@@ -18,7 +18,7 @@ base = None
 for G in gs:
     times = []
     for k in range(G if not SHARDS else min(G, int(SHARDS))):
-        r = surf_amd.Renderer(scene, W, H, shard=surf_amd.ShardSpec(k, G, 16 if G > 1 else 0),
+        r = surf_amd.Renderer(scene, W, H, shard=surf_amd.ShardSpec(k, G, int(os.environ.get("ROWBLOCK", "16")) if G > 1 else 0),
                               pool_capacity=int(os.environ["CAP"]) if os.environ.get("CAP") else None)
         if os.environ.get("LONG"):
             r.set_long_paths(*[int(x) for x in os.environ["LONG"].split(",")])
@@ -34,7 +34,7 @@ for G in gs:
         times.append(time.perf_counter() - t0)
         st = r.stats()
         r.close()
-        if G == 1 or k == 0:
+        if G == 1 or k == 0 or os.environ.get("VERBOSE"):
             print(json.dumps({"G": G, "shard": k, "ms": round(times[-1] * 1e3, 1), "tail_paths": st["tail_paths"],
                               "max_seg": st.get("max_segments"), "iters": st["iterations"]}), flush=True)
     t = max(times)
