@@ -43,6 +43,9 @@ constexpr int kBlock = 256;
 #ifndef SURF_SEG_TIMING
 #define SURF_SEG_TIMING 0
 #endif
+#ifndef SURF_TAIL_WAVES
+#define SURF_TAIL_WAVES 3          /* k_tail waves per SIMD (2, 3: same speed; 4, 6: slower) */
+#endif
 #ifndef SURF_TRACE_WAVES
 #define SURF_TRACE_WAVES 1
 #endif
@@ -1409,7 +1412,7 @@ __device__ __forceinline__ bool runPath(const DevScene& S, const TraceTables& Tt
  * drain stage.  firstCounted: the first extension ray of each input path is
  * already in the event counts (regen counted it). */
 template <bool LDS_TABLES>
-__global__ __launch_bounds__(64, 3) void k_tail(DevScene S, Pool cur, uint32_t n, uint32_t lpw, float4* __restrict__ rad,
+__global__ __launch_bounds__(64, SURF_TAIL_WAVES) void k_tail(DevScene S, Pool cur, uint32_t n, uint32_t lpw, float4* __restrict__ rad,
                                              uint32_t* __restrict__ frameDone, uint32_t npx, uint32_t window, Counters* C,
                                              uint32_t stackWords, uint32_t firstCounted, uint32_t budget, Pool surv) {
     extern __shared__ uint32_t lds[];

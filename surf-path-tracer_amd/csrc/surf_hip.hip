@@ -296,7 +296,7 @@ int allocWavefront(surf_ctx* c) {
     for (auto& e : c->pev) SURF_CHECK(c, hipEventCreate(&e));
     const uint64_t maxBlocks = (cap + kBlock - 1) / kBlock;
     c->gridWork = (uint32_t)std::min<uint64_t>(maxBlocks, (uint64_t)cus * 8);
-    c->coopMax = (uint32_t)cus * 12;
+    c->coopMax = (uint32_t)cus * 4 * SURF_TAIL_WAVES;   /* resident k_tail waves: lanes per wave = paths / this */
     if (const char* e = std::getenv("SURF_DRAIN_REPLAYS")) c->drainReplays = std::max(1, std::atoi(e));    /* 3 waves per SIMD of the tail kernels (launch bounds) */
     c->gridRegen = (uint32_t)std::min<uint64_t>(maxBlocks, (uint64_t)cus * 8);
     c->allocated = true;
