@@ -108,12 +108,16 @@ struct surf_ctx {
     bool coopEligible = false;     /* single-leaf TLAS of <= 64 instances, LDS tables */
     int traceMode = 0;             /* surf_trace_closest/_any: 0 one ray per lane, 1 one ray per wave */
     bool persistent = false;       /* out-of-step lanes with per-wave ray ranges: measured 4x slower */
+    bool sortRays = true;          /* order each phase's rays by start instance (SURF_SORT=0: off) */
     /* long paths: escape queues + long pools, advanced by the k_long chain of the graph (surf_set_long_paths) */
     uint32_t longThresh = 0;       /* escape length (0 = off) */
     uint32_t longBudget = 8;       /* segments per long path per phase */
     hipStream_t stream2 = nullptr; /* the k_long branch while the graph is captured */
     hipEvent_t evFork = nullptr, evShade[kPhasesPerGraph] = {}, evLong[kPhasesPerGraph] = {};
     LongPools LP{};
+    /* ray order (k_bincount / k_binscan / k_binscatter each phase) */
+    uint32_t* order = nullptr;
+    uint32_t* binHist = nullptr;
     uint32_t tailLanes = 0;
     uint32_t segMaxBase = 0;       /* longest path of finished streams */
 
@@ -256,7 +260,10 @@ int allocWavefront(surf_ctx* c) {
         if ((rc = devAlloc(c, c->wfAllocs, &c->pool[p].o, cap))) return rc;
         if ((rc = devAlloc(c, c->wfAllocs, &c->pool[p].d, cap))) return rc;
         if ((rc = devAlloc(c, c->wfAllocs, &c->pool[p].T, cap))) return rc;
+        if ((rc = devAlloc(c, c->wfAllocs, &c->pool[p].key, cap))) return rc;
     }
+    if ((rc = devAlloc(c, c->wfAllocs, &c->order, cap))) return rc;
+    if ((rc = devAlloc(c, c->wfAllocs, &c->binHist, (size_t)kBins * kSortBlocks))) return rc;
     /* grid: 8 workgroups of 256 per CU saturate the 256-CU chip; grid-stride beyond */
     int cus = 256;
     hipDeviceProp_t prop;
@@ -286,6 +293,7 @@ int allocWavefront(surf_ctx* c) {
     if ((rc = devAlloc(c, c->wfAllocs, &c->Q.o, cap))) return rc;
     if ((rc = devAlloc(c, c->wfAllocs, &c->Q.d, cap))) return rc;
     if ((rc = devAlloc(c, c->wfAllocs, &c->Q.c, cap))) return rc;
+    if ((rc = devAlloc(c, c->wfAllocs, &c->Q.key, cap))) return rc;
     if ((rc = devAlloc(c, c->wfAllocs, &c->rad, (size_t)c->npx * c->window))) return rc;
     if ((rc = devAlloc(c, c->wfAllocs, &c->ctr, 1))) return rc;
     if ((rc = devAlloc(c, c->wfAllocs, &c->frameDone, (size_t)kStripes * c->window))) return rc;
@@ -304,6 +312,16 @@ int allocWavefront(surf_ctx* c) {
 }
 
 StreamGeom geom(const surf_ctx* c) { return StreamGeom{c->dRows, c->width, c->npx, c->window}; }
+
+/* Counting sort of the pool (which 0) or shadow queue (which 1) of phase par
+ * by its 4-bit key into c->order. */
+void launchSort(surf_ctx* c, const uint8_t* key, int par, int which) {
+    hipLaunchKernelGGL(k_bincount, dim3(kSortBlocks), dim3(kBlock), 0, c->stream, key, (const Counters*)c->ctr, par, which,
+                       c->binHist);
+    hipLaunchKernelGGL(k_binscan, dim3(1), dim3(1024), 0, c->stream, c->binHist, kBins * kSortBlocks);
+    hipLaunchKernelGGL(k_binscatter, dim3(kSortBlocks), dim3(kBlock), 0, c->stream, key, (const Counters*)c->ctr, par, which,
+                       (const uint32_t*)c->binHist, c->order);
+}
 
 /* k_long for phase ph: lp[ph & 1] + esc[(ph - 1) % 4] -> lp[(ph + 1) & 1]. */
 void launchLong(surf_ctx* c, int ph, hipStream_t st) {
@@ -331,26 +349,32 @@ void launchPhase(surf_ctx* c, int ph, hipEvent_t* ev, bool capture) {
     const bool lng = c->longThresh != 0;
     if (lng && !capture) launchLong(c, ph, c->stream);
     if (ev) (void)hipEventRecord(ev[0], c->stream);
-    if (c->persistent && c->ldsTables && c->S.tlasLeafCount > 0)
+    const bool persistent = c->persistent && c->ldsTables && c->S.tlasLeafCount > 0;
+    const uint32_t* order = nullptr;
+    if (c->sortRays && !persistent) {
+        launchSort(c, c->pool[par].key, par, 0);
+        order = c->order;
+    }
+    if (persistent)
         hipLaunchKernelGGL(k_extend_p<true>, dim3(c->gridWork), dim3(kBlock), lds, c->stream, c->S, c->pool[par], c->hitTUV,
                            c->hitInst, (const Counters*)c->ctr, par, sw);
     else if (c->ldsTables)
         hipLaunchKernelGGL(k_extend<true>, dim3(c->gridWork), dim3(kBlock), lds, c->stream, c->S, c->pool[par], c->hitTUV,
-                           c->hitInst, (const Counters*)c->ctr, par, sw);
+                           c->hitInst, (const Counters*)c->ctr, par, sw, order);
     else
         hipLaunchKernelGGL(k_extend<false>, dim3(c->gridWork), dim3(kBlock), lds, c->stream, c->S, c->pool[par], c->hitTUV,
-                           c->hitInst, (const Counters*)c->ctr, par, sw);
+                           c->hitInst, (const Counters*)c->ctr, par, sw, order);
     if (ev) (void)hipEventRecord(ev[1], c->stream);
     if (lng && capture && ph >= 3) (void)hipStreamWaitEvent(c->stream, c->evLong[ph - 3], 0);
     const uint32_t escQ = (uint32_t)ph & 3u;
     if (c->ldsTables)
         hipLaunchKernelGGL(k_shade<true>, dim3(c->gridWork), dim3(kBlock), 0, c->stream, c->S, c->pool[par], c->pool[par ^ 1],
                            c->hitTUV, (const uint32_t*)c->hitInst, c->Q, c->rad, c->frameDone, c->npx, c->window, c->ctr, par,
-                           c->LP, escQ);
+                           c->LP, escQ, order);
     else
         hipLaunchKernelGGL(k_shade<false>, dim3(c->gridWork), dim3(kBlock), 0, c->stream, c->S, c->pool[par], c->pool[par ^ 1],
                            c->hitTUV, (const uint32_t*)c->hitInst, c->Q, c->rad, c->frameDone, c->npx, c->window, c->ctr, par,
-                           c->LP, escQ);
+                           c->LP, escQ, order);
     if (lng && capture && ph + 1 < kPhasesPerGraph) {
         (void)hipEventRecord(c->evShade[ph], c->stream);
         (void)hipStreamWaitEvent(c->stream2, c->evShade[ph], 0);
@@ -358,10 +382,14 @@ void launchPhase(surf_ctx* c, int ph, hipEvent_t* ev, bool capture) {
         (void)hipEventRecord(c->evLong[ph + 1], c->stream2);
     }
     if (ev) (void)hipEventRecord(ev[2], c->stream);
+    /* shadow rays toward the same light together (the pool order no longer needed: reuse it) */
+    if (order) launchSort(c, c->Q.key, par, 1);
     if (c->ldsTables)
-        hipLaunchKernelGGL(k_connect<true>, dim3(c->gridWork), dim3(kBlock), lds, c->stream, c->S, c->Q, c->rad, c->ctr, par, sw);
+        hipLaunchKernelGGL(k_connect<true>, dim3(c->gridWork), dim3(kBlock), lds, c->stream, c->S, c->Q, c->rad, c->ctr, par, sw,
+                           (const uint32_t*)order);
     else
-        hipLaunchKernelGGL(k_connect<false>, dim3(c->gridWork), dim3(kBlock), lds, c->stream, c->S, c->Q, c->rad, c->ctr, par, sw);
+        hipLaunchKernelGGL(k_connect<false>, dim3(c->gridWork), dim3(kBlock), lds, c->stream, c->S, c->Q, c->rad, c->ctr, par, sw,
+                           (const uint32_t*)order);
     if (ev) (void)hipEventRecord(ev[3], c->stream);
     hipLaunchKernelGGL(k_regen, dim3(c->gridRegen), dim3(kBlock), 0, c->stream, c->cam, c->pool[par ^ 1], c->rad, c->ctr, par,
                        c->capacity, geom(c));
@@ -694,6 +722,7 @@ int createCtx(int dev, uint32_t w, uint32_t h, std::vector<uint32_t> rows, surf_
         return fail(nullptr, SURF_ERR_NO_DEVICE, std::string("device is ") + prop.gcnArchName + ", this build targets gfx950");
     auto* c = new surf_ctx();
     c->device = dev;
+    if (const char* e = std::getenv("SURF_SORT")) c->sortRays = e[0] != '0';
     c->width = w;
     c->height = h;
     c->rows = std::move(rows);
