@@ -641,9 +641,142 @@ __device__ __forceinline__ bool leafWave(const float4* tri, uint32_t lf, uint32_
     return any;
 }
 
+/* SURF_SEG_TIMING builds: per-segment breakdown of traceWave (diagnostics). */
+#if SURF_SEG_TIMING
+__device__ unsigned long long g_segStats[8];
+#endif
+struct SegStats { unsigned long long cycInst, cycLoop, visits, leaves, tris, entered; };
+
+/* Lanes-as-planes slab distances of the record held in row `row` (lanes
+ * 16 row .. 16 row + 13) of v: the DPP moves of slabPair stay inside a row of
+ * 16 lanes, so every row evaluates its own record. */
+template <bool FIN>
+__device__ __forceinline__ void slabPairRow(float v, float oA, float rdA, float depth, uint32_t row, float& d0, float& d1) {
+    const float t = (v - oA) * rdA;
+    float m0, m1;
+    if (FIN) {
+        /* o, 1/d and every box finite: no NaN can arise, the ternary min/max
+         * equal IEEE min/max (slabFinite), and the lane moves fold into the
+         * min/max as DPP operands (6 VALU ops instead of 17).  m0 / m1 are
+         * valid in lanes 4 and 10 of each row (their l-4, l-2 sources). */
+        float t0a, t1a;
+        asm volatile(
+            "s_nop 1\n\t"
+            "v_min_f32_dpp %0, %4, %4 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+            "v_max_f32_dpp %1, %4, %4 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+            "s_nop 1\n\t"
+            "v_max_f32_dpp %2, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf\n\t"
+            "v_min_f32_dpp %3, %1, %1 row_shr:4 row_mask:0xf bank_mask:0xf\n\t"
+            "s_nop 1\n\t"
+            "v_max_f32_dpp %2, %0, %2 row_shr:2 row_mask:0xf bank_mask:0xf\n\t"
+            "v_min_f32_dpp %3, %1, %3 row_shr:2 row_mask:0xf bank_mask:0xf"
+            : "=&v"(t0a), "=&v"(t1a), "=&v"(m0), "=&v"(m1)
+            : "v"(t));
+    } else {
+        const float tp = dppMov<kDppSwap1>(t);
+        const float t0a = tmin(t, tp), t1a = tmax(t, tp);
+        const float t0x = dppMov<kDppShr4>(t0a), t0y = dppMov<kDppShr2>(t0a);
+        const float t1x = dppMov<kDppShr4>(t1a), t1y = dppMov<kDppShr2>(t1a);
+        m0 = tmax(tmax(t0x, t0y), t0a);
+        m1 = tmin(tmin(t1x, t1y), t1a);
+    }
+    const float dist = (m1 >= m0 && m0 < depth && m1 > 0.0f) ? m0 : kFarAway;
+    d0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dist), (int)(4u + 16u * row)));
+    d1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dist), (int)(10u + 16u * row)));
+}
+
+/* slab()'s t0 / t1 before its hit test: the same operations in the same order. */
+__device__ __forceinline__ void slabRange(float4 lo, float4 hi, V3 o, V3 rd, float& t0, float& t1) {
+    const float tx0 = (lo.x - o.x) * rd.x, tx1 = (hi.x - o.x) * rd.x;
+    t0 = tmin(tx0, tx1); t1 = tmax(tx0, tx1);
+    const float ty0 = (lo.y - o.y) * rd.y, ty1 = (hi.y - o.y) * rd.y;
+    t0 = tmax(t0, tmin(ty0, ty1)); t1 = tmin(t1, tmax(ty0, ty1));
+    const float tz0 = (lo.z - o.z) * rd.z, tz1 = (hi.z - o.z) * rd.z;
+    t0 = tmax(t0, tmin(tz0, tz1)); t1 = tmin(t1, tmax(tz0, tz1));
+}
+__device__ __forceinline__ float slabHit(float t0, float t1, float depth) {
+    return (t1 >= t0 && t0 < depth && t1 > 0.0f) ? t0 : kFarAway;
+}
+__device__ __forceinline__ float bcast(float v, uint32_t l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), (int)l)); }
+
+/* A load the compiler may not sink past the code between it and its use (it
+ * would sink a load used on one branch into that branch, after the slab test
+ * it is meant to overlap).  Its VGPR is outside the compiler's wait-count
+ * tracking, so the value is passed through waitLoads() before any use. */
+__device__ __forceinline__ float loadEarly(const float* p) {
+    float v;
+    asm volatile("global_load_dword %0, %1, off" : "=v"(v) : "v"(p));
+    return v;
+}
+__device__ __forceinline__ void waitLoads(float& v) { asm volatile("s_waitcnt vmcnt(0)" : "+v"(v)); }
+/* ... and not before a and b are computed (the scheduler would hoist it). */
+__device__ __forceinline__ void waitLoadsAfter(float& v, float a, float b) {
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(v) : "s"(a), "s"(b));
+}
+
+/* The DFS below one BLAS root (blasTrace's loop), from the root's children:
+ * near child cn at distance dn (!= kFarAway), far child cf at df.  Latency:
+ * a visit issues the load of BOTH children's records (row 0 of the VGPR:
+ * left child, row 1: right; rows 2/3 repeat them) before its own slab test,
+ * so the near child's record is in registers when the decision is made; a
+ * pop loads the popped node's record into every row. */
+template <bool ANY, bool FIN>
+__device__ __forceinline__ bool blasWalk(const DevScene& S, uint32_t nodeOff, const float4* tri, V3 o, V3 d, V3 rd,
+                                         float dn, float df, uint32_t cn, uint32_t cf, float& depth, float& hu, float& hv,
+                                         uint32_t& hprim, SegStats* ss) {
+    const uint32_t lane = __lane_id(), l16 = lane & 15u;
+    const uint32_t dw = planeDword(l16), ax = l16 < 12u ? (l16 % 6u) >> 1 : 0u;
+    const uint32_t half = (lane >> 4) & 1u;
+    const float oA = pick3(o, ax), rdA = pick3(rd, ax);
+    const float* nodesF = reinterpret_cast<const float*>(S.nodes);
+    uint32_t stk = 0, sp = 0;
+    if (df != kFarAway) { stk = lane == sp ? cf : stk; ++sp; }
+    float cur = nodesF[16u * cn + dw];
+    uint32_t row = 0;
+    bool any = false;
+#if SURF_SEG_TIMING
+    if (ss) ++ss->entered;
+#endif
+    for (;;) {
+        const uint32_t lf = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(cur), (int)(12u + 16u * row));
+        const uint32_t cnt = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(cur), (int)(13u + 16u * row));
+#if SURF_SEG_TIMING
+        if (ss) { if (cnt) { ++ss->leaves; ss->tris += cnt; } else ++ss->visits; }
+#endif
+        if (cnt != 0u) {
+            if (leafWave<ANY>(tri, lf, cnt, o, d, depth, hu, hv, hprim)) {
+                if (ANY) return true;
+                any = true;
+            }
+            if (sp == 0u) break;
+            const uint32_t node = (uint32_t)__builtin_amdgcn_readlane((int)stk, (int)--sp);
+            cur = nodesF[16u * node + dw];
+            row = 0;
+            continue;
+        }
+        const uint32_t c0 = nodeOff + lf;
+        float nxt = loadEarly(nodesF + 16u * (c0 + half) + dw);
+        slabPairRow<FIN>(cur, oA, rdA, depth, row, dn, df);
+        uint32_t far = c0 + 1u, nearRow = 0u;
+        if (dn > df) { const float t = dn; dn = df; df = t; far = c0; nearRow = 1u; }
+        waitLoadsAfter(nxt, dn, df);   /* on every path: the register must not be reused while the load is in flight */
+        if (dn == kFarAway) {
+            if (sp == 0u) break;
+            const uint32_t node = (uint32_t)__builtin_amdgcn_readlane((int)stk, (int)--sp);
+            cur = nodesF[16u * node + dw];
+            row = 0;
+        } else {
+            cur = nxt;
+            row = nearRow;
+            if (df != kFarAway) { stk = lane == sp ? far : stk; ++sp; }
+        }
+    }
+    return any;
+}
+
 template <bool ANY>
 __device__ __forceinline__ bool blasWave(const DevScene& S, const TraceInst& I, V3 o, V3 d, float& depth, float& hu, float& hv,
-                                         uint32_t& hprim) {
+                                         uint32_t& hprim, SegStats* ss = nullptr) {
     const uint32_t lane = __lane_id();
     const uint32_t nodeOff = I.meta.x;
     const float4* tri = S.tris + 3u * I.meta.y;
@@ -658,53 +791,101 @@ __device__ __forceinline__ bool blasWave(const DevScene& S, const TraceInst& I, 
     uint32_t cn = nodeOff + rlf, cf = cn + 1u;
     if (dn > df) { const float t = dn; dn = df; df = t; const uint32_t c = cn; cn = cf; cf = c; }
     if (dn == kFarAway) return false;
-    uint32_t stk = 0, sp = 0, node = cn;
-    if (df != kFarAway) { stk = lane == sp ? cf : stk; ++sp; }
-    bool any = false;
-    for (;;) {
-        const float v = reinterpret_cast<const float*>(S.nodes + 4u * node)[dw];
-        const uint32_t lf = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(v), 12);
-        const uint32_t cnt = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(v), 13);
-        if (cnt != 0u) {
-            if (leafWave<ANY>(tri, lf, cnt, o, d, depth, hu, hv, hprim)) {
-                if (ANY) return true;
-                any = true;
-            }
-            if (sp == 0u) break;
-            node = (uint32_t)__builtin_amdgcn_readlane((int)stk, (int)--sp);
-            continue;
-        }
-        slabPair(v, oA, rdA, depth, dn, df);
-        cn = nodeOff + lf; cf = cn + 1u;
-        if (dn > df) { const float t = dn; dn = df; df = t; const uint32_t c = cn; cn = cf; cf = c; }
-        if (dn == kFarAway) {
-            if (sp == 0u) break;
-            node = (uint32_t)__builtin_amdgcn_readlane((int)stk, (int)--sp);
-        } else {
-            node = cn;
-            if (df != kFarAway) { stk = lane == sp ? cf : stk; ++sp; }
-        }
-    }
-    return any;
+    if (S.finiteBoxes && finite3(o) && finite3(rd))
+        return blasWalk<ANY, true>(S, nodeOff, tri, o, d, rd, dn, df, cn, cf, depth, hu, hv, hprim, ss);
+    return blasWalk<ANY, false>(S, nodeOff, tri, o, d, rd, dn, df, cn, cf, depth, hu, hv, hprim, ss);
 }
 
-/* BvhTLAS::intersect / intersectAny over a single-leaf TLAS (bvh.cpp:654-778). */
+/* BvhTLAS::intersect / intersectAny over a single-leaf TLAS (bvh.cpp:654-778).
+ * With <= 64 instances, lane k first computes instance k's object-space ray,
+ * 1/d and the slab ranges of its root's two children (all instances at once,
+ * the same operations as blasWave); the instances are then taken in TLAS
+ * order, each applying the depth test to its ranges at its turn (with the
+ * depth the earlier instances left), so a missed instance costs a few
+ * readlanes instead of a serial transform, three divisions and a slab test. */
 template <bool ANY>
 __device__ __forceinline__ bool traceWave(const DevScene& S, const TraceTables& Tt, V3 o, V3 d, float& depth, float& hu,
-                                          float& hv, uint32_t& hinst, uint32_t& hprim) {
+                                          float& hv, uint32_t& hinst, uint32_t& hprim, SegStats* ss = nullptr) {
     bool any = false;
-    for (uint32_t k = 0; k < S.tlasLeafCount; ++k) {
+    const uint32_t nI = S.tlasLeafCount;
+    if (nI > 64u) {
+        for (uint32_t k = 0; k < nI; ++k) {
+            const uint32_t ii = Tt.order[k];
+            const TraceInst& I = Tt.inst[ii];
+            V3 oo = mk3(rowDot(I.m0, o.x, o.y, o.z, 1.0f), rowDot(I.m1, o.x, o.y, o.z, 1.0f), rowDot(I.m2, o.x, o.y, o.z, 1.0f));
+            if (!I.meta.z) oo = divs(oo, rowDot(I.m3, o.x, o.y, o.z, 1.0f));
+            const V3 dd = mk3(rowDot(I.m0, d.x, d.y, d.z, 0.0f), rowDot(I.m1, d.x, d.y, d.z, 0.0f), rowDot(I.m2, d.x, d.y, d.z, 0.0f));
+            if (blasWave<ANY>(S, I, oo, dd, depth, hu, hv, hprim, ss)) {
+                if (ANY) return true;
+                any = true;
+                hinst = ii;
+            }
+        }
+        return any;
+    }
+#if SURF_SEG_TIMING
+    unsigned long long t0 = __builtin_readcyclecounter();
+#endif
+    const uint32_t lane = __lane_id();
+    V3 oo = mk3(0.0f, 0.0f, 0.0f), dd = oo, rd = oo;
+    float a0 = 0.0f, a1 = 0.0f, b0 = 0.0f, b1 = 0.0f;
+    if (lane < nI) {
+        const TraceInst& I = Tt.inst[Tt.order[lane]];
+        oo = mk3(rowDot(I.m0, o.x, o.y, o.z, 1.0f), rowDot(I.m1, o.x, o.y, o.z, 1.0f), rowDot(I.m2, o.x, o.y, o.z, 1.0f));
+        if (!I.meta.z) oo = divs(oo, rowDot(I.m3, o.x, o.y, o.z, 1.0f));
+        dd = mk3(rowDot(I.m0, d.x, d.y, d.z, 0.0f), rowDot(I.m1, d.x, d.y, d.z, 0.0f), rowDot(I.m2, d.x, d.y, d.z, 0.0f));
+        rd = mk3(1.0f / dd.x, 1.0f / dd.y, 1.0f / dd.z);
+        slabRange(I.r0, I.r1, oo, rd, a0, a1);
+        slabRange(I.r2, I.r3, oo, rd, b0, b1);
+    }
+    /* candidates: a root child that misses at the entry depth misses at every
+     * later (smaller) depth too; root leaves are always taken */
+    const bool rootLeaf = lane < nI && f2u(Tt.inst[Tt.order[lane]].r1.w) != 0u;
+    unsigned long long cand = __ballot(lane < nI && (rootLeaf || slabHit(a0, a1, depth) != kFarAway ||
+                                                     slabHit(b0, b1, depth) != kFarAway));
+    while (cand) {
+        const uint32_t k = (uint32_t)(__ffsll((long long)cand) - 1);
+        cand &= cand - 1ull;
         const uint32_t ii = Tt.order[k];
         const TraceInst& I = Tt.inst[ii];
-        V3 oo = mk3(rowDot(I.m0, o.x, o.y, o.z, 1.0f), rowDot(I.m1, o.x, o.y, o.z, 1.0f), rowDot(I.m2, o.x, o.y, o.z, 1.0f));
-        if (!I.meta.z) oo = divs(oo, rowDot(I.m3, o.x, o.y, o.z, 1.0f));
-        const V3 dd = mk3(rowDot(I.m0, d.x, d.y, d.z, 0.0f), rowDot(I.m1, d.x, d.y, d.z, 0.0f), rowDot(I.m2, d.x, d.y, d.z, 0.0f));
-        if (blasWave<ANY>(S, I, oo, dd, depth, hu, hv, hprim)) {
+        const uint32_t nodeOff = I.meta.x;
+        const float4* tri = S.tris + 3u * I.meta.y;
+        const uint32_t rlf = f2u(I.r0.w), rcnt = f2u(I.r1.w);
+        float dn = 0.0f, df = 0.0f;
+        uint32_t cn = nodeOff + rlf, cf = cn + 1u;
+        if (rcnt == 0u) {
+            /* root: never box-tested (bvh.cpp:131); its children's boxes are in its record */
+            dn = slabHit(bcast(a0, k), bcast(a1, k), depth);
+            df = slabHit(bcast(b0, k), bcast(b1, k), depth);
+            if (dn > df) { const float t = dn; dn = df; df = t; const uint32_t c = cn; cn = cf; cf = c; }
+            if (dn == kFarAway) continue;
+        }
+        const V3 ok = mk3(bcast(oo.x, k), bcast(oo.y, k), bcast(oo.z, k));
+        const V3 dk = mk3(bcast(dd.x, k), bcast(dd.y, k), bcast(dd.z, k));
+#if SURF_SEG_TIMING
+        if (ss) { const unsigned long long t1 = __builtin_readcyclecounter(); ss->cycInst += t1 - t0; t0 = t1; }
+#endif
+        bool h;
+        if (rcnt != 0u) {
+            h = leafWave<ANY>(tri, rlf, rcnt, ok, dk, depth, hu, hv, hprim);
+        } else {
+            const V3 rk = mk3(bcast(rd.x, k), bcast(rd.y, k), bcast(rd.z, k));
+            h = (S.finiteBoxes && finite3(ok) && finite3(rk))
+                    ? blasWalk<ANY, true>(S, nodeOff, tri, ok, dk, rk, dn, df, cn, cf, depth, hu, hv, hprim, ss)
+                    : blasWalk<ANY, false>(S, nodeOff, tri, ok, dk, rk, dn, df, cn, cf, depth, hu, hv, hprim, ss);
+        }
+#if SURF_SEG_TIMING
+        if (ss) { const unsigned long long t1 = __builtin_readcyclecounter(); ss->cycLoop += t1 - t0; t0 = t1; }
+#endif
+        if (h) {
             if (ANY) return true;
             any = true;
             hinst = ii;
         }
     }
+#if SURF_SEG_TIMING
+    if (ss) ss->cycInst += __builtin_readcyclecounter() - t0;
+#endif
     return any;
 }
 
@@ -1690,6 +1871,10 @@ __global__ __launch_bounds__(64, 3) void k_tail_coop(DevScene S, Pool cur, uint3
     unsigned long long nExt = 0, nHit = 0, nCont = 0, nSh = 0, nAcc = 0, nUn = 0;
 #if SURF_SEG_TIMING
     unsigned long long cyc[3] = {0, 0, 0};
+    SegStats ss{0, 0, 0, 0, 0, 0};
+    SegStats* ssp = &ss;
+#else
+    SegStats* ssp = nullptr;
 #endif
     for (;;) {
         float depth = kFarAway, u = 0.0f, v = 0.0f;
@@ -1697,8 +1882,9 @@ __global__ __launch_bounds__(64, 3) void k_tail_coop(DevScene S, Pool cur, uint3
 #if SURF_SEG_TIMING
         const unsigned long long c0 = __builtin_readcyclecounter();
 #endif
-        const bool hit = WAVE ? traceWave<false>(S, Tt, xyz(o4), xyz(d4), depth, u, v, inst, prim)
+        const bool hit = WAVE ? traceWave<false>(S, Tt, xyz(o4), xyz(d4), depth, u, v, inst, prim, ssp)
                               : traceSceneCoop(S, Tt, xyz(o4), xyz(d4), depth, u, v, inst, prim, stk, astk, stride);
+        (void)ssp;
         ++nExt;
         ShadeOut r;
 #if SURF_SEG_TIMING
@@ -1754,6 +1940,8 @@ __global__ __launch_bounds__(64, 3) void k_tail_coop(DevScene S, Pool cur, uint3
 #if SURF_SEG_TIMING
         atomicAdd(&C->dbg[0], cyc[0]); atomicAdd(&C->dbg[1], cyc[1]); atomicAdd(&C->dbg[2], cyc[2]);
         atomicAdd(&C->dbg[3], nExt); atomicAdd(&C->dbg[4], nSh);
+        atomicAdd(&g_segStats[0], ss.cycInst); atomicAdd(&g_segStats[1], ss.cycLoop); atomicAdd(&g_segStats[2], ss.visits);
+        atomicAdd(&g_segStats[3], ss.leaves); atomicAdd(&g_segStats[4], ss.tris); atomicAdd(&g_segStats[5], ss.entered);
 #endif
     }
 }

@@ -598,6 +598,10 @@ int runTail(surf_ctx* c, bool longPool) {
         const double ns = (double)std::max(1ull, g[3]);
         std::fprintf(stderr, "[surf tail] coop cycles per segment: extend %.0f shade %.0f connect %.0f (%llu segments, %llu shadow)\n",
                      g[0] / ns, g[1] / ns, g[2] / ns, g[3], g[4]);
+        unsigned long long h[8];
+        SURF_CHECK(c, hipMemcpyFromSymbol(h, HIP_SYMBOL(g_segStats), sizeof(h)));
+        std::fprintf(stderr, "[surf tail] extend per segment: instance prologues %.0f cycles, BLAS loops %.0f cycles, %.1f interior visits, "
+                     "%.1f leaves, %.1f triangles, %.2f instances entered\n", h[0] / ns, h[1] / ns, h[2] / ns, h[3] / ns, h[4] / ns, h[5] / ns);
     }
 #endif
     if (longPool) {
