@@ -178,7 +178,7 @@ int surf_set_zero_cutoff(surf_ctx* ctx, int enabled);
  * Drains the context first. */
 int surf_set_tail_policy(surf_ctx* ctx, uint32_t threshold_paths, uint32_t lanes_per_wave, uint32_t stage_segments);
 /* Drain paths handed to the cooperative tail (one path per 64-lane wave, the
- * lanes-as-planes traversal; default 20000, 0 = never).  Identical results. */
+ * lanes-as-planes traversal; default 60000, 0 = never).  Identical results. */
 int surf_set_tail_coop(surf_ctx* ctx, uint32_t max_paths);
 /* Long paths: a path whose next segment would be its `escape_segments`-th
  * leaves the wavefront (which advances a path one segment per iteration, i.e.

@@ -103,7 +103,7 @@ struct surf_ctx {
     Pool surv[2]{};                /* drain survivors, ping-pong between stages */
     uint32_t survCap = 0;
     uint32_t coopMax = 0;          /* survivors handled by the cooperative tail (one path per wave) */
-    uint32_t coopAll = 20000;      /* drain paths left to the cooperative (one path per wave) tail (surf_set_tail_coop) */
+    uint32_t coopAll = 60000;      /* drain paths left to the cooperative (one path per wave) tail (surf_set_tail_coop) */
     int drainReplays = 1;          /* graph replays per host poll while draining (SURF_DRAIN_REPLAYS) */
     bool coopEligible = false;     /* single-leaf TLAS of <= 64 instances, LDS tables */
     int traceMode = 0;             /* surf_trace_closest/_any: 0 one ray per lane, 1 one ray per wave */
@@ -558,7 +558,13 @@ int runTail(surf_ctx* c, bool longPool) {
         }
         if (c->coopEligible && cnt <= c->coopAll) {
             /* the wave traversal keeps no stack in LDS: only the trace tables */
-            if (waveEligible(c))
+            /* tables from global memory (wave-uniform reads): the LDS copies would
+             * cap the one-wave blocks at ~2 waves per SIMD (SURF_COOP_LDS=1: A/B) */
+            static const bool coopLds = std::getenv("SURF_COOP_LDS") && std::atoi(std::getenv("SURF_COOP_LDS")) != 0;
+            if (waveEligible(c) && !coopLds)
+                hipLaunchKernelGGL((k_tail_coop<false, true>), dim3(cnt), dim3(64), 0, c->stream, c->S, in, cnt, c->rad, c->frameDone,
+                                   c->npx, c->window, c->ctr, 0u, firstCounted);
+            else if (waveEligible(c))
                 hipLaunchKernelGGL((k_tail_coop<true, true>), dim3(cnt), dim3(64), traversalLds(c, 64) - (size_t)stackWords(c, 64) * sizeof(uint32_t),
                                    c->stream, c->S, in, cnt, c->rad, c->frameDone, c->npx, c->window, c->ctr, 0u, firstCounted);
             else
@@ -1085,6 +1091,17 @@ int surf_upload_scene(surf_ctx* c, const surf_scene_desc* d) {
     S.bgColor[0] = bg.color.x; S.bgColor[1] = bg.color.y; S.bgColor[2] = bg.color.z;
     S.bgA[0] = bg.gradient_a.x; S.bgA[1] = bg.gradient_a.y; S.bgA[2] = bg.gradient_a.z;
     S.bgB[0] = bg.gradient_b.x; S.bgB[1] = bg.gradient_b.y; S.bgB[2] = bg.gradient_b.z;
+    {
+        /* ray-order cells (a sort key only: any value is correct, a stale box after refits too) */
+        const surf_bvh_node& root = d->tlas_nodes[0];
+        const float lo[3] = {root.bb_min.x, root.bb_min.y, root.bb_min.z}, hi[3] = {root.bb_max.x, root.bb_max.y, root.bb_max.z};
+        for (int a = 0; a < 3; ++a) {
+            const float ext = hi[a] - lo[a];
+            const bool ok = std::isfinite(lo[a]) && std::isfinite(ext) && ext > 0.0f;
+            S.cellLo[a] = ok ? lo[a] : 0.0f;
+            S.cellScale[a] = ok ? 2.0f / ext : 0.0f;
+        }
+    }
     c->S = S;
     c->ldsTables = d->instance_count <= kLdsInst && d->instance_count <= kLdsTraceInst && d->material_count <= kLdsMats &&
                    d->light_count <= kLdsLights;
