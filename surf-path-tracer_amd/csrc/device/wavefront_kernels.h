@@ -76,6 +76,7 @@ struct TraceInst {
     float4 m0, m1, m2, m3;
     uint4 meta;               /* nodeOffset, idxOffset, affineInv, instance id */
     float4 r0, r1, r2, r3;    /* root node record */
+    float4 wlo, whi;          /* conservative world box of the BLAS's triangles (wlo.w != 0: usable) */
 };
 constexpr uint32_t kLdsTraceInst = 64;   /* instances staged in LDS (9 KB) */
 
@@ -443,10 +444,27 @@ __device__ __forceinline__ bool traceScene(const DevScene& S, const TraceTables&
     bool any = false;
     if (S.tlasLeafCount) {
         /* single-leaf TLAS (the bundled scene): every lane visits the same
-         * instances in the same order -> wave-uniform loop over LDS records */
+         * instances in the same order -> wave-uniform loop over LDS records.
+         * A lane skips an instance whose conservative world box (the BLAS's
+         * triangles under M, padded far beyond float rounding) its ray misses
+         * within [0, depth): no triangle of it can produce an accepted hit, so
+         * the skip changes no result; a wave skips the instance's transform,
+         * divisions and traversal when all its lanes do (coherent rays: the
+         * shadow queue is ordered by light and origin cell). */
+        const V3 rdw = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+        const bool cullOk = finite3(o) && finite3(rdw);
         for (uint32_t k = 0; k < S.tlasLeafCount; ++k) {
             const uint32_t ii = Tt.order[k];
-            if (instanceTrace<ANY>(S, Tt.inst[ii], o, d, depth, hu, hv, hprim, stk, stride, 0u)) {
+            const TraceInst& I = Tt.inst[ii];
+            if (cullOk && I.wlo.w != 0.0f) {
+                const float tx0 = (I.wlo.x - o.x) * rdw.x, tx1 = (I.whi.x - o.x) * rdw.x;
+                const float ty0 = (I.wlo.y - o.y) * rdw.y, ty1 = (I.whi.y - o.y) * rdw.y;
+                const float tz0 = (I.wlo.z - o.z) * rdw.z, tz1 = (I.whi.z - o.z) * rdw.z;
+                const float t0 = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fminf(tz0, tz1));
+                const float t1 = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
+                if (t1 < t0 || t1 < 0.0f || t0 >= depth) continue;
+            }
+            if (instanceTrace<ANY>(S, I, o, d, depth, hu, hv, hprim, stk, stride, 0u)) {
                 if (ANY) return true;
                 any = true;
                 hinst = ii;

@@ -68,6 +68,7 @@ struct surf_ctx {
     /* what surf_update_instances may change: instance records, TLAS, lights */
     uint32_t nMaterials = 0, nLightsUp = 0, tlasNodeCount = 0, maxBlasDepth = 0;
     std::map<std::tuple<uint32_t, uint32_t, uint32_t>, std::array<float4, 4>> blasRoots;  /* (node, idx, tri offset) -> root record */
+    std::map<uint32_t, std::array<double, 6>> blasBounds;   /* tri offset -> bounds of its BLAS's triangles (v0, v0+e1, v0+e2) */
     /* camera */
     bool hasCamera = false;
     DevCamera cam{};
@@ -957,6 +958,37 @@ int buildInstanceTables(surf_ctx* c, const surf_gpu_instance* instances, uint32_
         R.m3 = make_float4(m[3], m[7], m[11], m[15]);
         R.meta = make_uint4(D.nodeOffset, D.idxOffset, D.affineInv, i);
         R.r0 = root->second[0]; R.r1 = root->second[1]; R.r2 = root->second[2]; R.r3 = root->second[3];
+        /* conservative world box: the triangle bounds' corners under M (double),
+         * padded by 1e-4 of the box's coordinate magnitude (~1000x float
+         * rounding of the transforms, slab terms and the triangle test); not
+         * usable (never culls) for a projective M or non-finite bounds */
+        R.wlo = make_float4(0, 0, 0, 0);
+        R.whi = make_float4(0, 0, 0, 0);
+        const auto bb = c->blasBounds.find(g.tri_offset);
+        if (bb != c->blasBounds.end() && affine(g.transform)) {
+            const float* M = g.transform;    /* column-major object -> world */
+            double lo[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, hi[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
+            for (int corner = 0; corner < 8; ++corner) {
+                const double p[3] = {bb->second[(corner & 1) ? 3 : 0], bb->second[(corner & 2) ? 4 : 1], bb->second[(corner & 4) ? 5 : 2]};
+                for (int r = 0; r < 3; ++r) {
+                    const double w = (double)M[r] * p[0] + (double)M[4 + r] * p[1] + (double)M[8 + r] * p[2] + (double)M[12 + r];
+                    lo[r] = std::min(lo[r], w); hi[r] = std::max(hi[r], w);
+                }
+            }
+            double mag = 0.0;
+            for (int r = 0; r < 3; ++r) mag = std::max({mag, std::fabs(lo[r]), std::fabs(hi[r]), hi[r] - lo[r]});
+            const double pad = 1e-4 * mag + 1e-6;
+            bool ok = std::isfinite(mag) && mag < 1e30;
+            float flo[3], fhi[3];
+            for (int r = 0; r < 3; ++r) {
+                flo[r] = (float)(lo[r] - pad); fhi[r] = (float)(hi[r] + pad);
+                ok = ok && std::isfinite(flo[r]) && std::isfinite(fhi[r]);
+            }
+            if (ok) {
+                R.wlo = make_float4(flo[0], flo[1], flo[2], 1.0f);
+                R.whi = make_float4(fhi[0], fhi[1], fhi[2], 0.0f);
+            }
+        }
     }
     T.tnodes.assign((size_t)nTlas * 4, make_float4(0, 0, 0, 0));
     std::vector<uint8_t> tseen(n, 0);
@@ -1044,6 +1076,18 @@ int surf_upload_scene(surf_ctx* c, const surf_scene_desc* d) {
         tris[3 * (size_t)k + 0] = make_float4(T.v0.x, T.v0.y, T.v0.z, u2f(d->blas_indices[k]));
         tris[3 * (size_t)k + 1] = make_float4(T.v1.x - T.v0.x, T.v1.y - T.v0.y, T.v1.z - T.v0.z, 0.0f);
         tris[3 * (size_t)k + 2] = make_float4(T.v2.x - T.v0.x, T.v2.y - T.v0.y, T.v2.z - T.v0.z, 0.0f);
+    }
+    /* object-space bounds of each BLAS's triangles as the traversal sees them
+     * (v0, v0 + e1, v0 + e2 of the slot records), for the world-box cull */
+    c->blasBounds.clear();
+    for (uint32_t k = 0; k < d->blas_index_count; ++k) {
+        if (idxTri[k] < 0) continue;
+        auto it = c->blasBounds.emplace((uint32_t)idxTri[k], std::array<double, 6>{HUGE_VAL, HUGE_VAL, HUGE_VAL, -HUGE_VAL, -HUGE_VAL, -HUGE_VAL}).first;
+        const float4 a = tris[3 * (size_t)k], e1 = tris[3 * (size_t)k + 1], e2 = tris[3 * (size_t)k + 2];
+        const double v[3][3] = {{a.x, a.y, a.z}, {(double)a.x + e1.x, (double)a.y + e1.y, (double)a.z + e1.z},
+                                {(double)a.x + e2.x, (double)a.y + e2.y, (double)a.z + e2.z}};
+        for (const auto& p : v)
+            for (int q = 0; q < 3; ++q) { it->second[q] = std::min(it->second[q], p[q]); it->second[3 + q] = std::max(it->second[3 + q], p[q]); }
     }
     std::vector<float4> normals((size_t)d->triangle_count * 3), verts((size_t)d->triangle_count * 4);
     for (uint32_t t = 0; t < d->triangle_count; ++t) {
