@@ -667,7 +667,7 @@ __device__ __forceinline__ bool leafWave(const float4* tri, uint32_t lf, uint32_
 #if SURF_SEG_TIMING
 __device__ unsigned long long g_segStats[8];
 #endif
-struct SegStats { unsigned long long cycInst, cycLoop, visits, leaves, tris, entered; };
+struct SegStats { unsigned long long cycInst, cycLoop, visits, leaves, tris, entered, cycWait, cycLeaf; };
 
 /* Lanes-as-planes slab distances of the record held in row `row` (lanes
  * 16 row .. 16 row + 13) of v: the DPP moves of slabPair stay inside a row of
@@ -745,16 +745,20 @@ __device__ __forceinline__ void waitLoadsAfter(float& v, float a, float b) {
 template <bool ANY, bool FIN>
 __device__ __forceinline__ bool blasWalk(const DevScene& S, uint32_t nodeOff, const float4* tri, V3 o, V3 d, V3 rd,
                                          float dn, float df, uint32_t cn, uint32_t cf, float& depth, float& hu, float& hv,
-                                         uint32_t& hprim, SegStats* ss) {
+                                         uint32_t& hprim, float* rs, SegStats* ss) {
     const uint32_t lane = __lane_id(), l16 = lane & 15u;
     const uint32_t dw = planeDword(l16), ax = l16 < 12u ? (l16 % 6u) >> 1 : 0u;
     const uint32_t half = (lane >> 4) & 1u;
     const float oA = pick3(o, ax), rdA = pick3(rd, ax);
     const float* nodesF = reinterpret_cast<const float*>(S.nodes);
-    uint32_t stk = 0, sp = 0;
-    if (df != kFarAway) { stk = lane == sp ? cf : stk; ++sp; }
-    float cur = nodesF[16u * cn + dw];
-    uint32_t row = 0;
+    /* the root's children: both records (rows 0/1), the far one to the stack */
+    const uint32_t cmin = cn < cf ? cn : cf;
+    float cur = nodesF[16u * (cmin + half) + dw];
+    uint32_t row = cn - cmin, sp = 0;
+    if (df != kFarAway) {
+        if (half != row && lane < 32u) rs[l16] = cur;
+        sp = 1;
+    }
     bool any = false;
 #if SURF_SEG_TIMING
     if (ss) ++ss->entered;
@@ -766,31 +770,46 @@ __device__ __forceinline__ bool blasWalk(const DevScene& S, uint32_t nodeOff, co
         if (ss) { if (cnt) { ++ss->leaves; ss->tris += cnt; } else ++ss->visits; }
 #endif
         if (cnt != 0u) {
-            if (leafWave<ANY>(tri, lf, cnt, o, d, depth, hu, hv, hprim)) {
+#if SURF_SEG_TIMING
+            const unsigned long long tl0 = __builtin_readcyclecounter();
+#endif
+            const bool lh = leafWave<ANY>(tri, lf, cnt, o, d, depth, hu, hv, hprim);
+#if SURF_SEG_TIMING
+            if (ss) ss->cycLeaf += __builtin_readcyclecounter() - tl0;
+#endif
+            if (lh) {
                 if (ANY) return true;
                 any = true;
             }
             if (sp == 0u) break;
-            const uint32_t node = (uint32_t)__builtin_amdgcn_readlane((int)stk, (int)--sp);
-            cur = nodesF[16u * node + dw];
+            cur = rs[16u * --sp + l16];
             row = 0;
             continue;
         }
         const uint32_t c0 = nodeOff + lf;
         float nxt = loadEarly(nodesF + 16u * (c0 + half) + dw);
         slabPairRow<FIN>(cur, oA, rdA, depth, row, dn, df);
-        uint32_t far = c0 + 1u, nearRow = 0u;
-        if (dn > df) { const float t = dn; dn = df; df = t; far = c0; nearRow = 1u; }
+        uint32_t nearRow = 0u;
+        if (dn > df) { const float t = dn; dn = df; df = t; nearRow = 1u; }
+#if SURF_SEG_TIMING
+        const unsigned long long tw0 = __builtin_readcyclecounter();
+#endif
         waitLoadsAfter(nxt, dn, df);   /* on every path: the register must not be reused while the load is in flight */
+#if SURF_SEG_TIMING
+        if (ss) { asm volatile("" : "+v"(nxt)); ss->cycWait += __builtin_readcyclecounter() - tw0; }
+#endif
         if (dn == kFarAway) {
             if (sp == 0u) break;
-            const uint32_t node = (uint32_t)__builtin_amdgcn_readlane((int)stk, (int)--sp);
-            cur = nodesF[16u * node + dw];
+            cur = rs[16u * --sp + l16];
             row = 0;
         } else {
             cur = nxt;
             row = nearRow;
-            if (df != kFarAway) { stk = lane == sp ? far : stk; ++sp; }
+            /* the far child's record (already fetched, the other row) to the LDS stack */
+            if (df != kFarAway) {
+                if (half != nearRow && lane < 32u) rs[16u * sp + l16] = nxt;
+                ++sp;
+            }
         }
     }
     return any;
@@ -798,7 +817,7 @@ __device__ __forceinline__ bool blasWalk(const DevScene& S, uint32_t nodeOff, co
 
 template <bool ANY>
 __device__ __forceinline__ bool blasWave(const DevScene& S, const TraceInst& I, V3 o, V3 d, float& depth, float& hu, float& hv,
-                                         uint32_t& hprim, SegStats* ss = nullptr) {
+                                         uint32_t& hprim, float* rs, SegStats* ss = nullptr) {
     const uint32_t lane = __lane_id();
     const uint32_t nodeOff = I.meta.x;
     const float4* tri = S.tris + 3u * I.meta.y;
@@ -814,8 +833,8 @@ __device__ __forceinline__ bool blasWave(const DevScene& S, const TraceInst& I, 
     if (dn > df) { const float t = dn; dn = df; df = t; const uint32_t c = cn; cn = cf; cf = c; }
     if (dn == kFarAway) return false;
     if (S.finiteBoxes && finite3(o) && finite3(rd))
-        return blasWalk<ANY, true>(S, nodeOff, tri, o, d, rd, dn, df, cn, cf, depth, hu, hv, hprim, ss);
-    return blasWalk<ANY, false>(S, nodeOff, tri, o, d, rd, dn, df, cn, cf, depth, hu, hv, hprim, ss);
+        return blasWalk<ANY, true>(S, nodeOff, tri, o, d, rd, dn, df, cn, cf, depth, hu, hv, hprim, rs, ss);
+    return blasWalk<ANY, false>(S, nodeOff, tri, o, d, rd, dn, df, cn, cf, depth, hu, hv, hprim, rs, ss);
 }
 
 /* BvhTLAS::intersect / intersectAny over a single-leaf TLAS (bvh.cpp:654-778).
@@ -827,7 +846,7 @@ __device__ __forceinline__ bool blasWave(const DevScene& S, const TraceInst& I, 
  * readlanes instead of a serial transform, three divisions and a slab test. */
 template <bool ANY>
 __device__ __forceinline__ bool traceWave(const DevScene& S, const TraceTables& Tt, V3 o, V3 d, float& depth, float& hu,
-                                          float& hv, uint32_t& hinst, uint32_t& hprim, SegStats* ss = nullptr) {
+                                          float& hv, uint32_t& hinst, uint32_t& hprim, float* rs, SegStats* ss = nullptr) {
     bool any = false;
     const uint32_t nI = S.tlasLeafCount;
     if (nI > 64u) {
@@ -837,7 +856,7 @@ __device__ __forceinline__ bool traceWave(const DevScene& S, const TraceTables& 
             V3 oo = mk3(rowDot(I.m0, o.x, o.y, o.z, 1.0f), rowDot(I.m1, o.x, o.y, o.z, 1.0f), rowDot(I.m2, o.x, o.y, o.z, 1.0f));
             if (!I.meta.z) oo = divs(oo, rowDot(I.m3, o.x, o.y, o.z, 1.0f));
             const V3 dd = mk3(rowDot(I.m0, d.x, d.y, d.z, 0.0f), rowDot(I.m1, d.x, d.y, d.z, 0.0f), rowDot(I.m2, d.x, d.y, d.z, 0.0f));
-            if (blasWave<ANY>(S, I, oo, dd, depth, hu, hv, hprim, ss)) {
+            if (blasWave<ANY>(S, I, oo, dd, depth, hu, hv, hprim, rs, ss)) {
                 if (ANY) return true;
                 any = true;
                 hinst = ii;
@@ -893,8 +912,8 @@ __device__ __forceinline__ bool traceWave(const DevScene& S, const TraceTables& 
         } else {
             const V3 rk = mk3(bcast(rd.x, k), bcast(rd.y, k), bcast(rd.z, k));
             h = (S.finiteBoxes && finite3(ok) && finite3(rk))
-                    ? blasWalk<ANY, true>(S, nodeOff, tri, ok, dk, rk, dn, df, cn, cf, depth, hu, hv, hprim, ss)
-                    : blasWalk<ANY, false>(S, nodeOff, tri, ok, dk, rk, dn, df, cn, cf, depth, hu, hv, hprim, ss);
+                    ? blasWalk<ANY, true>(S, nodeOff, tri, ok, dk, rk, dn, df, cn, cf, depth, hu, hv, hprim, rs, ss)
+                    : blasWalk<ANY, false>(S, nodeOff, tri, ok, dk, rk, dn, df, cn, cf, depth, hu, hv, hprim, rs, ss);
         }
 #if SURF_SEG_TIMING
         if (ss) { const unsigned long long t1 = __builtin_readcyclecounter(); ss->cycLoop += t1 - t0; t0 = t1; }
@@ -1886,7 +1905,10 @@ __global__ __launch_bounds__(64, SURF_COOP_WAVES) void k_tail_coop(DevScene S, P
                                                   uint32_t* __restrict__ frameDone, uint32_t npx, uint32_t window, Counters* C,
                                                   uint32_t stackWords, uint32_t firstCounted) {
     extern __shared__ uint32_t lds[];
-    const TraceTables Tt = traceTables<LDS_TABLES>(S, lds, 2u * stackWords);
+    /* WAVE: the trace tables (instances x 180 B) always in LDS -- every lane of
+     * traceWave's prologue reads its own instance record; the shading tables
+     * (static, sized for 64 instances/materials) only with LDS_TABLES */
+    const TraceTables Tt = traceTables<LDS_TABLES || WAVE>(S, lds, 2u * stackWords);
     __shared__ DevInstance sInst[LDS_TABLES ? kLdsInst : 1];
     __shared__ DevMaterial sMat[LDS_TABLES ? kLdsMats : 1];
     __shared__ uint2 sLights[LDS_TABLES ? kLdsLights : 1];
@@ -1900,6 +1922,7 @@ __global__ __launch_bounds__(64, SURF_COOP_WAVES) void k_tail_coop(DevScene S, P
     const bool lead = threadIdx.x == 0;
     uint32_t* stk = lds + threadIdx.x;
     float* astk = reinterpret_cast<float*>(lds + stackWords) + threadIdx.x;
+    float* rstk = reinterpret_cast<float*>(lds);     /* WAVE: the record stack (16 words per entry) */
     const uint32_t stride = blockDim.x;
     const uint32_t maxSeg = C->maxSeg, zeroCutoff = C->zeroCutoff;
     float4 o4 = cur.o[i], d4 = cur.d[i], T4 = cur.T[i];
@@ -1907,7 +1930,7 @@ __global__ __launch_bounds__(64, SURF_COOP_WAVES) void k_tail_coop(DevScene S, P
     unsigned long long nExt = 0, nHit = 0, nCont = 0, nSh = 0, nAcc = 0, nUn = 0;
 #if SURF_SEG_TIMING
     unsigned long long cyc[3] = {0, 0, 0};
-    SegStats ss{0, 0, 0, 0, 0, 0};
+    SegStats ss{0, 0, 0, 0, 0, 0, 0, 0};
     SegStats* ssp = &ss;
 #else
     SegStats* ssp = nullptr;
@@ -1918,7 +1941,7 @@ __global__ __launch_bounds__(64, SURF_COOP_WAVES) void k_tail_coop(DevScene S, P
 #if SURF_SEG_TIMING
         const unsigned long long c0 = __builtin_readcyclecounter();
 #endif
-        const bool hit = WAVE ? traceWave<false>(S, Tt, xyz(o4), xyz(d4), depth, u, v, inst, prim, ssp)
+        const bool hit = WAVE ? traceWave<false>(S, Tt, xyz(o4), xyz(d4), depth, u, v, inst, prim, rstk, ssp)
                               : traceSceneCoop(S, Tt, xyz(o4), xyz(d4), depth, u, v, inst, prim, stk, astk, stride);
         (void)ssp;
         ++nExt;
@@ -1940,7 +1963,7 @@ __global__ __launch_bounds__(64, SURF_COOP_WAVES) void k_tail_coop(DevScene S, P
             if (WAVE) {
                 float sdep = r.so.w, su = 0.0f, sv = 0.0f;
                 uint32_t si = kUnset, sp = kUnset;
-                occ = traceWave<true>(S, Tt, xyz(r.so), xyz(r.sd), sdep, su, sv, si, sp);
+                occ = traceWave<true>(S, Tt, xyz(r.so), xyz(r.sd), sdep, su, sv, si, sp, rstk);
             } else {
                 occ = traceAnyCoop(S, Tt, xyz(r.so), xyz(r.sd), r.so.w, stk, stride);
             }
@@ -1978,6 +2001,7 @@ __global__ __launch_bounds__(64, SURF_COOP_WAVES) void k_tail_coop(DevScene S, P
         atomicAdd(&C->dbg[3], nExt); atomicAdd(&C->dbg[4], nSh);
         atomicAdd(&g_segStats[0], ss.cycInst); atomicAdd(&g_segStats[1], ss.cycLoop); atomicAdd(&g_segStats[2], ss.visits);
         atomicAdd(&g_segStats[3], ss.leaves); atomicAdd(&g_segStats[4], ss.tris); atomicAdd(&g_segStats[5], ss.entered);
+        atomicAdd(&g_segStats[6], ss.cycWait); atomicAdd(&g_segStats[7], ss.cycLeaf);
 #endif
     }
 }
@@ -2088,7 +2112,7 @@ __global__ __launch_bounds__(64) void k_trace_closest_coop(DevScene S, const flo
     float depth = kFarAway, u = 0.0f, v = 0.0f;
     uint32_t inst = kUnset, prim = kUnset;
     const V3 ro = mk3(o[3 * i], o[3 * i + 1], o[3 * i + 2]), rdir = mk3(d[3 * i], d[3 * i + 1], d[3 * i + 2]);
-    const bool hit = WAVE ? traceWave<false>(S, Tt, ro, rdir, depth, u, v, inst, prim)
+    const bool hit = WAVE ? traceWave<false>(S, Tt, ro, rdir, depth, u, v, inst, prim, reinterpret_cast<float*>(lds))
                           : traceSceneCoop(S, Tt, ro, rdir, depth, u, v, inst, prim, lds + threadIdx.x,
                                            reinterpret_cast<float*>(lds + stackWords) + threadIdx.x, blockDim.x);
     if (threadIdx.x == 0) {
@@ -2109,7 +2133,7 @@ __global__ __launch_bounds__(64) void k_trace_any_coop(DevScene S, const float* 
     if (WAVE) {
         float depth = tmaxv[i], u = 0.0f, v = 0.0f;
         uint32_t inst = kUnset, prim = kUnset;
-        oc = traceWave<true>(S, Tt, ro, rdir, depth, u, v, inst, prim);
+        oc = traceWave<true>(S, Tt, ro, rdir, depth, u, v, inst, prim, reinterpret_cast<float*>(lds));
     } else {
         oc = traceAnyCoop(S, Tt, ro, rdir, tmaxv[i], lds + threadIdx.x, blockDim.x);
     }

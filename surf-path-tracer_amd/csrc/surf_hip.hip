@@ -179,6 +179,8 @@ void destroyGraph(surf_ctx* c) {
 /* Dynamic LDS of a traversal kernel with `block` threads: the per-lane stack,
  * then (LDS tables) the TraceInst table and the TLAS index array. */
 uint32_t stackWords(const surf_ctx* c, uint32_t block) { return c->stackDepth * block; }
+/* one-ray-per-wave traversal (traceWave): a stack of node records, 16 words per entry */
+uint32_t recStackWords(const surf_ctx* c) { return c->stackDepth * 16u; }
 size_t traversalLds(const surf_ctx* c, uint32_t block) {
     size_t b = (size_t)stackWords(c, block) * sizeof(uint32_t);
     if (c->ldsTables) b += (size_t)c->nInstances * (sizeof(TraceInst) + sizeof(uint32_t));
@@ -563,11 +565,13 @@ int runTail(surf_ctx* c, bool longPool) {
              * cap the one-wave blocks at ~2 waves per SIMD (SURF_COOP_LDS=1: A/B) */
             static const bool coopLds = std::getenv("SURF_COOP_LDS") && std::atoi(std::getenv("SURF_COOP_LDS")) != 0;
             if (waveEligible(c) && !coopLds)
-                hipLaunchKernelGGL((k_tail_coop<false, true>), dim3(cnt), dim3(64), 0, c->stream, c->S, in, cnt, c->rad, c->frameDone,
-                                   c->npx, c->window, c->ctr, 0u, firstCounted);
+                hipLaunchKernelGGL((k_tail_coop<false, true>), dim3(cnt), dim3(64),
+                                   traversalLds(c, 64) - (size_t)stackWords(c, 64) * sizeof(uint32_t) + (size_t)recStackWords(c) * sizeof(float),
+                                   c->stream, c->S, in, cnt, c->rad, c->frameDone, c->npx, c->window, c->ctr, recStackWords(c) / 2u, firstCounted);
             else if (waveEligible(c))
-                hipLaunchKernelGGL((k_tail_coop<true, true>), dim3(cnt), dim3(64), traversalLds(c, 64) - (size_t)stackWords(c, 64) * sizeof(uint32_t),
-                                   c->stream, c->S, in, cnt, c->rad, c->frameDone, c->npx, c->window, c->ctr, 0u, firstCounted);
+                hipLaunchKernelGGL((k_tail_coop<true, true>), dim3(cnt), dim3(64),
+                                   traversalLds(c, 64) - (size_t)stackWords(c, 64) * sizeof(uint32_t) + (size_t)recStackWords(c) * sizeof(float),
+                                   c->stream, c->S, in, cnt, c->rad, c->frameDone, c->npx, c->window, c->ctr, recStackWords(c) / 2u, firstCounted);
             else
                 hipLaunchKernelGGL((k_tail_coop<true, false>), dim3(cnt), dim3(64), traversalLds(c, 64) + (size_t)stackWords(c, 64) * sizeof(float),
                                    c->stream, c->S, in, cnt, c->rad, c->frameDone, c->npx, c->window, c->ctr, stackWords(c, 64), firstCounted);
@@ -608,7 +612,8 @@ int runTail(surf_ctx* c, bool longPool) {
         unsigned long long h[8];
         SURF_CHECK(c, hipMemcpyFromSymbol(h, HIP_SYMBOL(g_segStats), sizeof(h)));
         std::fprintf(stderr, "[surf tail] extend per segment: instance prologues %.0f cycles, BLAS loops %.0f cycles, %.1f interior visits, "
-                     "%.1f leaves, %.1f triangles, %.2f instances entered\n", h[0] / ns, h[1] / ns, h[2] / ns, h[3] / ns, h[4] / ns, h[5] / ns);
+                     "%.1f leaves, %.1f triangles, %.2f instances entered; %.0f cycles waiting for prefetched records, %.0f in leaves\n",
+                     h[0] / ns, h[1] / ns, h[2] / ns, h[3] / ns, h[4] / ns, h[5] / ns, h[6] / ns, h[7] / ns);
     }
 #endif
     if (longPool) {

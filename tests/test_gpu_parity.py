@@ -51,6 +51,39 @@ def test_closest_hit_records_bitexact(oracle_scene, product_scene, mode):
     assert (gpu[3] != UNSET).mean() > 0.9
 
 
+def test_boundary_rays_bitexact(oracle_scene, product_scene):
+    """Rays the instance cull and the slab fast paths must not get wrong: aimed
+    at surface points (hits at the end of a shadow segment, tmax exactly the
+    distance), grazing along axis planes (zero direction components: 1/d = inf),
+    and from outside the room toward it."""
+    W = H = 64
+    (eo, ed), _ = oracle_scene.record_rays(W, H, 2, 0, W * H)
+    t, _, _, inst, _ = oracle_scene.trace_closest(eo, ed)
+    hit = inst != UNSET
+    P = (eo[hit] + t[hit, None] * ed[hit])[:6000]
+    rng = np.random.default_rng(11)
+    src = rng.uniform([-12, -2, -12], [12, 11, 12], size=(len(P), 3)).astype(np.float32)
+    dv = (P - src).astype(np.float32)
+    dist = np.linalg.norm(dv, axis=1).astype(np.float32)
+    dn = (dv / dist[:, None]).astype(np.float32)
+    axis = np.zeros((3000, 3), np.float32)
+    axis[np.arange(3000), rng.integers(0, 3, 3000)] = rng.choice([-1.0, 1.0], 3000).astype(np.float32)
+    ao = rng.uniform([-9, -0.9, -9], [9, 8.9, 9], size=(3000, 3)).astype(np.float32)
+    o = np.concatenate([src, ao]).astype(np.float32)
+    d = np.concatenate([dn, axis]).astype(np.float32)
+    r = surf_amd.Renderer(product_scene, W, H)
+    for mode in (0, 2):
+        r.set_trace_mode(mode)
+        gpu = r.trace_closest(o, d)
+        cpu = oracle_scene.trace_closest(o, d)
+        for n, g, c in zip(["t", "u", "v", "inst", "prim"], gpu, cpu):
+            bad = np.nonzero(g.view(np.uint32) != c.view(np.uint32))[0]
+            assert len(bad) == 0, f"mode {mode} {n}: {len(bad)} of {len(g)} differ, first {bad[:5]}"
+        for tm in (dist, np.nextafter(dist, np.float32(0)), np.nextafter(dist, np.float32(np.inf))):
+            tmax = np.concatenate([tm, np.full(3000, 1e30, np.float32)]).astype(np.float32)
+            assert np.array_equal(r.trace_any(o, d, tmax), oracle_scene.trace_any(o, d, tmax)), f"mode {mode}"
+
+
 @pytest.mark.parametrize("mode", [0, 1, 2], ids=["lane-per-ray", "wave-per-ray", "wave-lanes-as-planes"])
 def test_any_hit_bitexact(oracle_scene, product_scene, mode):
     W = H = 96
