@@ -1018,10 +1018,18 @@ __global__ __launch_bounds__(kBlock) void k_bincount(const uint8_t* __restrict__
 
 /* Exclusive scan of the bin-major [kBins][blocks] counts: one block of 1024. */
 __global__ __launch_bounds__(1024) void k_binscan(uint32_t* __restrict__ hist, uint32_t total) {
+    constexpr uint32_t kPer = kBins * kSortBlocks / 1024u;    /* counts per thread (the host passes total = kBins x blocks) */
+    static_assert(kBins * kSortBlocks % 1024u == 0u, "scan layout");
     __shared__ uint32_t part[1024];
-    const uint32_t t = threadIdx.x, per = (total + 1023u) / 1024u, a = t * per, b = min(total, a + per);
+    const uint32_t t = threadIdx.x, a = t * kPer;
+    (void)total;
+    /* all kPer loads in flight at once (a rolled loop waited for each in turn: 20 us per launch) */
+    uint32_t c[kPer];
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; ++k) c[k] = hist[a + k];
     uint32_t sum = 0;
-    for (uint32_t k = a; k < b; ++k) sum += hist[k];
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; ++k) sum += c[k];
     part[t] = sum;
     __syncthreads();
     for (uint32_t off = 1; off < 1024u; off <<= 1) {
@@ -1031,7 +1039,8 @@ __global__ __launch_bounds__(1024) void k_binscan(uint32_t* __restrict__ hist, u
         __syncthreads();
     }
     uint32_t run = part[t] - sum;
-    for (uint32_t k = a; k < b; ++k) { const uint32_t c = hist[k]; hist[k] = run; run += c; }
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; ++k) { hist[a + k] = run; run += c[k]; }
 }
 
 __global__ __launch_bounds__(kBlock) void k_binscatter(const uint8_t* __restrict__ key, const Counters* C, int par, int which,
