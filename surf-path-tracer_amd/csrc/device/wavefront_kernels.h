@@ -707,6 +707,49 @@ __device__ __forceinline__ void slabPairRow(float v, float oA, float rdA, float 
     d1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dist), (int)(10u + 16u * row)));
 }
 
+/* slabPairRow's decision without leaving the vector unit: lane 10 of the row
+ * takes box 0's distance from lane 4 (DPP row_shr:6) and forms blasTrace's
+ * choices -- bit 0: the right child is nearer (dn > df), bit 1: the nearer
+ * child is hit, bit 2: the farther child is hit -- read out with one readlane
+ * (instead of two readlanes and float compares on scalar operands). */
+constexpr int kDppShr6 = 0x116;
+template <bool FIN>
+__device__ __forceinline__ uint32_t slabDecide(float v, float oA, float rdA, float depth, uint32_t row) {
+    const float t = (v - oA) * rdA;
+    float m0, m1;
+    if (FIN) {
+        float t0a, t1a;
+        asm volatile(
+            "s_nop 1\n\t"
+            "v_min_f32_dpp %0, %4, %4 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+            "v_max_f32_dpp %1, %4, %4 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+            "s_nop 1\n\t"
+            "v_max_f32_dpp %2, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf\n\t"
+            "v_min_f32_dpp %3, %1, %1 row_shr:4 row_mask:0xf bank_mask:0xf\n\t"
+            "s_nop 1\n\t"
+            "v_max_f32_dpp %2, %0, %2 row_shr:2 row_mask:0xf bank_mask:0xf\n\t"
+            "v_min_f32_dpp %3, %1, %3 row_shr:2 row_mask:0xf bank_mask:0xf"
+            : "=&v"(t0a), "=&v"(t1a), "=&v"(m0), "=&v"(m1)
+            : "v"(t));
+    } else {
+        const float tp = dppMov<kDppSwap1>(t);
+        const float t0a = tmin(t, tp), t1a = tmax(t, tp);
+        const float t0x = dppMov<kDppShr4>(t0a), t0y = dppMov<kDppShr2>(t0a);
+        const float t1x = dppMov<kDppShr4>(t1a), t1y = dppMov<kDppShr2>(t1a);
+        m0 = tmax(tmax(t0x, t0y), t0a);
+        m1 = tmin(tmin(t1x, t1y), t1a);
+    }
+    const float dist = (m1 >= m0 && m0 < depth && m1 > 0.0f) ? m0 : kFarAway;   /* never NaN */
+    const float d0 = dppMov<kDppShr6>(dist);          /* lane 10 <- lane 4: box 0 */
+    const bool sw = d0 > dist;                          /* if (dn > df) swap */
+    const float nearD = sw ? dist : d0, farD = sw ? d0 : dist;
+    const uint32_t bits = (sw ? 1u : 0u) | (nearD != kFarAway ? 2u : 0u) | (farD != kFarAway ? 4u : 0u);
+    return (uint32_t)__builtin_amdgcn_readlane((int)bits, (int)(10u + 16u * row));
+}
+__device__ __forceinline__ void waitLoadsAfterBits(float& v, uint32_t bits) {
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(v) : "s"(bits));
+}
+
 /* slab()'s t0 / t1 before its hit test: the same operations in the same order. */
 __device__ __forceinline__ void slabRange(float4 lo, float4 hi, V3 o, V3 rd, float& t0, float& t1) {
     const float tx0 = (lo.x - o.x) * rd.x, tx1 = (hi.x - o.x) * rd.x;
@@ -788,17 +831,16 @@ __device__ __forceinline__ bool blasWalk(const DevScene& S, uint32_t nodeOff, co
         }
         const uint32_t c0 = nodeOff + lf;
         float nxt = loadEarly(nodesF + 16u * (c0 + half) + dw);
-        slabPairRow<FIN>(cur, oA, rdA, depth, row, dn, df);
-        uint32_t nearRow = 0u;
-        if (dn > df) { const float t = dn; dn = df; df = t; nearRow = 1u; }
+        const uint32_t bits = slabDecide<FIN>(cur, oA, rdA, depth, row);
+        const uint32_t nearRow = bits & 1u;
 #if SURF_SEG_TIMING
         const unsigned long long tw0 = __builtin_readcyclecounter();
 #endif
-        waitLoadsAfter(nxt, dn, df);   /* on every path: the register must not be reused while the load is in flight */
+        waitLoadsAfterBits(nxt, bits);   /* on every path: the register must not be reused while the load is in flight */
 #if SURF_SEG_TIMING
         if (ss) { asm volatile("" : "+v"(nxt)); ss->cycWait += __builtin_readcyclecounter() - tw0; }
 #endif
-        if (dn == kFarAway) {
+        if (!(bits & 2u)) {
             if (sp == 0u) break;
             cur = rs[16u * --sp + l16];
             row = 0;
@@ -806,7 +848,7 @@ __device__ __forceinline__ bool blasWalk(const DevScene& S, uint32_t nodeOff, co
             cur = nxt;
             row = nearRow;
             /* the far child's record (already fetched, the other row) to the LDS stack */
-            if (df != kFarAway) {
+            if (bits & 4u) {
                 if (half != nearRow && lane < 32u) rs[16u * sp + l16] = nxt;
                 ++sp;
             }
