@@ -1954,6 +1954,109 @@ __global__ __launch_bounds__(kBlock, 2) void k_long(DevScene S, LongPools LP, fl
     }
 }
 
+/* k_long with one path per 64-lane block (traceWave, the cooperative tail's
+ * segment): same inputs, outputs, counters and queue protocol as k_long, for
+ * long paths whose per-segment latency, not their number, is what matters.
+ * LDS: the traversal's record stack (stackWords = 16 x depth), then the trace
+ * tables.  Shading tables from global memory (wave-uniform reads). */
+__global__ __launch_bounds__(64, SURF_COOP_WAVES) void k_long_wave(DevScene S, LongPools LP, float4* __restrict__ rad,
+                                                                   uint32_t* __restrict__ frameDone, uint32_t npx, uint32_t window,
+                                                                   Counters* C, uint32_t in, uint32_t eq, uint32_t stackWords) {
+    extern __shared__ uint32_t lds[];
+    const uint32_t nL = min(C->lpN[in], LP.lpCap), nE = min(C->escN[eq], LP.escCap), n = nL + nE;
+    if (blockIdx.x < n) {
+        __builtin_amdgcn_s_setprio(2);
+        const TraceTables Tt = stageTrace(S, lds, stackWords);
+        const ShadeTables Tb{S.inst, S.mats, S.lights};
+        float* rstk = reinterpret_cast<float*>(lds);
+        const bool lead = threadIdx.x == 0;
+        const uint32_t maxSeg = C->maxSeg, zeroCutoff = C->zeroCutoff, budget = C->longBudget;
+        const Pool src = LP.lp[in], dst = LP.lp[in ^ 1u];
+        const EscQ E = LP.esc[eq];
+        uint32_t* fd = frameDone + (blockIdx.x % kStripes) * window;
+        unsigned long long cExt = 0, cHit = 0, cCont = 0, cSh = 0, cAcc = 0, cUn = 0, cFin = 0;
+        for (uint32_t v = blockIdx.x; v < n; v += gridDim.x) {
+            float4 o4, d4, T4;
+            if (v < nL) {
+                o4 = src.o[v]; d4 = src.d[v]; T4 = src.T[v];
+            } else {
+                const uint32_t k = v - nL;
+                o4 = E.o[k]; d4 = E.d[k]; T4 = E.T[k];
+                const float4 sc = E.sc[k];
+                if (sc.w != 0.0f) {
+                    /* the escaping bounce's shadow ray (n_shadow counted by k_shade) */
+                    const float4 so = E.so[k], sd = E.sd[k];
+                    float sdep = so.w, su = 0.0f, sv = 0.0f;
+                    uint32_t si = kUnset, sp = kUnset;
+                    if (!traceWave<true>(S, Tt, xyz(so), xyz(sd), sdep, su, sv, si, sp, rstk)) {
+                        if (lead) addRadianceAtomic(rad, f2u(sd.w), xyz(sc));
+                        ++cUn; ++cAcc;
+                    }
+                }
+            }
+            bool alive = true;
+            for (uint32_t sgm = 0; sgm < budget; ++sgm) {
+                float depth = kFarAway, u = 0.0f, vv = 0.0f;
+                uint32_t inst = kUnset, prim = kUnset;
+                const bool hit = traceWave<false>(S, Tt, xyz(o4), xyz(d4), depth, u, vv, inst, prim, rstk);
+                ++cExt;
+                ShadeOut r;
+                shadePath(S, Tb, o4, d4, T4, make_float4(depth, u, vv, u2f(prim)), hit ? inst : kUnset, maxSeg, zeroCutoff, r);
+                if (lead && r.addRad) addRadianceAtomic(rad, f2u(o4.w), r.radd);
+                cHit += r.hitGeom; cAcc += r.accd;
+                if (r.shadow) {
+                    ++cSh;
+                    float sdep = r.so.w, su = 0.0f, sv = 0.0f;
+                    uint32_t si = kUnset, sp = kUnset;
+                    if (!traceWave<true>(S, Tt, xyz(r.so), xyz(r.sd), sdep, su, sv, si, sp, rstk)) {
+                        if (lead) addRadianceAtomic(rad, f2u(r.sd.w), xyz(r.sc));
+                        ++cUn; ++cAcc;
+                    }
+                }
+                if (lead && r.capped) {
+                    const unsigned long long kc = atomicAdd(&C->ev[7], 1ull);
+                    if (kc < 64) C->capped[kc] = f2u(o4.w);
+                }
+                if (!r.cont) {
+                    if (lead) atomicMax(&C->segMax, r.seg);
+                    alive = false;
+                    break;
+                }
+                ++cCont;
+                o4 = r.o; d4 = r.d; T4 = r.T;
+            }
+            if (lead) {
+                if (alive) {
+                    const uint32_t j = atomicAdd(&C->lpN[in ^ 1u], 1u);
+                    dst.o[j] = o4; dst.d[j] = d4; dst.T[j] = T4;
+                } else {
+                    __threadfence();
+                    atomicAdd(&fd[f2u(o4.w) / npx], 1u);
+                    atomicSub(&C->longPop, 1u);
+                    ++cFin;
+                }
+            }
+        }
+        if (lead) {
+            unsigned long long* ev = C->evS[blockIdx.x % kStripes];
+            const unsigned long long vals[7] = {cExt, cHit, cCont, cSh, cAcc, cUn, cFin};
+            const int idx[7] = {0, 1, 2, 3, 4, 5, 8};
+#pragma unroll
+            for (int q = 0; q < 7; ++q)
+                if (vals[q]) atomicAdd(&ev[idx[q]], vals[q]);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        if (atomicAdd(&C->lpDone, 1u) == gridDim.x - 1u) {
+            atomicExch(&C->lpN[in], 0u);
+            atomicExch(&C->escN[eq], 0u);
+            atomicExch(&C->lpDone, 0u);
+        }
+    }
+}
+
 /* Cooperative tail: one path per 64-lane wave (block), for the few very long
  * paths left at the end of a drain, whose single-lane segment latency bounds
  * the drain.  Each segment: closest hit with the instances traced in parallel

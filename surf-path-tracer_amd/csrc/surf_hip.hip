@@ -113,6 +113,8 @@ struct surf_ctx {
     /* long paths: escape queues + long pools, advanced by the k_long chain of the graph (surf_set_long_paths) */
     uint32_t longThresh = 0;       /* escape length (0 = off) */
     uint32_t longBudget = 8;       /* segments per long path per phase */
+    bool longWave = false;         /* k_long_wave (one path per wave) instead of k_long (SURF_LONG_WAVE=1) */
+    uint32_t longBlocks = 0;       /* k_long_wave grid (SURF_LONG_BLOCKS; default 4 waves per CU) */
     hipStream_t stream2 = nullptr; /* the k_long branch while the graph is captured */
     hipEvent_t evFork = nullptr, evShade[kPhasesPerGraph] = {}, evLong[kPhasesPerGraph] = {};
     LongPools LP{};
@@ -307,7 +309,10 @@ int allocWavefront(surf_ctx* c) {
     for (auto& e : c->pev) SURF_CHECK(c, hipEventCreate(&e));
     const uint64_t maxBlocks = (cap + kBlock - 1) / kBlock;
     c->gridWork = (uint32_t)std::min<uint64_t>(maxBlocks, (uint64_t)cus * 8);
-    c->coopMax = (uint32_t)cus * 4 * SURF_TAIL_WAVES;   /* resident k_tail waves: lanes per wave = paths / this */
+    c->coopMax = (uint32_t)cus * 4 * SURF_TAIL_WAVES;
+    c->longBlocks = (uint32_t)cus * 4;
+    if (const char* e = std::getenv("SURF_LONG_BLOCKS")) c->longBlocks = std::max(1, std::atoi(e));
+    if (const char* e = std::getenv("SURF_LONG_WAVE")) c->longWave = std::atoi(e) != 0;   /* resident k_tail waves: lanes per wave = paths / this */
     if (const char* e = std::getenv("SURF_DRAIN_REPLAYS")) c->drainReplays = std::max(1, std::atoi(e));    /* 3 waves per SIMD of the tail kernels (launch bounds) */
     c->gridRegen = (uint32_t)std::min<uint64_t>(maxBlocks, (uint64_t)cus * 8);
     c->allocated = true;
@@ -327,10 +332,16 @@ void launchSort(surf_ctx* c, const uint8_t* key, int par, int which) {
 }
 
 /* k_long for phase ph: lp[ph & 1] + esc[(ph - 1) % 4] -> lp[(ph + 1) & 1]. */
+bool waveEligible(const surf_ctx* c);
 void launchLong(surf_ctx* c, int ph, hipStream_t st) {
     const uint32_t in = (uint32_t)ph & 1u, eq = ((uint32_t)ph + 3u) & 3u;
     const size_t lds = traversalLds(c, kBlock);
-    if (c->ldsTables)
+    if (c->longWave && c->coopEligible && waveEligible(c)) {
+        /* one path per wave: the long paths' segment latency (surf_set_long_paths) */
+        hipLaunchKernelGGL(k_long_wave, dim3(c->longBlocks), dim3(64),
+                           traversalLds(c, 64) - (size_t)stackWords(c, 64) * sizeof(uint32_t) + (size_t)recStackWords(c) * sizeof(float),
+                           st, c->S, c->LP, c->rad, c->frameDone, c->npx, c->window, c->ctr, in, eq, recStackWords(c));
+    } else if (c->ldsTables)
         hipLaunchKernelGGL(k_long<true>, dim3(c->gridWork), dim3(kBlock), lds, st, c->S, c->LP, c->rad, c->frameDone, c->npx,
                            c->window, c->ctr, in, eq, stackWords(c, kBlock));
     else

@@ -154,14 +154,17 @@ def test_drain_policies_bitexact(oracle_scene, product_scene, policy):
     r0.close()
 
 
-@pytest.mark.parametrize("escape,per_phase", [(2, 1), (4, 8), (24, 8), (3, 64)],
-                         ids=["escape2-1seg", "escape4-8seg", "escape24-8seg", "escape3-64seg"])
-def test_long_path_worker_bitexact(oracle_scene, product_scene, escape, per_phase):
+@pytest.mark.parametrize("escape,per_phase,wave", [(2, 1, 0), (4, 8, 0), (24, 8, 0), (3, 64, 0), (4, 8, 1), (2, 3, 1)],
+                         ids=["escape2-1seg", "escape4-8seg", "escape24-8seg", "escape3-64seg", "wave-escape4-8seg",
+                              "wave-escape2-3seg"])
+def test_long_path_worker_bitexact(oracle_scene, product_scene, escape, per_phase, wave, monkeypatch):
     """Paths escaping the wavefront to the long pool (escape queues with the
     shadow ray carried along, the k_long chain of the phase graph, the staged
     tail over the long pool) give the oracle's radiance and event counts bit
-    for bit.  escape 2/3 pushes most paths through the long pool."""
+    for bit.  escape 2/3 pushes most paths through the long pool.  wave=1:
+    the one-path-per-wave long step (k_long_wave, SURF_LONG_WAVE=1)."""
     W, H, F = 128, 96, 6
+    monkeypatch.setenv("SURF_LONG_WAVE", str(wave))
     r = surf_amd.Renderer(product_scene, W, H, pool_capacity=8192)
     r.set_long_paths(escape, per_phase)
     r.render(2, 0, 0)
