@@ -2065,7 +2065,7 @@ __global__ __launch_bounds__(64, SURF_COOP_WAVES) void k_long_wave(DevScene S, L
  * lane 0 does the writes.  Identical results to k_tail.  LDS: traversal stack,
  * box-distance stack (stackWords words each), then the trace tables. */
 template <bool LDS_TABLES, bool WAVE>
-__global__ __launch_bounds__(64, SURF_COOP_WAVES) void k_tail_coop(DevScene S, Pool cur, uint32_t n, float4* __restrict__ rad,
+__global__ __launch_bounds__(64, LDS_TABLES ? 3 : SURF_COOP_WAVES) void k_tail_coop(DevScene S, Pool cur, uint32_t n, float4* __restrict__ rad,
                                                   uint32_t* __restrict__ frameDone, uint32_t npx, uint32_t window, Counters* C,
                                                   uint32_t stackWords, uint32_t firstCounted) {
     extern __shared__ uint32_t lds[];

@@ -974,26 +974,45 @@ int buildInstanceTables(surf_ctx* c, const surf_gpu_instance* instances, uint32_
         R.m3 = make_float4(m[3], m[7], m[11], m[15]);
         R.meta = make_uint4(D.nodeOffset, D.idxOffset, D.affineInv, i);
         R.r0 = root->second[0]; R.r1 = root->second[1]; R.r2 = root->second[2]; R.r3 = root->second[3];
-        /* conservative world box: the triangle bounds' corners under M (double),
-         * padded by 1e-4 of the box's coordinate magnitude (~1000x float
-         * rounding of the transforms, slab terms and the triangle test); not
-         * usable (never culls) for a projective M or non-finite bounds */
+        /* conservative world box: the triangle bounds' corners mapped to world
+         * space by the inverse of the M^-1 the traversal applies (inverted in
+         * double, so the box matches the object-space rays whatever M says),
+         * padded by 1e-4 of the box's coordinate magnitude times the matrix's
+         * condition number (~1000x the float rounding of the ray transform,
+         * slab terms and triangle test); not usable (never culls) for a
+         * projective or singular M^-1 or non-finite bounds */
         R.wlo = make_float4(0, 0, 0, 0);
         R.whi = make_float4(0, 0, 0, 0);
         const auto bb = c->blasBounds.find(g.tri_offset);
-        if (bb != c->blasBounds.end() && affine(g.transform)) {
-            const float* M = g.transform;    /* column-major object -> world */
+        double A[3][3], t[3], B[3][3];      /* M^-1 = [A t; 0 1] (column-major input), B = A^-1 */
+        for (int r = 0; r < 3; ++r) {
+            for (int q = 0; q < 3; ++q) A[r][q] = (double)g.inv_transform[4 * q + r];
+            t[r] = (double)g.inv_transform[12 + r];
+        }
+        const double det = A[0][0] * (A[1][1] * A[2][2] - A[1][2] * A[2][1]) - A[0][1] * (A[1][0] * A[2][2] - A[1][2] * A[2][0]) +
+                           A[0][2] * (A[1][0] * A[2][1] - A[1][1] * A[2][0]);
+        if (bb != c->blasBounds.end() && D.affineInv && std::isfinite(det) && det != 0.0) {
+            B[0][0] = (A[1][1] * A[2][2] - A[1][2] * A[2][1]) / det; B[0][1] = (A[0][2] * A[2][1] - A[0][1] * A[2][2]) / det;
+            B[0][2] = (A[0][1] * A[1][2] - A[0][2] * A[1][1]) / det; B[1][0] = (A[1][2] * A[2][0] - A[1][0] * A[2][2]) / det;
+            B[1][1] = (A[0][0] * A[2][2] - A[0][2] * A[2][0]) / det; B[1][2] = (A[0][2] * A[1][0] - A[0][0] * A[1][2]) / det;
+            B[2][0] = (A[1][0] * A[2][1] - A[1][1] * A[2][0]) / det; B[2][1] = (A[0][1] * A[2][0] - A[0][0] * A[2][1]) / det;
+            B[2][2] = (A[0][0] * A[1][1] - A[0][1] * A[1][0]) / det;
+            double na = 0.0, nb = 0.0;
+            for (int r = 0; r < 3; ++r)
+                for (int q = 0; q < 3; ++q) { na += A[r][q] * A[r][q]; nb += B[r][q] * B[r][q]; }
+            const double cond = std::sqrt(na * nb);
             double lo[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, hi[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
             for (int corner = 0; corner < 8; ++corner) {
-                const double p[3] = {bb->second[(corner & 1) ? 3 : 0], bb->second[(corner & 2) ? 4 : 1], bb->second[(corner & 4) ? 5 : 2]};
+                const double p[3] = {bb->second[(corner & 1) ? 3 : 0] - t[0], bb->second[(corner & 2) ? 4 : 1] - t[1],
+                                     bb->second[(corner & 4) ? 5 : 2] - t[2]};
                 for (int r = 0; r < 3; ++r) {
-                    const double w = (double)M[r] * p[0] + (double)M[4 + r] * p[1] + (double)M[8 + r] * p[2] + (double)M[12 + r];
+                    const double w = B[r][0] * p[0] + B[r][1] * p[1] + B[r][2] * p[2];
                     lo[r] = std::min(lo[r], w); hi[r] = std::max(hi[r], w);
                 }
             }
             double mag = 0.0;
             for (int r = 0; r < 3; ++r) mag = std::max({mag, std::fabs(lo[r]), std::fabs(hi[r]), hi[r] - lo[r]});
-            const double pad = 1e-4 * mag + 1e-6;
+            const double pad = 1e-4 * mag * std::max(1.0, cond) + 1e-6;
             bool ok = std::isfinite(mag) && mag < 1e30;
             float flo[3], fhi[3];
             for (int r = 0; r < 3; ++r) {
