@@ -1020,17 +1020,25 @@ __device__ __forceinline__ void blockCount(Counters* C, const int (&idx)[N], con
  * k_shade through order[]; hit records stay in order i, so the paths, their
  * results and the append order of the next pool are unchanged in content --
  * only the interleaving of lanes changes. */
-constexpr uint32_t kBins = 64;
+#ifndef SURF_POOL_DIR
+#define SURF_POOL_DIR 0            /* direction-sign bits in the pool key (0, 1: d.x, 2: d.x and d.z) */
+#endif
+constexpr uint32_t kBins = 64u << SURF_POOL_DIR;
 constexpr uint32_t kSortBlocks = 256;
+static_assert(kBins <= 256u, "pool/shadow keys are one byte");
 
 /* Pool order key: the instance the path starts on (<= 14; camera rays: kBins - 1)
  * x the x/z quadrant of the scene box holding its origin.  1 M recorded
  * extension rays (tools/order_probe.py, order_probe2.py): 634 us shuffled,
  * 345 by start instance, 334 by start x quadrant. */
-__device__ __forceinline__ uint8_t poolKey(const DevScene& S, uint32_t inst, float4 o) {
+__device__ __forceinline__ uint8_t poolKey(const DevScene& S, uint32_t inst, float4 o, float4 d) {
     const uint32_t cx = (o.x - S.cellLo[0]) * S.cellScale[0] >= 1.0f ? 1u : 0u;
     const uint32_t cz = (o.z - S.cellLo[2]) * S.cellScale[2] >= 1.0f ? 1u : 0u;
-    return (uint8_t)((inst < 14u ? inst : 14u) * 4u + cx + 2u * cz);
+    uint32_t k = (inst < 14u ? inst : 14u) * 4u + cx + 2u * cz;
+    if (SURF_POOL_DIR >= 1) k = k * 2u + (d.x < 0.0f ? 1u : 0u);
+    if (SURF_POOL_DIR >= 2) k = k * 2u + (d.z < 0.0f ? 1u : 0u);
+    (void)d;
+    return (uint8_t)k;
 }
 
 /* Shadow-ray order key: light slot (mod 2) x the octant cell of the scene box
@@ -1605,7 +1613,7 @@ __global__ __launch_bounds__(kBlock, SURF_SHADE_WAVES) void k_shade(DevScene S, 
         js += rankBelow(mSh);
         if (r.cont && !esc) {
             stS(&nxt.o[jc], r.o); stS(&nxt.d[jc], r.d); stS(&nxt.T[jc], r.T);
-            nxt.key[jc] = poolKey(S, hinst, r.o);   /* starts on the instance it hit, from this quadrant */
+            nxt.key[jc] = poolKey(S, hinst, r.o, r.d);   /* starts on the instance it hit, from this quadrant */
         }
         if (r.shadow && !esc) {
             stS(&Q.o[js], r.so); stS(&Q.d[js], r.sd); stS(&Q.c[js], r.sc);
