@@ -1113,6 +1113,27 @@ __global__ __launch_bounds__(kBlock) void k_binscatter(const uint8_t* __restrict
     for (uint32_t i = a + threadIdx.x; i < b; i += blockDim.x) order[atomicAdd(&base[key[i]], 1u)] = i;
 }
 
+/* Move variant of k_binscatter: the records themselves (three float4 streams:
+ * the pool's o, d, T or the shadow queue's o, d, c) are scattered to their
+ * sorted slot, so the consumers read them sequentially with no order[]
+ * indirection.  Reads are sequential, each lane's three 16-B writes land in
+ * the bin's run of slots. */
+struct Rec3 { const float4* a; const float4* b; const float4* c; };
+struct Rec3w { float4* a; float4* b; float4* c; };
+__global__ __launch_bounds__(kBlock) void k_binmove(const uint8_t* __restrict__ key, const Counters* C, int par, int which,
+                                                    const uint32_t* __restrict__ hist, Rec3 src, Rec3w dst) {
+    __shared__ uint32_t base[kBins];
+    if (threadIdx.x < kBins) base[threadIdx.x] = hist[threadIdx.x * gridDim.x + blockIdx.x];
+    __syncthreads();
+    uint32_t a, b;
+    sortChunk(sortCount(C, par, which), a, b);
+    for (uint32_t i = a + threadIdx.x; i < b; i += blockDim.x) {
+        const float4 x = ldS(&src.a[i]), y = ldS(&src.b[i]), z = ldS(&src.c[i]);
+        const uint32_t p = atomicAdd(&base[key[i]], 1u);
+        stS(&dst.a[p], x); stS(&dst.b[p], y); stS(&dst.c[p], z);
+    }
+}
+
 /* ------------------------------------------------------------------ kernels */
 template <bool LDS>
 __global__ __launch_bounds__(kBlock, SURF_TRACE_WAVES) void k_extend(DevScene S, Pool cur, float4* __restrict__ hitTUV,

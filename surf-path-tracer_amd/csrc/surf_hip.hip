@@ -110,6 +110,9 @@ struct surf_ctx {
     int traceMode = 0;             /* surf_trace_closest/_any: 0 one ray per lane, 1 one ray per wave */
     bool persistent = false;       /* out-of-step lanes with per-wave ray ranges: measured 4x slower */
     bool sortRays = true;          /* order each phase's rays by start instance (SURF_SORT=0: off) */
+    bool moveRays = false;         /* sort by moving the records into srt/srtQ instead of indexing them (SURF_SORT_MOVE=1) */
+    Pool srt{};                    /* the phase's pool in sorted order (moveRays) */
+    ShadowQ srtQ{};                /* the phase's shadow queue in sorted order (moveRays) */
     /* long paths: escape queues + long pools, advanced by the k_long chain of the graph (surf_set_long_paths) */
     uint32_t longThresh = 0;       /* escape length (0 = off) */
     uint32_t longBudget = 8;       /* segments per long path per phase */
@@ -268,6 +271,11 @@ int allocWavefront(surf_ctx* c) {
         if ((rc = devAlloc(c, c->wfAllocs, &c->pool[p].key, cap))) return rc;
     }
     if ((rc = devAlloc(c, c->wfAllocs, &c->order, cap))) return rc;
+    if (c->moveRays) {
+        if ((rc = devAlloc(c, c->wfAllocs, &c->srt.o, cap))) return rc;
+        if ((rc = devAlloc(c, c->wfAllocs, &c->srt.d, cap))) return rc;
+        if ((rc = devAlloc(c, c->wfAllocs, &c->srt.T, cap))) return rc;
+    }
     if ((rc = devAlloc(c, c->wfAllocs, &c->binHist, (size_t)kBins * kSortBlocks))) return rc;
     /* grid: 8 workgroups of 256 per CU saturate the 256-CU chip; grid-stride beyond */
     int cus = 256;
@@ -299,6 +307,11 @@ int allocWavefront(surf_ctx* c) {
     if ((rc = devAlloc(c, c->wfAllocs, &c->Q.d, cap))) return rc;
     if ((rc = devAlloc(c, c->wfAllocs, &c->Q.c, cap))) return rc;
     if ((rc = devAlloc(c, c->wfAllocs, &c->Q.key, cap))) return rc;
+    if (c->moveRays) {
+        if ((rc = devAlloc(c, c->wfAllocs, &c->srtQ.o, cap))) return rc;
+        if ((rc = devAlloc(c, c->wfAllocs, &c->srtQ.d, cap))) return rc;
+        if ((rc = devAlloc(c, c->wfAllocs, &c->srtQ.c, cap))) return rc;
+    }
     if ((rc = devAlloc(c, c->wfAllocs, &c->rad, (size_t)c->npx * c->window))) return rc;
     if ((rc = devAlloc(c, c->wfAllocs, &c->ctr, 1))) return rc;
     if ((rc = devAlloc(c, c->wfAllocs, &c->frameDone, (size_t)kStripes * c->window))) return rc;
@@ -329,6 +342,18 @@ void launchSort(surf_ctx* c, const uint8_t* key, int par, int which) {
     hipLaunchKernelGGL(k_binscan, dim3(1), dim3(1024), 0, c->stream, c->binHist, kBins * kSortBlocks);
     hipLaunchKernelGGL(k_binscatter, dim3(kSortBlocks), dim3(kBlock), 0, c->stream, key, (const Counters*)c->ctr, par, which,
                        (const uint32_t*)c->binHist, c->order);
+}
+
+/* The same sort, moving the records: pool (which 0) -> c->srt, shadow queue (which 1) -> c->srtQ. */
+void launchMove(surf_ctx* c, int par, int which) {
+    const uint8_t* key = which ? c->Q.key : c->pool[par].key;
+    hipLaunchKernelGGL(k_bincount, dim3(kSortBlocks), dim3(kBlock), 0, c->stream, key, (const Counters*)c->ctr, par, which,
+                       c->binHist);
+    hipLaunchKernelGGL(k_binscan, dim3(1), dim3(1024), 0, c->stream, c->binHist, kBins * kSortBlocks);
+    const Rec3 src = which ? Rec3{c->Q.o, c->Q.d, c->Q.c} : Rec3{c->pool[par].o, c->pool[par].d, c->pool[par].T};
+    const Rec3w dst = which ? Rec3w{c->srtQ.o, c->srtQ.d, c->srtQ.c} : Rec3w{c->srt.o, c->srt.d, c->srt.T};
+    hipLaunchKernelGGL(k_binmove, dim3(kSortBlocks), dim3(kBlock), 0, c->stream, key, (const Counters*)c->ctr, par, which,
+                       (const uint32_t*)c->binHist, src, dst);
 }
 
 /* k_long for phase ph: lp[ph & 1] + esc[(ph - 1) % 4] -> lp[(ph + 1) & 1]. */
@@ -365,28 +390,33 @@ void launchPhase(surf_ctx* c, int ph, hipEvent_t* ev, bool capture) {
     if (ev) (void)hipEventRecord(ev[0], c->stream);
     const bool persistent = c->persistent && c->ldsTables && c->S.tlasLeafCount > 0;
     const uint32_t* order = nullptr;
-    if (c->sortRays && !persistent) {
+    const bool sorted = c->sortRays && !persistent, move = sorted && c->moveRays;
+    Pool cur = c->pool[par];                     /* the pool k_extend / k_shade read */
+    if (move) {
+        launchMove(c, par, 0);
+        cur = c->srt;
+    } else if (sorted) {
         launchSort(c, c->pool[par].key, par, 0);
         order = c->order;
     }
     if (persistent)
-        hipLaunchKernelGGL(k_extend_p<true>, dim3(c->gridWork), dim3(kBlock), lds, c->stream, c->S, c->pool[par], c->hitTUV,
+        hipLaunchKernelGGL(k_extend_p<true>, dim3(c->gridWork), dim3(kBlock), lds, c->stream, c->S, cur, c->hitTUV,
                            c->hitInst, (const Counters*)c->ctr, par, sw);
     else if (c->ldsTables)
-        hipLaunchKernelGGL(k_extend<true>, dim3(c->gridWork), dim3(kBlock), lds, c->stream, c->S, c->pool[par], c->hitTUV,
+        hipLaunchKernelGGL(k_extend<true>, dim3(c->gridWork), dim3(kBlock), lds, c->stream, c->S, cur, c->hitTUV,
                            c->hitInst, (const Counters*)c->ctr, par, sw, order);
     else
-        hipLaunchKernelGGL(k_extend<false>, dim3(c->gridWork), dim3(kBlock), lds, c->stream, c->S, c->pool[par], c->hitTUV,
+        hipLaunchKernelGGL(k_extend<false>, dim3(c->gridWork), dim3(kBlock), lds, c->stream, c->S, cur, c->hitTUV,
                            c->hitInst, (const Counters*)c->ctr, par, sw, order);
     if (ev) (void)hipEventRecord(ev[1], c->stream);
     if (lng && capture && ph >= 3) (void)hipStreamWaitEvent(c->stream, c->evLong[ph - 3], 0);
     const uint32_t escQ = (uint32_t)ph & 3u;
     if (c->ldsTables)
-        hipLaunchKernelGGL(k_shade<true>, dim3(c->gridWork), dim3(kBlock), 0, c->stream, c->S, c->pool[par], c->pool[par ^ 1],
+        hipLaunchKernelGGL(k_shade<true>, dim3(c->gridWork), dim3(kBlock), 0, c->stream, c->S, cur, c->pool[par ^ 1],
                            c->hitTUV, (const uint32_t*)c->hitInst, c->Q, c->rad, c->frameDone, c->npx, c->window, c->ctr, par,
                            c->LP, escQ, order);
     else
-        hipLaunchKernelGGL(k_shade<false>, dim3(c->gridWork), dim3(kBlock), 0, c->stream, c->S, c->pool[par], c->pool[par ^ 1],
+        hipLaunchKernelGGL(k_shade<false>, dim3(c->gridWork), dim3(kBlock), 0, c->stream, c->S, cur, c->pool[par ^ 1],
                            c->hitTUV, (const uint32_t*)c->hitInst, c->Q, c->rad, c->frameDone, c->npx, c->window, c->ctr, par,
                            c->LP, escQ, order);
     if (lng && capture && ph + 1 < kPhasesPerGraph) {
@@ -397,13 +427,21 @@ void launchPhase(surf_ctx* c, int ph, hipEvent_t* ev, bool capture) {
     }
     if (ev) (void)hipEventRecord(ev[2], c->stream);
     /* shadow rays toward the same light together (the pool order no longer needed: reuse it) */
-    if (order) launchSort(c, c->Q.key, par, 1);
+    ShadowQ q = c->Q;
+    const uint32_t* qorder = nullptr;
+    if (move) {
+        launchMove(c, par, 1);
+        q = c->srtQ;
+    } else if (sorted) {
+        launchSort(c, c->Q.key, par, 1);
+        qorder = c->order;
+    }
     if (c->ldsTables)
-        hipLaunchKernelGGL(k_connect<true>, dim3(c->gridWork), dim3(kBlock), lds, c->stream, c->S, c->Q, c->rad, c->ctr, par, sw,
-                           (const uint32_t*)order);
+        hipLaunchKernelGGL(k_connect<true>, dim3(c->gridWork), dim3(kBlock), lds, c->stream, c->S, q, c->rad, c->ctr, par, sw,
+                           qorder);
     else
-        hipLaunchKernelGGL(k_connect<false>, dim3(c->gridWork), dim3(kBlock), lds, c->stream, c->S, c->Q, c->rad, c->ctr, par, sw,
-                           (const uint32_t*)order);
+        hipLaunchKernelGGL(k_connect<false>, dim3(c->gridWork), dim3(kBlock), lds, c->stream, c->S, q, c->rad, c->ctr, par, sw,
+                           qorder);
     if (ev) (void)hipEventRecord(ev[3], c->stream);
     hipLaunchKernelGGL(k_regen, dim3(c->gridRegen), dim3(kBlock), 0, c->stream, c->cam, c->pool[par ^ 1], c->rad, c->ctr, par,
                        c->capacity, geom(c));
@@ -750,6 +788,7 @@ int createCtx(int dev, uint32_t w, uint32_t h, std::vector<uint32_t> rows, surf_
     auto* c = new surf_ctx();
     c->device = dev;
     if (const char* e = std::getenv("SURF_SORT")) c->sortRays = e[0] != '0';
+    if (const char* e = std::getenv("SURF_SORT_MOVE")) c->moveRays = e[0] != '0';
     c->width = w;
     c->height = h;
     c->rows = std::move(rows);
