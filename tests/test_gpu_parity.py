@@ -182,6 +182,28 @@ def test_long_path_worker_bitexact(oracle_scene, product_scene, escape, per_phas
     r.close()
 
 
+@pytest.mark.parametrize("sort,move", [("0", "0"), ("1", "0"), ("1", "1")], ids=["unsorted", "order-index", "order-move"])
+def test_ray_order_modes_bitexact(oracle_scene, product_scene, sort, move, monkeypatch):
+    """The ray order is lane interleaving only: no sort (SURF_SORT=0), the
+    order[] gather (default) and the moved records (SURF_SORT_MOVE=1,
+    k_binmove) all give the oracle's radiance and event counts bit for bit."""
+    W, H, F = 128, 96, 4
+    monkeypatch.setenv("SURF_SORT", sort)
+    monkeypatch.setenv("SURF_SORT_MOVE", move)
+    r = surf_amd.Renderer(product_scene, W, H, pool_capacity=8192)
+    r.render(F, 0, 0)
+    g = r.accumulator()
+    st = r.stats()
+    oracle.set_zero_cutoff(True)
+    try:
+        c2, cnt, _ = oracle_scene.render(W, H, F)
+    finally:
+        oracle.set_zero_cutoff(False)
+    _assert_bitexact(g, c2, f"ray order sort={sort} move={move}")
+    _assert_counts(st, cnt)
+    r.close()
+
+
 def test_long_path_worker_full_frame(oracle_scene, product_scene):
     """1280x720 with long paths on: a band of rows against the oracle."""
     W, H, F = 1280, 720, 2
