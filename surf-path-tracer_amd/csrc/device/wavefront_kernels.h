@@ -38,7 +38,7 @@ constexpr uint32_t kFlagMedium = 1u, kFlagSpecular = 2u;
 constexpr int kBlock = 256;
 /* Minimum waves per SIMD the register allocator must allow (occupancy). */
 #ifndef SURF_SHADE_WAVES
-#define SURF_SHADE_WAVES 3
+#define SURF_SHADE_WAVES 4
 #endif
 #ifndef SURF_SEG_TIMING
 #define SURF_SEG_TIMING 0
@@ -47,7 +47,7 @@ constexpr int kBlock = 256;
 #define SURF_TAIL_WAVES 3          /* k_tail waves per SIMD (2, 3: same speed; 4, 6: slower) */
 #endif
 #ifndef SURF_TRACE_WAVES
-#define SURF_TRACE_WAVES 1
+#define SURF_TRACE_WAVES 2
 #endif
 #ifndef SURF_COOP_WAVES
 #define SURF_COOP_WAVES 4          /* k_tail_coop waves per SIMD (launch bounds; 3: 136 VGPRs, 5: spills) */
