@@ -130,7 +130,7 @@ struct surf_ctx {
     /* graph */
     hipGraphExec_t graphExec = nullptr;
     hipGraph_t graph = nullptr;
-    uint32_t gridWork = 0, gridRegen = 0;
+    uint32_t gridWork = 0, gridRegen = 0, gridExtend = 0, gridConnect = 0;
 
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipEvent_t pev[kPhasesPerGraph * 4 + 1] = {};
@@ -321,7 +321,17 @@ int allocWavefront(surf_ctx* c) {
         return fail(c, SURF_ERR_OOM, "hipHostMalloc of the counter block failed");
     for (auto& e : c->pev) SURF_CHECK(c, hipEventCreate(&e));
     const uint64_t maxBlocks = (cap + kBlock - 1) / kBlock;
-    c->gridWork = (uint32_t)std::min<uint64_t>(maxBlocks, (uint64_t)cus * 8);
+    uint64_t perCu = 8;                                   /* workgroups per CU of the wavefront kernels (SURF_GRID_PER_CU) */
+    if (const char* e = std::getenv("SURF_GRID_PER_CU")) perCu = (uint64_t)std::max(1, std::atoi(e));
+    c->gridWork = (uint32_t)std::min<uint64_t>(maxBlocks, (uint64_t)cus * perCu);
+    /* per-kernel grids (measured): k_extend gains from one ray per
+     * thread (latency hiding across many short-lived blocks), k_connect peaks
+     * at 12 workgroups per CU, k_shade at 8 */
+    uint64_t extPerCu = 48, conPerCu = 12;
+    if (const char* e = std::getenv("SURF_GRID_EXTEND")) extPerCu = (uint64_t)std::max(1, std::atoi(e));
+    if (const char* e = std::getenv("SURF_GRID_CONNECT")) conPerCu = (uint64_t)std::max(1, std::atoi(e));
+    c->gridExtend = (uint32_t)std::min<uint64_t>(maxBlocks, (uint64_t)cus * extPerCu);
+    c->gridConnect = (uint32_t)std::min<uint64_t>(maxBlocks, (uint64_t)cus * conPerCu);
     c->coopMax = (uint32_t)cus * 4 * SURF_TAIL_WAVES;
     c->longBlocks = (uint32_t)cus * 4;
     if (const char* e = std::getenv("SURF_LONG_BLOCKS")) c->longBlocks = std::max(1, std::atoi(e));
@@ -403,10 +413,10 @@ void launchPhase(surf_ctx* c, int ph, hipEvent_t* ev, bool capture) {
         hipLaunchKernelGGL(k_extend_p<true>, dim3(c->gridWork), dim3(kBlock), lds, c->stream, c->S, cur, c->hitTUV,
                            c->hitInst, (const Counters*)c->ctr, par, sw);
     else if (c->ldsTables)
-        hipLaunchKernelGGL(k_extend<true>, dim3(c->gridWork), dim3(kBlock), lds, c->stream, c->S, cur, c->hitTUV,
+        hipLaunchKernelGGL(k_extend<true>, dim3(c->gridExtend), dim3(kBlock), lds, c->stream, c->S, cur, c->hitTUV,
                            c->hitInst, (const Counters*)c->ctr, par, sw, order);
     else
-        hipLaunchKernelGGL(k_extend<false>, dim3(c->gridWork), dim3(kBlock), lds, c->stream, c->S, cur, c->hitTUV,
+        hipLaunchKernelGGL(k_extend<false>, dim3(c->gridExtend), dim3(kBlock), lds, c->stream, c->S, cur, c->hitTUV,
                            c->hitInst, (const Counters*)c->ctr, par, sw, order);
     if (ev) (void)hipEventRecord(ev[1], c->stream);
     if (lng && capture && ph >= 3) (void)hipStreamWaitEvent(c->stream, c->evLong[ph - 3], 0);
@@ -437,10 +447,10 @@ void launchPhase(surf_ctx* c, int ph, hipEvent_t* ev, bool capture) {
         qorder = c->order;
     }
     if (c->ldsTables)
-        hipLaunchKernelGGL(k_connect<true>, dim3(c->gridWork), dim3(kBlock), lds, c->stream, c->S, q, c->rad, c->ctr, par, sw,
+        hipLaunchKernelGGL(k_connect<true>, dim3(c->gridConnect), dim3(kBlock), lds, c->stream, c->S, q, c->rad, c->ctr, par, sw,
                            qorder);
     else
-        hipLaunchKernelGGL(k_connect<false>, dim3(c->gridWork), dim3(kBlock), lds, c->stream, c->S, q, c->rad, c->ctr, par, sw,
+        hipLaunchKernelGGL(k_connect<false>, dim3(c->gridConnect), dim3(kBlock), lds, c->stream, c->S, q, c->rad, c->ctr, par, sw,
                            qorder);
     if (ev) (void)hipEventRecord(ev[3], c->stream);
     hipLaunchKernelGGL(k_regen, dim3(c->gridRegen), dim3(kBlock), 0, c->stream, c->cam, c->pool[par ^ 1], c->rad, c->ctr, par,
