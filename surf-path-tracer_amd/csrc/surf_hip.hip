@@ -60,6 +60,7 @@ struct surf_ctx {
 
     /* scene */
     bool hasScene = false;
+    bool connectGlobal = false;    /* k_connect reads its tables from global memory (SURF_CONNECT_GLOBAL=1, tuning) */
     bool ldsTables = false;        /* instance/material/light tables fit the per-workgroup LDS copy */
     DevScene S{};
     std::vector<void*> sceneAllocs;
@@ -446,7 +447,7 @@ void launchPhase(surf_ctx* c, int ph, hipEvent_t* ev, bool capture) {
         launchSort(c, c->Q.key, par, 1);
         qorder = c->order;
     }
-    if (c->ldsTables)
+    if (c->ldsTables && !c->connectGlobal)
         hipLaunchKernelGGL(k_connect<true>, dim3(c->gridConnect), dim3(kBlock), lds, c->stream, c->S, q, c->rad, c->ctr, par, sw,
                            qorder);
     else
@@ -799,6 +800,7 @@ int createCtx(int dev, uint32_t w, uint32_t h, std::vector<uint32_t> rows, surf_
     c->device = dev;
     if (const char* e = std::getenv("SURF_SORT")) c->sortRays = e[0] != '0';
     if (const char* e = std::getenv("SURF_SORT_MOVE")) c->moveRays = e[0] != '0';
+    if (const char* e = std::getenv("SURF_CONNECT_GLOBAL")) c->connectGlobal = e[0] != '0';
     c->width = w;
     c->height = h;
     c->rows = std::move(rows);
