@@ -33,7 +33,7 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 EXTEND_BYTES_PER_RAY = 52
 # rocprofv3 PMC summary of this bench command (tools/profile_round.sh + tools/summarize_profile.py):
 # HBM bytes per k_extend launch, FETCH_SIZE x2 + WRITE_SIZE (MI355X_MICROARCH.md, HBM/rocprofv3 section).
-PMC_SUMMARY = os.path.join(REPO, "profiles", "r1_s9", "summary.json")
+PMC_SUMMARY = os.path.join(REPO, "profiles", "r1_s10", "summary.json")
 
 
 def parse():

@@ -60,6 +60,7 @@ struct surf_ctx {
 
     /* scene */
     bool hasScene = false;
+    uint32_t extBlock = 128;       /* k_extend workgroup size (SURF_EXTEND_BLOCK=128|256): 128 measured 5 % faster */
     bool connectGlobal = false;    /* k_connect reads its tables from global memory (SURF_CONNECT_GLOBAL=1, tuning) */
     bool ldsTables = false;        /* instance/material/light tables fit the per-workgroup LDS copy */
     DevScene S{};
@@ -331,7 +332,9 @@ int allocWavefront(surf_ctx* c) {
     uint64_t extPerCu = 48, conPerCu = 12;
     if (const char* e = std::getenv("SURF_GRID_EXTEND")) extPerCu = (uint64_t)std::max(1, std::atoi(e));
     if (const char* e = std::getenv("SURF_GRID_CONNECT")) conPerCu = (uint64_t)std::max(1, std::atoi(e));
-    c->gridExtend = (uint32_t)std::min<uint64_t>(maxBlocks, (uint64_t)cus * extPerCu);
+    if (const char* e = std::getenv("SURF_EXTEND_BLOCK")) c->extBlock = std::atoi(e) == 128 ? 128u : 256u;
+    if (c->extBlock == 128) extPerCu *= 2;                 /* the same threads per CU in half-size workgroups */
+    c->gridExtend = (uint32_t)std::min<uint64_t>((cap + c->extBlock - 1) / c->extBlock, (uint64_t)cus * extPerCu);
     c->gridConnect = (uint32_t)std::min<uint64_t>(maxBlocks, (uint64_t)cus * conPerCu);
     c->coopMax = (uint32_t)cus * 4 * SURF_TAIL_WAVES;
     c->longBlocks = (uint32_t)cus * 4;
@@ -414,11 +417,11 @@ void launchPhase(surf_ctx* c, int ph, hipEvent_t* ev, bool capture) {
         hipLaunchKernelGGL(k_extend_p<true>, dim3(c->gridWork), dim3(kBlock), lds, c->stream, c->S, cur, c->hitTUV,
                            c->hitInst, (const Counters*)c->ctr, par, sw);
     else if (c->ldsTables)
-        hipLaunchKernelGGL(k_extend<true>, dim3(c->gridExtend), dim3(kBlock), lds, c->stream, c->S, cur, c->hitTUV,
-                           c->hitInst, (const Counters*)c->ctr, par, sw, order);
+        hipLaunchKernelGGL(k_extend<true>, dim3(c->gridExtend), dim3(c->extBlock), traversalLds(c, c->extBlock), c->stream, c->S,
+                           cur, c->hitTUV, c->hitInst, (const Counters*)c->ctr, par, stackWords(c, c->extBlock), order);
     else
-        hipLaunchKernelGGL(k_extend<false>, dim3(c->gridExtend), dim3(kBlock), lds, c->stream, c->S, cur, c->hitTUV,
-                           c->hitInst, (const Counters*)c->ctr, par, sw, order);
+        hipLaunchKernelGGL(k_extend<false>, dim3(c->gridExtend), dim3(c->extBlock), traversalLds(c, c->extBlock), c->stream, c->S,
+                           cur, c->hitTUV, c->hitInst, (const Counters*)c->ctr, par, stackWords(c, c->extBlock), order);
     if (ev) (void)hipEventRecord(ev[1], c->stream);
     if (lng && capture && ph >= 3) (void)hipStreamWaitEvent(c->stream, c->evLong[ph - 3], 0);
     const uint32_t escQ = (uint32_t)ph & 3u;
