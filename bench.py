@@ -1,23 +1,39 @@
 """Benchmark: Mrays/s of the MI355X wavefront path tracer on BASELINE.json's
-headline workload (C3: bundled indoor scene, 1280x720, unbounded bounces +
-Russian roulette, 256 spp = 16 steps x 16 frames), next to the reference CPU
-algorithm (oracle/cpu_ref_bench, OpenMP) timed on this host.
+headline workload, next to the reference CPU algorithm timed on this host.
 
-    python bench.py [--gpus N --steps K --warmup W]
+    python bench.py [--gpus N --steps K --warmup W] [--workload C3|C2|C4|C5]
 
-One step = one batch of --frames-per-step frames (1 sample per pixel each) over
-the full frame.  With N > 1 (torch.distributed.run, one rank per GPU) each rank
-renders an interleaved 16-row shard of every frame and the float accumulator
-is gathered to rank 0 over RCCL once per step; the total work is fixed, so
-scaling is "strong".  Mrays/s = W*H*frames / seconds / 1e6 (main.cpp:431).
+Workloads (BASELINE.json configs):
+  C3  bundled indoor scene, 1280x720, 256 spp, unbounded bounces + Russian roulette (headline)
+  C2  the same scene, 1280x720, 64 spp, at most 8 path segments
+  C4  1920x1080, 1024 spp (row-sharded over the GPUs)
+  C5  indoor + 648 Suzannes baked into one 10.2M-triangle BLAS, 1280x720, 64 spp
+
+One step = one complete render of the workload: clear the accumulator, render
+its spp frames (one sample per pixel each, frame f seeded initSeed(p + 1799 f)
+as renderer.cpp:169; step i renders frames [i*spp, (i+1)*spp)), drain the
+sample stream until every frame is accumulated.  With N > 1 (torch.distributed
+.run, one rank per GPU) each rank renders an interleaved row shard of every
+frame (row b -> rank b % N) and, after its drain, its float accumulator is
+gathered to rank 0 over RCCL once per render; the total work is fixed, so
+scaling is "strong".  Mrays/s = W*H*spp*steps / seconds / 1e6 (main.cpp:431:
+camera samples per second).
+
+The CPU baseline (rank 0, N = 1) is the oracle's restatement of the
+reference's CPU renderer (oracle/cpu_ref_bench, OpenMP rows like
+renderer.cpp:163) on a bounded sample: every --cpu-row-step-th row of the
+last timed step's frames.  Its accumulator rows are compared bit for bit with
+the GPU's ("parity" in the JSON line).
 
 Prints ONE JSON line (rank 0).
 """
 import argparse
 import json
 import os
+import platform
 import subprocess
 import sys
+import tempfile
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
@@ -28,64 +44,116 @@ for p in (REPO, PKG):
 
 METRIC = "Mrays/s at 1280×720, 256 spp, indoor scene; 1/2/4/8 MI355X + CPU ref"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-# Algorithmic HBM bytes per extension ray of k_extend (DESIGN.md "Roofline"):
-# read ray o (16 B) + d (16 B), write hit (t,u,v,prim 16 B + inst 4 B).
+# Algorithmic HBM bytes per extension ray of k_extend:
+# read ray o, d (32 B: origin, direction, tmax, id), write hit t, u, v, inst, prim (20 B).
 EXTEND_BYTES_PER_RAY = 52
-# rocprofv3 PMC summary of this bench command (tools/profile_round.sh + tools/summarize_profile.py):
-# HBM bytes per k_extend launch, FETCH_SIZE x2 + WRITE_SIZE (MI355X_MICROARCH.md, HBM/rocprofv3 section).
-PMC_SUMMARY = os.path.join(REPO, "profiles", "r1_s10", "summary.json")
+# rocprofv3 summary of this bench command (tools/profile_round.sh + tools/summarize_profile.py):
+# k_extend's average duration (--kernel-trace --stats) and HBM bytes per launch (FETCH_SIZE x2 +
+# WRITE_SIZE, separate PMC passes, MI355X_MICROARCH.md HBM/rocprofv3 section).
+PMC_SUMMARY = os.path.join(REPO, "profiles", "r2_c3", "summary.json")
+
+WORKLOADS = {
+    "C3": dict(scene="indoor", width=1280, height=720, spp=256, max_segments=0, cpu_row_step=5),
+    "C2": dict(scene="indoor", width=1280, height=720, spp=64, max_segments=8, cpu_row_step=2),
+    "C4": dict(scene="indoor", width=1920, height=1080, spp=1024, max_segments=0, cpu_row_step=20),
+    "C5": dict(scene="c5", width=1280, height=720, spp=64, max_segments=0, cpu_row_step=45),
+}
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=16)
-    ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--width", type=int, default=1280)
-    ap.add_argument("--height", type=int, default=720)
-    ap.add_argument("--frames-per-step", type=int, default=16)
-    ap.add_argument("--max-segments", type=int, default=0, help="0 = unbounded + RR (C3); 8 = C2")
+    ap.add_argument("--steps", type=int, default=3, help="timed renders")
+    ap.add_argument("--warmup", type=int, default=1, help="untimed renders before the timed region")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="C3")
+    ap.add_argument("--width", type=int, default=0, help="override the workload's width")
+    ap.add_argument("--height", type=int, default=0, help="override the workload's height")
+    ap.add_argument("--spp", type=int, default=0, help="override the workload's samples per pixel (frames per render)")
     ap.add_argument("--row-block", type=int, default=1,
-                    help="rows per interleaved shard block (1 spreads the long-path-heavy rows over all GPUs)")
-    ap.add_argument("--scene", choices=["indoor", "c5"], default="indoor",
-                    help="indoor = bundled scene (C2/C3); c5 = +648-Suzanne 10.2M-triangle lattice BLAS (C5)")
-    ap.add_argument("--cpu-frames", type=int, default=48, help="frames of the CPU baseline sample (full frame)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+                    help="N > 1: rows per interleaved shard block (1 spreads the long-path-heavy rows over all GPUs)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0: the lease's CPU share (OMP_NUM_THREADS, else the affinity mask)")
+    ap.add_argument("--cpu-row-step", type=int, default=0, help="CPU sample: every n-th row of the last step's frames")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--profile-pass", type=int, default=1,
+                    help="renders re-run with per-kernel HIP events for the roofline (0 = none)")
     ap.add_argument("--tail", type=str, default="", help="tuning: drain policy 'threshold,lanes_per_wave,stage_segments'")
     ap.add_argument("--tail-coop", type=int, default=-1, help="tuning: cooperative drain when <= N paths remain")
-    ap.add_argument("--long", type=str, default="", help="tuning: long-path worker 'escape_segments,budget'")
-    ap.add_argument("--persistent", type=int, default=-1, help="tuning: force the out-of-step traversal on (1) / off (0)")
-    ap.add_argument("--profile-pass", type=int, default=-1,
-                    help="steps re-run with per-kernel HIP events for the roofline (-1 = --steps, same composition as the timed run)")
     return ap.parse_args()
 
 
-def workload(args):
-    if args.scene == "c5":
-        return "C5" if args.max_segments == 0 else f"C5-max{args.max_segments}seg"
-    return {0: "C3", 8: "C2"}.get(args.max_segments, f"max{args.max_segments}seg")
+def host_cpu_info():
+    """What the CPU baseline ran on: the model, sockets and hardware threads of
+    the host, and the share of it this process may use."""
+    info = {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)),
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"), "model": platform.processor() or None, "sockets": None}
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            k, _, v = line.partition(":")
+            if k.strip() == "Model name":
+                info["model"] = v.strip()
+            elif k.strip() == "Socket(s)":
+                info["sockets"] = int(v.strip())
+    except (OSError, ValueError, subprocess.SubprocessError):
+        pass
+    return info
 
 
-def cpu_baseline(args):
-    """Reference CPU algorithm (oracle restatement, OpenMP rows) on a bounded sample."""
+def cpu_threads(args):
+    if args.cpu_threads > 0:
+        return args.cpu_threads
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        return int(omp)            # the lease's CPU share (the GPU pool sets it per GPU)
+    return len(os.sched_getaffinity(0))
+
+
+def cpu_baseline(args, wl, first_frame, gpu_acc):
+    """Reference CPU algorithm (oracle restatement, OpenMP rows) on a bounded
+    sample of the last timed render, checked bit for bit against the GPU's rows."""
+    import numpy as np
     exe = os.path.join(REPO, "oracle", "cpu_ref_bench")
     if not os.path.exists(exe):
         subprocess.run(["make", "-s", "-C", os.path.join(REPO, "oracle")], check=True)
-    env = dict(os.environ, OMP_NUM_THREADS=str(args.cpu_threads))
-    r0, r1, frames = 0, args.height, args.cpu_frames
-    if args.scene == "c5":                # ~60x slower per sample: a centred row band, one frame
-        r0, r1, frames = args.height // 2 - 32, args.height // 2 + 32, 1
-    cmd = [exe, "--cutoff"] + (["--variant", "1"] if args.scene == "c5" else []) + [os.path.join(REPO, "assets"),
-           str(args.width), str(args.height), str(frames), str(r0), str(r1), str(args.max_segments), str(args.cpu_threads)]
-    out = subprocess.run(cmd, capture_output=True, text=True, env=env, check=True).stdout.strip().splitlines()[-1]
-    r = json.loads(out)
-    return {"value": round(r["mrays_per_s"], 4), "unit": "Mrays/s", "cores": r["threads"], "kind": "port",
-            "sample": f"{args.width}x{args.height} rows {r0}..{r1 - 1}, frames 0..{frames - 1} (1 spp each), "
-                      f"{'unbounded+RR' if args.max_segments == 0 else 'max %d segments' % args.max_segments}, "
-                      f"throughput cutoff on (as the GPU), oracle/cpu_ref_bench, {r['seconds']:.2f} s",
-            "seconds": r["seconds"], "samples": r["samples"],
-            "events": {k: r[k] for k in ("n_ext", "n_hit", "n_cont", "n_shadow", "n_acc", "n_unocc")}}
+    threads = cpu_threads(args)
+    env = dict(os.environ, OMP_NUM_THREADS=str(threads))
+    W, H, F, step = wl["width"], wl["height"], wl["spp"], wl["cpu_row_step"]
+    with tempfile.TemporaryDirectory() as tmp:
+        dump = os.path.join(tmp, "acc.f32")
+        cmd = [exe, "--cutoff", "--first", str(first_frame), "--row-step", str(step), "--dump", dump]
+        if wl["scene"] == "c5":
+            cmd += ["--variant", "1"]
+        cmd += [os.path.join(REPO, "assets"), str(W), str(H), str(F), "0", str(H), str(wl["max_segments"]), str(threads)]
+        out = subprocess.run(cmd, capture_output=True, text=True, env=env, check=True).stdout.strip().splitlines()[-1]
+        r = json.loads(out)
+        cpu_rows = np.fromfile(dump, dtype=np.float32).reshape(-1, W, 4)
+    gpu_rows = gpu_acc[0::step]
+    d = (gpu_rows[..., :3].astype(np.float64) - cpu_rows[..., :3].astype(np.float64)) / F
+    per = np.sqrt((d ** 2).sum(-1))
+    parity = {"rows": f"0:{H}:{step}", "frames": [first_frame, first_frame + F],
+              "bitexact": bool(np.array_equal(gpu_rows.view(np.uint32), cpu_rows.view(np.uint32))),
+              "rms_l2": float(np.sqrt((per ** 2).mean())), "max_l2": float(per.max()), "tolerance_l2": 1e-3}
+    cpu = {"value": round(r["mrays_per_s"], 4), "unit": "Mrays/s", "cores": r["threads"], "kind": "port",
+           "sample": f"{W}x{H} rows 0,{step},{2 * step},.. ({r['rows']} rows), frames {first_frame}..{first_frame + F - 1} "
+                     f"(1 spp each; the last timed render's frames), "
+                     f"{'unbounded+RR' if wl['max_segments'] == 0 else 'max %d segments' % wl['max_segments']}, "
+                     f"throughput cutoff on (as the GPU), oracle/cpu_ref_bench -O3, {r['seconds']:.2f} s",
+           "seconds": r["seconds"], "samples": r["samples"], "host": host_cpu_info(),
+           "events": {k: r[k] for k in ("n_ext", "n_hit", "n_cont", "n_shadow", "n_acc", "n_unocc")}}
+    return cpu, parity
+
+
+def rocprof_summary(workload):
+    """k_extend's rocprofv3 average and PMC traffic from the committed summary of this command."""
+    if not os.path.exists(PMC_SUMMARY):
+        return None
+    s = json.load(open(PMC_SUMMARY))
+    if s.get("workload", "C3") != workload:
+        return None
+    k = next((v for n, v in s.get("kernels", {}).items() if n.startswith("k_extend")), None)
+    pmc = s.get("k_extend_pmc", {})
+    return {"source": os.path.relpath(PMC_SUMMARY, REPO), "avg_launch_ms": k["avg_us"] / 1e3 if k else None,
+            "traffic": pmc.get("hbm_bytes_per_launch_corrected")}
 
 
 def main():
@@ -95,8 +163,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch          # torch first: it loads the HIP runtime the library then binds to
     import torch.distributed as dist
-    import numpy as np
     import surf_amd
+
+    wl = dict(WORKLOADS[args.workload])
+    for k in ("width", "height", "spp"):
+        if getattr(args, k):
+            wl[k] = getattr(args, k)
+    if args.cpu_row_step:
+        wl["cpu_row_step"] = args.cpu_row_step
+    W, H, SPP, MAXSEG = wl["width"], wl["height"], wl["spp"], wl["max_segments"]
 
     dist_on = world > 1
     if dist_on:
@@ -106,9 +181,8 @@ def main():
     torch.cuda.init()
 
     surf_amd.load()
-    W, H, F = args.width, args.height, args.frames_per_step
     tb = time.perf_counter()
-    scene = surf_amd.Scene.indoor(variant=1 if args.scene == "c5" else 0)
+    scene = surf_amd.Scene.indoor(variant=1 if wl["scene"] == "c5" else 0)
     scene_build_s = time.perf_counter() - tb
     spec = surf_amd.ShardSpec(rank, world, args.row_block if world > 1 else 0)
     r = surf_amd.Renderer(scene, W, H, device=local, shard=spec)
@@ -116,40 +190,37 @@ def main():
         r.set_tail_policy(*[int(x) for x in args.tail.split(",")])
     if args.tail_coop >= 0:
         r.set_tail_coop(args.tail_coop)
-    if args.long:
-        r.set_long_paths(*[int(x) for x in args.long.split(",")])
-    if args.persistent >= 0:
-        r.set_persistent(bool(args.persistent))
     rows = len(r.rows)
-    acc_dev = torch.empty((rows, W, 4), dtype=torch.float32, device=dev)
-    gather = None
+    gather = acc_dev = None
     if dist_on:
         from surf_amd.dist import RowGather
+        acc_dev = torch.empty((rows, W, 4), dtype=torch.float32, device=dev)
         gather = RowGather(W, H, world, rank, args.row_block, dev)
 
     def step(i):
-        r.render(F, i * F, args.max_segments)
-        if dist_on:                       # one RCCL gather of the accumulator per step
+        """One complete render: frames [i*SPP, (i+1)*SPP), drained; N > 1: one RCCL gather."""
+        r.clear_accumulator()
+        r.render(SPP, i * SPP, MAXSEG)
+        r.synchronize()                   # every frame of the render accumulated
+        if dist_on:
             r.copy_accumulator_to(acc_dev.data_ptr())
             gather.gather(acc_dev)
 
     for w in range(args.warmup):
         step(w)
-    r.clear_accumulator()
     # ---- timed region ----
     if dist_on:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    r.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(i)
-    r.synchronize()                       # drains the sample stream: every path finished
+        step(args.warmup + i)
     torch.cuda.synchronize(dev)
     if dist_on:
         dist.barrier()
     dt = time.perf_counter() - t0
-    st = r.stats()
+    last_first = (args.warmup + args.steps - 1) * SPP
+    st = r.stats()                        # the last render's counts (cleared per step)
     ev = {k: st[k] for k in ("n_ext", "n_hit", "n_cont", "n_shadow", "n_acc", "n_unocc", "iterations", "tail_paths")}
     if dist_on:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
@@ -158,51 +229,49 @@ def main():
         evt = torch.tensor([ev[k] for k in ev], dtype=torch.float64, device=dev)
         dist.all_reduce(evt)
         ev = {k: int(v) for k, v in zip(ev, evt.tolist())}
-    samples = W * H * F * args.steps
-    value = samples / dt / 1e6
+    gpu_acc = r.accumulator() if (rank == 0 and world == 1 and not args.no_cpu) else None
+    samples_per_render = W * H * SPP
+    value = samples_per_render * args.steps / dt / 1e6
 
-    # ---- roofline of the dominant kernel (k_extend), HIP events on the render stream ----
-    roof = None
-    kernel_ms = None
-    if args.profile_pass < 0:
-        args.profile_pass = args.steps
+    # ---- roofline of the dominant wavefront kernel (k_extend), HIP events on the render stream ----
+    roof = kernel_ms = None
     if args.profile_pass > 0:
         r.set_profiling(True)
-        r.clear_accumulator()
         for i in range(args.profile_pass):
-            r.render(F, i * F, args.max_segments)
-        pe = r.stats()
+            r.clear_accumulator()
+            r.render(SPP, i * SPP, MAXSEG)
+            r.synchronize()
+        pe = r.stats()                    # the last profiled render
         r.set_profiling(False)
         launches = max(pe["launches_extend"], 1)
-        bytes_per_launch = EXTEND_BYTES_PER_RAY * pe["n_ext"] / launches
+        rays_per_launch = pe["n_ext_wavefront"] / launches
+        bytes_per_launch = EXTEND_BYTES_PER_RAY * rays_per_launch
         avg_ms = pe["ms_extend"] / launches
         achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
-        traffic, traffic_src = None, None
-        if os.path.exists(PMC_SUMMARY):
-            pmc = json.load(open(PMC_SUMMARY)).get("k_extend_pmc", {})
-            traffic = pmc.get("hbm_bytes_per_launch_corrected")
-            traffic_src = os.path.relpath(PMC_SUMMARY, REPO)
         roof = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": round(traffic) if traffic else None,
-                "traffic_source": traffic_src,
+                "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
                 "kernel": "k_extend", "avg_launch_ms": round(avg_ms, 5), "launches": int(pe["launches_extend"]),
+                "rays_per_launch": round(rays_per_launch, 1), "bytes_per_ray": EXTEND_BYTES_PER_RAY,
                 "algorithmic_bytes_per_launch": round(bytes_per_launch, 1)}
-        kernel_ms = {k: round(pe[k], 3) for k in ("ms_extend", "ms_shade", "ms_connect", "ms_regen", "ms_tail", "ms_total")}
-        kernel_ms["steps"] = args.profile_pass
+        rp = rocprof_summary(args.workload)
+        if rp:
+            roof["traffic"] = round(rp["traffic"]) if rp["traffic"] else None
+            roof["rocprof"] = {"source": rp["source"], "avg_launch_ms": rp["avg_launch_ms"],
+                               "frac": round(bytes_per_launch / (rp["avg_launch_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 6)
+                               if rp["avg_launch_ms"] else None}
+        kernel_ms = {k: round(pe[k], 3) for k in ("ms_sort", "ms_extend", "ms_shade", "ms_connect", "ms_regen", "ms_tail", "ms_total")}
+        kernel_ms["renders"] = args.profile_pass
         kernel_ms["tail_paths"] = int(pe["tail_paths"])
-        if dist_on:
-            t = torch.tensor([achieved], dtype=torch.float64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MIN)
 
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
+    cpu = parity = None
+    if gpu_acc is not None:
         try:
-            cpu = cpu_baseline(args)
+            cpu, parity = cpu_baseline(args, wl, last_first, gpu_acc)
         except Exception as e:  # reported, never silently replaced
-            cpu = {"value": None, "unit": "Mrays/s", "cores": args.cpu_threads, "kind": "port", "sample": f"failed: {e}"}
+            cpu = {"value": None, "unit": "Mrays/s", "cores": cpu_threads(args), "kind": "port", "sample": f"failed: {e}"}
 
     if rank == 0:
-        per_sample = {k: round(ev[k] / samples, 4) for k in ("n_ext", "n_hit", "n_cont", "n_shadow", "n_acc", "n_unocc")}
+        per_sample = {k: round(ev[k] / samples_per_render, 4) for k in ("n_ext", "n_hit", "n_cont", "n_shadow", "n_acc", "n_unocc")}
         out = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -216,19 +285,22 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic camera samples of the bundled indoor scene (reference OBJ assets)",
-            "config": {"workload": workload(args),
-                       "scene": "bundled indoor (main.cpp:161-346)" if args.scene == "indoor"
+            "config": {"workload": args.workload,
+                       "scene": "bundled indoor (main.cpp:161-346)" if wl["scene"] == "indoor"
                                 else "C5: indoor + 648 Suzannes in one 10.2M-triangle BLAS",
-                       "width": W, "height": H,
-                       "spp": F * args.steps, "frames_per_step": F,
-                       "bounces": "unbounded + russian roulette" if args.max_segments == 0 else f"<= {args.max_segments} segments",
-                       "parallelism": f"row-shard x{world} (16-row interleave) + RCCL gather" if world > 1 else "single GPU"},
+                       "width": W, "height": H, "spp": SPP, "renders": args.steps,
+                       "step": f"one complete {SPP}-frame render including its drain",
+                       "bounces": "unbounded + russian roulette" if MAXSEG == 0 else f"<= {MAXSEG} segments",
+                       "zero_cutoff": True,
+                       "parallelism": (f"row shards x{world} (rows interleaved in blocks of {args.row_block}) + one RCCL gather per render"
+                                       if world > 1 else "single GPU")},
             "roofline": roof,
             "cpu_baseline": cpu,
+            "parity": parity,
             "gpu_vs_cpu": round(value / cpu["value"], 2) if cpu and cpu.get("value") else None,
             "events_per_sample": per_sample,
-            "iterations": ev["iterations"],
-            "tail_paths": ev["tail_paths"],
+            "iterations_per_render": ev["iterations"],
+            "tail_paths_per_render": ev["tail_paths"],
             "kernel_ms_profile_pass": kernel_ms,
             "scene_build_s": round(scene_build_s, 3),
         }

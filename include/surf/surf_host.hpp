@@ -296,6 +296,9 @@ struct RendererConfig {
     U32 maxBounces = 5;          /* unused by the reference's iterative path; kept */
     U32 samplesPerFrame = 1;
     U32 maxSegments = 0;         /* 0: unbounded + Russian roulette (reference); N: cap (config C2) */
+    bool lumenOutput = false;    /* WF_LUMEN_OUTPUT (renderer.cpp:31, default 0): frameInfo().energy from the
+                                    accumulator; reading it drains the sample stream, so it is computed only
+                                    when frameInfo() is read after a render */
 };
 
 struct FrameInstrumentationData {
@@ -327,12 +330,13 @@ public:
     void clearAccumulator() override;
     void render(F32 deltaTime) override;
     RendererConfig& config() override { return m_config; }
-    const FrameInstrumentationData& frameInfo() override { return m_frameInfo; }
+    const FrameInstrumentationData& frameInfo() override;
 
     /* headless additions */
     std::vector<F32> readAccumulator();           /* width*height*4 floats */
     std::vector<U32> finalizeRGBA8();             /* width*height RGBA8 words */
     std::vector<U32> displayRGBA8();              /* finalize image through fs_quad.frag's sqrt gamma */
+    void synchronize();                           /* waits until every frame rendered so far is accumulated */
     surf_ctx* handle() const { return m_ctx; }
 private:
     surf_ctx* m_ctx = nullptr;
@@ -343,6 +347,7 @@ private:
     U32 m_sceneGeneration = 0;
     U32 m_totalSamples = 0;
     FrameInstrumentationData m_frameInfo;
+    bool m_energyStale = false;
 };
 
 static_assert(sizeof(Triangle) == sizeof(surf_triangle), "Triangle layout");

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define SURF_ABI_VERSION 1
+#define SURF_ABI_VERSION 2
 
 typedef enum {
     SURF_OK = 0,
@@ -122,13 +122,14 @@ typedef struct {
     uint64_t tail_paths;       /* paths finished by the tail kernel */
     double   ms_total;         /* device time of render + drain calls since the last clear */
     double   ms_extend, ms_shade, ms_connect, ms_regen, ms_tail, ms_accum;  /* per-kernel (surf_set_profiling) */
+    double   ms_sort;          /* ray-order sorts (pool + shadow queue), profiling mode */
     uint64_t launches_extend;  /* k_extend launches timed (profiling mode) */
+    uint64_t n_ext_wavefront;  /* extension rays traced by k_extend (n_ext minus the drain's) */
     uint32_t stack_depth;      /* traversal stack entries reserved per ray */
     uint32_t pool_capacity;    /* paths in flight */
     float    energy;           /* sum of acc.rgb / samples over the shard ("Lumen", renderer.cpp:191-201) */
     uint32_t max_segments;     /* longest path seen (extension rays), diagnostics */
-    uint64_t tail_survivors;   /* drain paths still alive after the tail's first stage */
-    uint64_t long_paths;       /* paths finished by the long-path worker (surf_set_long_paths) */
+    uint64_t tail_survivors;   /* drain paths handed to the cooperative tail */
 } surf_stats;
 
 typedef struct surf_ctx surf_ctx;       /* one per HIP device */
@@ -155,18 +156,25 @@ int surf_shard_rows(const surf_ctx* ctx, uint32_t* rows, uint32_t* row_count);
 /* Paths in flight (default: sized from the shard, >= 1M when possible). Must be
  * called before the first render. */
 int surf_set_pool_capacity(surf_ctx* ctx, uint32_t paths);
-/* Frame window (default 256, at most 16 GiB of radiance slots): frames whose
- * samples may be in flight at once.
- * Sample radiance is held per (frame slot, pixel) until a frame completes and
- * is accumulated in frame order; long Russian-roulette paths of old frames
- * overlap the bulk of newer ones instead of stalling each render call. */
+/* Frame window: frames whose samples may be in flight at once (default: as
+ * many as 32 GiB of radiance slots hold, at most 4096 -- 2330 frames at
+ * 1280x720, 1035 at 1920x1080, of the 288 GB HBM).  Sample radiance is held
+ * per (frame slot, pixel) until a frame completes and is accumulated in frame
+ * order; long Russian-roulette paths of old frames overlap the bulk of newer
+ * ones.  A stream longer than the window issues frame f only once frame
+ * f - window is accumulated, so the window is sized past the longest renders
+ * (C4: 1024 frames). */
 int surf_set_frame_batch(surf_ctx* ctx, uint32_t frames);
-/* Zero-throughput cutoff (default on): a path whose throughput T is exactly
- * (0,0,0) ends early.  Every later contribution would be T * finite = +0, so
- * the radiance is bit-identical to the reference's (tests check it against the
- * oracle run without the cutoff); only n_ext/n_cont/... shrink.  It bounds the
- * total-internal-reflection orbits in the glass lens, which the reference
- * traces for up to millions of segments. */
+/* Throughput cutoff (default on): a path whose throughput T is below FLT_MIN
+ * (1.17549435e-38) in every channel -- zero or denormal -- ends early.  The
+ * reference's Russian roulette ends such a path with certainty at its next
+ * diffuse bounce (p = max(T) < 2^-32, the smallest positive randomF32), so at
+ * most two contributions of < 1.2e-38 x (emission or light term) are dropped:
+ * radiance-neutral in f32 except for a pixel whose own energy is ~1e-38 (the
+ * parity tests compare the GPU with the cutoff against the oracle without it,
+ * bit for bit, on every tested image); n_ext/n_cont/... shrink.  It ends the
+ * total-internal-reflection orbits in the glass lens that the reference traces
+ * for up to millions of segments at a denormal throughput. */
 int surf_set_zero_cutoff(surf_ctx* ctx, int enabled);
 /* Drain policy: when no new sample may be issued and at most `threshold_paths`
  * paths are in flight, the tail kernel finishes them in stages: each stage
@@ -180,15 +188,6 @@ int surf_set_tail_policy(surf_ctx* ctx, uint32_t threshold_paths, uint32_t lanes
 /* Drain paths handed to the cooperative tail (one path per 64-lane wave, the
  * lanes-as-planes traversal; default 60000, 0 = never).  Identical results. */
 int surf_set_tail_coop(surf_ctx* ctx, uint32_t max_paths);
-/* Long paths: a path whose next segment would be its `escape_segments`-th
- * leaves the wavefront (which advances a path one segment per iteration, i.e.
- * per ~4 kernel launches over the whole pool) for the long pool, which a
- * second chain of the phase graph advances `segments_per_phase` segments per
- * phase, beside the wavefront kernels; the escaping bounce's shadow ray
- * travels with the path, so radiance is added in the reference's order.
- * Results do not depend on it (escape_segments 0 = off).  Drains the context
- * first. */
-int surf_set_long_paths(surf_ctx* ctx, uint32_t escape_segments, uint32_t segments_per_phase);
 /* Diagnostics: how many paths the segment cap ended in the current sample
  * stream, and the sample ids (frame slot * shard pixels + pixel) of the first
  * min(count, 64, max). */
@@ -243,17 +242,15 @@ int surf_trace_closest(surf_ctx* ctx, uint32_t n, const float* o, const float* d
 int surf_trace_any(surf_ctx* ctx, uint32_t n, const float* o, const float* d, const float* tmax,
                    uint8_t* occluded);
 /* 0: one ray per lane (the wavefront kernels' traversal); 1: one ray per
- * 64-lane wave with the instances traced in parallel (the cooperative tail's
- * traversal; needs a scene uploaded with a single-leaf TLAS of <= 64
- * instances).  Results are identical; selects what surf_trace_* run. */
+ * 64-lane wave, lanes as the node record's planes (the cooperative tail's
+ * traversal; needs a single-leaf TLAS of <= 64 instances and a BVH stack of
+ * <= 64 entries).  Results are identical; selects what surf_trace_* run. */
 int surf_set_trace_mode(surf_ctx* ctx, int mode);
-/* Wavefront traversal variant (default 0): lanes run out of step, each
- * fetching the next ray of its wave's range when done; 0 = one ray per lane in
- * lockstep.  Identical results; single-leaf TLAS scenes only use it. */
-int surf_set_persistent(surf_ctx* ctx, int enabled);
 
 /* ---- host scene build (the reference's main.cpp scene, OBJ assets) ----
- * variant 0: bundled indoor scene; 1: C5 deep scene (+648 Suzannes in one mesh). */
+ * variant 0: bundled indoor scene; 1: C5 deep scene (+648 Suzannes in one mesh);
+ * 2 / 3: general-TLAS test scenes (+40 / +80 scattered cube, Suzanne and lens
+ * instances: 51 instances with the LDS tables, 91 with global tables). */
 int surf_scene_build_indoor(const char* assets_dir, int variant, surf_scene** out);
 int surf_scene_desc_get(const surf_scene* scene, surf_scene_desc* out);
 /* GPUScene::update (sources/scene.cpp:267-282): rotate instance 3 by

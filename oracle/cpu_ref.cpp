@@ -607,6 +607,26 @@ Scene* buildIndoor(const std::string& dir, int variant) {
     Instance wallBack = makeInstance(planeB, floorM, scale(rotate(translate(I, mk(0.0f, 4.0f, 10.0f)), radiansf(90.0f), right), mk(10.0f, 10.0f, 5.0f)));   /* :327-341 */
     S->inst = {floorI, cubeL, cubeR, sus0, sus1, lens0, wallL, wallR, wallTop, wallFront, wallBack};          /* :360 */
     if (latB) S->inst.push_back(makeInstance(latB, diffM, I));
+    if (variant == 2 || variant == 3) {
+        /* general-TLAS test scenes (not in the reference's main.cpp): extra
+         * instances of the cube / Suzanne / lens meshes, sizes 0.3-0.9 and
+         * rotations varied so that BvhTLAS::build splits (bvh.cpp:780-993):
+         * 40 extras (51 instances, LDS tables) or 80 (91, global tables) */
+        const Blas* meshes[3] = {cubeB, susB, lensB};
+        Material* mats[5] = {floorM, diffM, specM, dielM, greenM};
+        const int extra = variant == 2 ? 40 : 80;
+        for (int k = 0; k < extra; ++k) {
+            const float x = -8.5f + 1.0f * (float)((k * 7) % 18);
+            const float y = -0.4f + 0.9f * (float)((k * 5) % 10);
+            float z = -8.5f + 1.0f * (float)((k * 11) % 18);
+            if (x > -2.5f && x < 2.5f && y < 2.5f && z < -4.5f) z = z + 6.0f;   /* keep clear of the camera (0, 0, -7) */
+            const float sc = 0.3f + 0.15f * (float)(k % 5);
+            M4 X = translate(I, mk(x, y, z));
+            if (k % 3 == 1) X = rotate(X, radiansf(17.0f * (float)(k % 7)), mk(0.0f, 1.0f, 0.0f));
+            X = scale(X, mk(sc, sc, sc));
+            S->inst.push_back(makeInstance(meshes[k % 3], mats[k % 5], X));
+        }
+    }
 
     /* Scene::Scene, scene.cpp:17-33 */
     InstPrims P; P.inst = &S->inst;
@@ -902,9 +922,13 @@ uint64_t orc_scene_export(const orc_scene* h, int which, void* dst) {
     return out.size();
 }
 
-double orc_render(orc_scene* h, uint32_t W, uint32_t H, uint32_t r0, uint32_t r1,
-                  uint32_t first, uint32_t frames, uint32_t maxSeg, int threads,
-                  float* acc, orc_counters* cnt) {
+/* Renderer::render (renderer.cpp:148-201) over an arbitrary list of image
+ * rows: rows dynamic over OpenMP threads (renderer.cpp:163), per-pixel seed per
+ * frame, acc += (rgb, 1) per sample (renderer.cpp:166-188).  acc holds
+ * nrows x W RGBA floats in list order. */
+double orc_render_rows(orc_scene* h, uint32_t W, uint32_t H, const uint32_t* rows, uint32_t nrows,
+                       uint32_t first, uint32_t frames, uint32_t maxSeg, int threads,
+                       float* acc, orc_counters* cnt) {
     Scene& S = *h->s;
     if (S.scrW != (float)W || S.scrH != (float)H) setCamera(S, W, H);
     if (threads > 0) omp_set_num_threads(threads);
@@ -913,12 +937,12 @@ double orc_render(orc_scene* h, uint32_t W, uint32_t H, uint32_t r0, uint32_t r1
     #pragma omp parallel
     {
         Counters C; uint32_t sm = 0;
-        /* renderer.cpp:163-186: rows dynamic, per-pixel seed per frame, acc += (rgb,1) */
         #pragma omp for schedule(dynamic)
-        for (int64_t y = (int64_t)r0; y < (int64_t)r1; ++y) {
+        for (int64_t k = 0; k < (int64_t)nrows; ++k) {
+            const uint32_t y = rows[k];
             for (uint32_t x = 0; x < W; ++x) {
                 uint64_t p = (uint64_t)x + (uint64_t)y * W;
-                float* a = acc + 4 * ((uint64_t)(y - r0) * W + x);
+                float* a = acc + 4 * ((uint64_t)k * W + x);
                 for (uint32_t f = 0; f < frames; ++f) {
                     uint32_t seed = seedOf((uint32_t)(p + (uint64_t)(first + f) * 1799u));
                     float jy = rndRange(seed, -0.5f, 0.5f);   /* GCC: last argument first */
@@ -940,11 +964,19 @@ double orc_render(orc_scene* h, uint32_t W, uint32_t H, uint32_t r0, uint32_t r1
     auto t1 = std::chrono::steady_clock::now();
     if (smax > S.stackMax) S.stackMax = smax;
     if (cnt) {
-        cnt->samples = (uint64_t)(r1 - r0) * W * frames;
+        cnt->samples = (uint64_t)nrows * W * frames;
         cnt->n_ext = tot.ext; cnt->n_hit = tot.hit; cnt->n_cont = tot.cont; cnt->n_shadow = tot.sh;
         cnt->n_acc = tot.acc; cnt->n_unocc = tot.unocc; cnt->max_segments = tot.maxSeg;
     }
     return std::chrono::duration<double>(t1 - t0).count();
+}
+
+double orc_render(orc_scene* h, uint32_t W, uint32_t H, uint32_t r0, uint32_t r1,
+                  uint32_t first, uint32_t frames, uint32_t maxSeg, int threads,
+                  float* acc, orc_counters* cnt) {
+    std::vector<uint32_t> rows;
+    for (uint32_t y = r0; y < r1; ++y) rows.push_back(y);
+    return orc_render_rows(h, W, H, rows.data(), (uint32_t)rows.size(), first, frames, maxSeg, threads, acc, cnt);
 }
 
 void orc_scene_update(orc_scene* h, float dt) {

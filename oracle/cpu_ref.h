@@ -71,6 +71,10 @@ double orc_render(orc_scene*, uint32_t width, uint32_t height,
                   uint32_t row_begin, uint32_t row_end,
                   uint32_t first_frame, uint32_t frames, uint32_t max_segments,
                   int threads, float* acc, orc_counters* counters);
+/* The same over an arbitrary row list (acc: nrows x width RGBA, list order). */
+double orc_render_rows(orc_scene*, uint32_t width, uint32_t height, const uint32_t* rows, uint32_t nrows,
+                       uint32_t first_frame, uint32_t frames, uint32_t max_segments, int threads,
+                       float* acc, orc_counters* out);
 
 /* Closest hit of n world-space rays (o,d: 3 floats each, depth starts 1e30).
  * out_t, out_u, out_v (floats), out_inst, out_prim (u32, ~0 when missed). */

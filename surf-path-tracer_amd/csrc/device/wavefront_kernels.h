@@ -107,22 +107,6 @@ struct DevCamera {
 };
 
 struct Pool { float4* o; float4* d; float4* T; uint8_t* key; };   /* key: ray-order bin (start instance) */
-/* Long paths (the reference's Russian roulette keeps ~0.04% of paths alive for
- * hundreds to thousands of segments): the wavefront advances a path one
- * segment per phase (~1.8 ms at 1280x720), so by the end of a stream tens of
- * thousands of them are still in flight.  A path reaching Counters::longThresh
- * segments therefore leaves the wavefront: k_shade appends it -- with the
- * shadow ray of that bounce, resolved first so radiance is added in the
- * reference's order -- to escape queue esc[phase % 4], and k_long, a second
- * chain of the phase graph that runs beside the wavefront kernels, advances
- * every long path up to Counters::longBudget segments per phase
- * (lp[phase & 1] + esc[(phase - 1) % 4] -> lp[(phase + 1) & 1]). */
-struct EscQ { float4 *o, *d, *T, *so, *sd, *sc; };   /* path + pending shadow ray (sc.w = 1 when present) */
-struct LongPools {
-    Pool lp[2];
-    EscQ esc[4];
-    uint32_t lpCap, escCap;
-};
 /* Where a path that used up its segment budget goes. */
 struct Sink { Pool q; uint32_t* n; uint32_t cap; };
 struct ShadowQ { float4* o; float4* d; float4* c; uint8_t* key; };   /* key: ray-order bin (light instance) */
@@ -138,17 +122,11 @@ struct Counters {
     uint32_t segMax;                 /* longest finished path (extension rays), diagnostics */
     uint32_t survN;                  /* k_tail survivors appended (may exceed survCap) */
     uint32_t survCap;
-    uint32_t longThresh;             /* a continuation with this many segments escapes the wavefront (0 = off) */
-    uint32_t longBudget;             /* segments per long path per k_long step */
-    uint32_t lpN[2];                 /* long pools (k_long appends; may exceed lpCap only by refusal) */
-    uint32_t escN[4];                /* escape queues (k_shade appends) */
-    uint32_t lpDone;                 /* k_long blocks finished (last one resets its inputs' counts) */
-    uint32_t longPop;                /* long paths in flight (escaped, not finished) <= lpCap */
-    uint32_t _pad2[2];
+    uint32_t _pad2[3];
     unsigned long long issued[2];    /* stream samples issued, per parity */
     unsigned long long limit;        /* host-written issue limit (frame window) */
     unsigned long long baseFrame;    /* absolute frame index of stream frame 0 */
-    unsigned long long ev[16];       /* ext, hit, cont, shadow, acc, unocc, tail paths, capped paths, long paths */
+    unsigned long long ev[16];       /* ext, hit, cont, shadow, acc, unocc, tail paths, capped paths, wavefront ext */
     uint32_t capped[64];             /* sample ids of the first paths ended by the segment cap (diagnostics) */
     /* event counts striped over kStripes cache lines (block b adds to stripe
      * b % kStripes): a counter shared by every block of a launch serializes its
@@ -324,71 +302,6 @@ __device__ __forceinline__ bool blasTrace(const DevScene& S, const TraceInst& I,
     return any;
 }
 
-/* Closest hit of one BLAS with depth starting at kFarAway, for the
- * instance-parallel merge (traceSceneCoop).  Same traversal as blasTrace; in
- * addition it carries A = the largest box entry distance on the path to the
- * current node (a second LDS stack) and flags `patho` when a hit is accepted at
- * t < A -- a triangle reported in front of a box that contains it (rounding).
- * Without such a hit, the traversal with any starting depth D returns exactly
- * this result when t < D and a miss otherwise: a box the depth-D traversal
- * prunes (entry >= its depth) could only have contributed a hit below that
- * entry by exactly this rounding effect, so both traversals accept the same
- * hits below D in the same order ("Cooperative tail"). */
-template <bool FIN>
-__device__ __forceinline__ bool blasTraceTrack(const DevScene& S, const TraceInst& I, V3 o, V3 d, V3 rd, float& depth,
-                                               float& hu, float& hv, uint32_t& hprim, uint32_t* stk, float* astk,
-                                               uint32_t stride, bool& patho) {
-    const uint32_t nodeOff = I.meta.x;
-    const float4* tri = S.tris + 3u * I.meta.y;
-    const float4 r0 = I.r0, r1 = I.r1;
-    const uint32_t rlf = f2u(r0.w), rcnt = f2u(r1.w);
-    if (rcnt != 0u) return leafTestUniform<false>(tri, rlf, rcnt, o, d, depth, hu, hv, hprim);   /* no boxes: exact for any D */
-    uint32_t* sp = stk;
-    float* ap = astk;
-    uint32_t node;
-    float A;
-    bool any = false;
-    {
-        float dn = boxDist<FIN>(r0, r1, o, rd, depth);
-        float df = boxDist<FIN>(I.r2, I.r3, o, rd, depth);
-        uint32_t cn = nodeOff + rlf, cf = cn + 1u;
-        if (dn > df) { const float t = dn; dn = df; df = t; const uint32_t c = cn; cn = cf; cf = c; }
-        if (dn == kFarAway) return false;
-        node = cn; A = dn;
-        if (df != kFarAway) { *sp = cf; *ap = df; sp += stride; ap += stride; }
-    }
-    for (;;) {
-        const float4* nd = S.nodes + 4u * node;
-        float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
-        pin(q0); pin(q1); pin(q2); pin(q3);
-        const uint32_t lf = f2u(q0.w), cnt = f2u(q1.w);
-        if (cnt != 0u) {
-            if (leafTest<false>(tri, lf, cnt, o, d, depth, hu, hv, hprim)) {
-                any = true;
-                if (depth < A) patho = true;
-            }
-            if (sp == stk) break;
-            sp -= stride; ap -= stride;
-            node = *sp; A = *ap;
-            continue;
-        }
-        float dn = boxDist<FIN>(q0, q1, o, rd, depth);
-        float df = boxDist<FIN>(q2, q3, o, rd, depth);
-        uint32_t cn = nodeOff + lf, cf = cn + 1u;
-        if (dn > df) { const float t = dn; dn = df; df = t; const uint32_t c = cn; cn = cf; cf = c; }
-        if (dn == kFarAway) {
-            if (sp == stk) break;
-            sp -= stride; ap -= stride;
-            node = *sp; A = *ap;
-        } else {
-            node = cn;
-            if (df != kFarAway) { *sp = cf; *ap = fmaxf(A, df); sp += stride; ap += stride; }
-            A = fmaxf(A, dn);
-        }
-    }
-    return any;
-}
-
 /* Instance::intersect(Any) (bvh.cpp:481-513): origin (M^-1 (o,1)).xyz / w,
  * direction (M^-1 (d,0)).xyz (not renormalized: t is shared with world space).
  * For an affine M^-1 (row 3 = 0,0,0,1) w is exactly 1 for finite o and x/1 = x,
@@ -512,77 +425,6 @@ __device__ __forceinline__ void instanceRay(const TraceInst& I, V3 o, V3 d, V3& 
     oo = mk3(rowDot(I.m0, o.x, o.y, o.z, 1.0f), rowDot(I.m1, o.x, o.y, o.z, 1.0f), rowDot(I.m2, o.x, o.y, o.z, 1.0f));
     if (!I.meta.z) oo = divs(oo, rowDot(I.m3, o.x, o.y, o.z, 1.0f));
     dd = mk3(rowDot(I.m0, d.x, d.y, d.z, 0.0f), rowDot(I.m1, d.x, d.y, d.z, 0.0f), rowDot(I.m2, d.x, d.y, d.z, 0.0f));
-}
-
-/* ------------------------------------------------------- cooperative (one ray per wave)
- * For the single-leaf TLAS with at most 64 instances: lane k traces instance
- * tlasIdx[k] in parallel; the reference's sequential instance loop is then
- * replayed on the results in TLAS order.  Lane k's result with depth kFarAway
- * equals the sequential call with the running depth D exactly (hit when t < D,
- * else miss) unless blasTraceTrack flagged a rounding hit; then lane k re-runs
- * the sequential call with depth D (never observed on the bundled scene, kept
- * for exactness).  All lanes must hold the same ray.  Returns the same
- * (hit, depth, u, v, inst, prim) as traceScene<false>. */
-__device__ __forceinline__ bool traceSceneCoop(const DevScene& S, const TraceTables& Tt, V3 o, V3 d, float& depth, float& hu,
-                                               float& hv, uint32_t& hinst, uint32_t& hprim, uint32_t* stk, float* astk,
-                                               uint32_t stride) {
-    const uint32_t lane = laneIdx();
-    const uint32_t n = S.tlasLeafCount;
-    float t = kFarAway, u = 0.0f, v = 0.0f;
-    uint32_t prim = kUnset, ii = kUnset;
-    bool hit = false, patho = false;
-    V3 oo = mk3(0.0f, 0.0f, 0.0f), dd = oo, rd = oo;
-    if (lane < n) {
-        ii = Tt.order[lane];
-        const TraceInst& I = Tt.inst[ii];
-        instanceRay(I, o, d, oo, dd);
-        rd = mk3(1.0f / dd.x, 1.0f / dd.y, 1.0f / dd.z);
-        if (S.finiteBoxes && finite3(oo) && finite3(rd))
-            hit = blasTraceTrack<true>(S, I, oo, dd, rd, t, u, v, prim, stk, astk, stride, patho);
-        else
-            hit = blasTraceTrack<false>(S, I, oo, dd, rd, t, u, v, prim, stk, astk, stride, patho);
-    }
-    /* replay of BvhTLAS::intersect's leaf loop (bvh.cpp:654-716) in TLAS order */
-    bool any = false;
-    float best = depth;
-    /* wave-uniform loop: v_readlane into SGPRs (no LDS round trip per value) */
-    const unsigned long long hitMask = __ballot(hit), pathoMask = __ballot(patho);
-    for (uint32_t k = 0; k < n; ++k) {
-        if (!((hitMask >> k) & 1ull)) continue;
-        float tk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t), (int)k));
-        if (!(tk < best)) continue;
-        float uk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(u), (int)k));
-        float vk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), (int)k));
-        uint32_t pk = (uint32_t)__builtin_amdgcn_readlane((int)prim, (int)k);
-        if ((pathoMask >> k) & 1ull) {
-            /* rounding case: lane k re-runs the sequential call with depth `best` */
-            bool h2 = false;
-            float t2 = best, u2 = 0.0f, v2 = 0.0f;
-            uint32_t p2 = kUnset;
-            if (lane == k) h2 = blasTrace<false, false>(S, Tt.inst[ii], oo, dd, rd, t2, u2, v2, p2, stk, stride, 0u);
-            if (!__shfl((int)h2, (int)k)) continue;
-            tk = __shfl(t2, (int)k); uk = __shfl(u2, (int)k); vk = __shfl(v2, (int)k); pk = (uint32_t)__shfl((int)p2, (int)k);
-        }
-        best = tk; hu = uk; hv = vk; hprim = pk;
-        hinst = Tt.order[k];
-        any = true;
-    }
-    depth = best;
-    return any;
-}
-
-/* Any hit: each instance's test is independent of the others (no depth update
- * survives a hit), so the sequential early-exit loop equals the OR. */
-__device__ __forceinline__ bool traceAnyCoop(const DevScene& S, const TraceTables& Tt, V3 o, V3 d, float tmaxv, uint32_t* stk,
-                                             uint32_t stride) {
-    const uint32_t lane = laneIdx();
-    bool occ = false;
-    if (lane < S.tlasLeafCount) {
-        float depth = tmaxv, u, v;
-        uint32_t prim;
-        occ = instanceTrace<true>(S, Tt.inst[Tt.order[lane]], o, d, depth, u, v, prim, stk, stride, 0u);
-    }
-    return __ballot(occ) != 0ull;
 }
 
 /* ------------------------------------------------- one ray per wave, lanes as planes
@@ -1113,27 +955,6 @@ __global__ __launch_bounds__(kBlock) void k_binscatter(const uint8_t* __restrict
     for (uint32_t i = a + threadIdx.x; i < b; i += blockDim.x) order[atomicAdd(&base[key[i]], 1u)] = i;
 }
 
-/* Move variant of k_binscatter: the records themselves (three float4 streams:
- * the pool's o, d, T or the shadow queue's o, d, c) are scattered to their
- * sorted slot, so the consumers read them sequentially with no order[]
- * indirection.  Reads are sequential, each lane's three 16-B writes land in
- * the bin's run of slots. */
-struct Rec3 { const float4* a; const float4* b; const float4* c; };
-struct Rec3w { float4* a; float4* b; float4* c; };
-__global__ __launch_bounds__(kBlock) void k_binmove(const uint8_t* __restrict__ key, const Counters* C, int par, int which,
-                                                    const uint32_t* __restrict__ hist, Rec3 src, Rec3w dst) {
-    __shared__ uint32_t base[kBins];
-    if (threadIdx.x < kBins) base[threadIdx.x] = hist[threadIdx.x * gridDim.x + blockIdx.x];
-    __syncthreads();
-    uint32_t a, b;
-    sortChunk(sortCount(C, par, which), a, b);
-    for (uint32_t i = a + threadIdx.x; i < b; i += blockDim.x) {
-        const float4 x = ldS(&src.a[i]), y = ldS(&src.b[i]), z = ldS(&src.c[i]);
-        const uint32_t p = atomicAdd(&base[key[i]], 1u);
-        stS(&dst.a[p], x); stS(&dst.b[p], y); stS(&dst.c[p], z);
-    }
-}
-
 /* ------------------------------------------------------------------ kernels */
 template <bool LDS>
 __global__ __launch_bounds__(kBlock, SURF_TRACE_WAVES) void k_extend(DevScene S, Pool cur, float4* __restrict__ hitTUV,
@@ -1155,164 +976,6 @@ __global__ __launch_bounds__(kBlock, SURF_TRACE_WAVES) void k_extend(DevScene S,
         const bool hit = traceScene<false>(S, Tt, xyz(o), xyz(d), depth, u, v, inst, prim, stk, stride);
         stS(&hitTUV[i], make_float4(depth, u, v, u2f(prim)));
         stSu(&hitInst[i], hit ? inst : kUnset);
-    }
-}
-
-/* ------------------------------------------------ persistent traversal
- * One ray per lane with the lanes running out of step: a lane whose ray is
- * done fetches the next ray of its wave's range while the others keep
- * traversing, and each lane walks the instance list on its own (the wave-
- * uniform instance loop of traceScene makes every instance cost the slowest
- * lane's BLAS walk).  Per lane the work is exactly traceScene's -- the same
- * instances in the same order, the same BLAS traversal -- only the
- * interleaving across rays changes, so results are identical.  Single-leaf
- * TLAS only (the bundled scene); the wave alternates between a setup phase
- * (fetch rays, enter the next instance) and a traversal phase (one node visit
- * per lane per step) that runs until kRefill lanes are waiting. */
-constexpr int kRefill = 16;
-
-struct PRay {                 /* a lane's ray state */
-    V3 o, d;                  /* world space */
-    V3 oo, dd, rd;            /* object space of instance k */
-    float depth, u, v;
-    uint32_t prim, inst, ii, k;
-    uint32_t node, nodeOff;
-    uint32_t* sp;
-    const float4* tri;
-    bool inB, fin, hitThis;
-};
-
-/* Enter instance pr.k (the reference's leaf loop body, bvh.cpp:481-513 + the
- * root step of BvhBLAS::intersect): transform, root leaf or root children.
- * Leaves pr.inB set when a BLAS walk starts; otherwise pr.k has advanced. */
-template <bool ANY>
-__device__ __forceinline__ void pEnter(const DevScene& S, const TraceTables& Tt, PRay& r, uint32_t* bottom, uint32_t stride) {
-    r.ii = Tt.order[r.k];
-    const TraceInst& I = Tt.inst[r.ii];
-    instanceRay(I, r.o, r.d, r.oo, r.dd);
-    r.rd = mk3(1.0f / r.dd.x, 1.0f / r.dd.y, 1.0f / r.dd.z);
-    r.fin = S.finiteBoxes && finite3(r.oo) && finite3(r.rd);
-    r.nodeOff = I.meta.x;
-    r.tri = S.tris + 3u * I.meta.y;
-    const float4 r0 = I.r0, r1 = I.r1;
-    const uint32_t rlf = f2u(r0.w), rcnt = f2u(r1.w);
-    if (rcnt != 0u) {
-        if (leafTest<ANY>(r.tri, rlf, rcnt, r.oo, r.dd, r.depth, r.u, r.v, r.prim)) { r.inst = r.ii; r.hitThis = true; }
-        ++r.k;
-        return;
-    }
-    float dn = r.fin ? slabFinite(r0.x, r0.y, r0.z, r1.x, r1.y, r1.z, r.oo, r.rd, r.depth)
-                     : slab(r0.x, r0.y, r0.z, r1.x, r1.y, r1.z, r.oo, r.rd, r.depth);
-    const float4 r2 = I.r2, r3 = I.r3;
-    float df = r.fin ? slabFinite(r2.x, r2.y, r2.z, r3.x, r3.y, r3.z, r.oo, r.rd, r.depth)
-                     : slab(r2.x, r2.y, r2.z, r3.x, r3.y, r3.z, r.oo, r.rd, r.depth);
-    uint32_t cn = r.nodeOff + rlf, cf = cn + 1u;
-    if (dn > df) { const float t = dn; dn = df; df = t; const uint32_t c = cn; cn = cf; cf = c; }
-    if (dn == kFarAway) { ++r.k; return; }
-    r.node = cn;
-    r.sp = bottom;
-    if (df != kFarAway) { *r.sp = cf; r.sp += stride; }
-    r.inB = true;
-}
-
-/* One node visit of the BLAS walk (BvhBLAS::intersect loop, bvh.cpp:129-191). */
-template <bool ANY>
-__device__ __forceinline__ void pStep(const DevScene& S, PRay& r, uint32_t* bottom, uint32_t stride) {
-    const float4* nd = S.nodes + 4u * r.node;
-    float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
-    pin(q0); pin(q1); pin(q2); pin(q3);
-    const uint32_t lf = f2u(q0.w), cnt = f2u(q1.w);
-    bool pop = false;
-    if (cnt != 0u) {
-        if (leafTest<ANY>(r.tri, lf, cnt, r.oo, r.dd, r.depth, r.u, r.v, r.prim)) {
-            r.hitThis = true;
-            if (ANY) { r.inB = false; return; }
-        }
-        pop = true;
-    } else {
-        float dn = r.fin ? slabFinite(q0.x, q0.y, q0.z, q1.x, q1.y, q1.z, r.oo, r.rd, r.depth)
-                         : slab(q0.x, q0.y, q0.z, q1.x, q1.y, q1.z, r.oo, r.rd, r.depth);
-        float df = r.fin ? slabFinite(q2.x, q2.y, q2.z, q3.x, q3.y, q3.z, r.oo, r.rd, r.depth)
-                         : slab(q2.x, q2.y, q2.z, q3.x, q3.y, q3.z, r.oo, r.rd, r.depth);
-        uint32_t cn = r.nodeOff + lf, cf = cn + 1u;
-        if (dn > df) { const float t = dn; dn = df; df = t; const uint32_t c = cn; cn = cf; cf = c; }
-        if (dn == kFarAway) pop = true;
-        else {
-            r.node = cn;
-            if (df != kFarAway) { *r.sp = cf; r.sp += stride; }
-        }
-    }
-    if (pop) {
-        if (r.sp == bottom) {          /* BLAS done: next instance */
-            r.inB = false;
-            if (r.hitThis) r.inst = r.ii;
-            ++r.k;
-        } else {
-            r.sp -= stride;
-            r.node = *r.sp;
-        }
-    }
-}
-
-template <bool LDS>
-__global__ __launch_bounds__(kBlock, SURF_TRACE_WAVES) void k_extend_p(DevScene S, Pool cur, float4* __restrict__ hitTUV,
-                                                                       uint32_t* __restrict__ hitInst, const Counters* C, int par,
-                                                                       uint32_t stackWords) {
-    extern __shared__ uint32_t lds[];
-    const TraceTables Tt = traceTables<LDS>(S, lds, stackWords);
-    const uint32_t n = C->nIn[par];
-    const uint32_t nInst = S.tlasLeafCount;
-    const uint32_t stride = blockDim.x;
-    uint32_t* const bottom = lds + threadIdx.x;
-    /* this wave's contiguous range of rays */
-    const uint32_t waves = gridDim.x * (blockDim.x >> 6);
-    const uint32_t w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    const uint32_t per = (n + waves - 1) / waves;
-    const uint32_t begin = min(n, w * per), end = min(n, begin + per);
-    uint32_t next = begin;
-    PRay r;
-    r.inB = false;
-    int ray = -1;
-    bool live = true;
-    for (;;) {
-        /* setup phase: refill lanes without a ray, advance lanes between instances */
-        for (;;) {
-            const bool need = live && ray < 0;
-            const unsigned long long mNeed = __ballot(need);
-            if (mNeed) {
-                const uint32_t cand = next + rankBelow(mNeed);
-                if (need) {
-                    if (cand < end) {
-                        ray = (int)cand;
-                        const float4 o4 = cur.o[cand], d4 = cur.d[cand];
-                        r.o = xyz(o4); r.d = xyz(d4);
-                        r.depth = kFarAway; r.u = 0.0f; r.v = 0.0f; r.prim = kUnset; r.inst = kUnset; r.k = 0;
-                    } else {
-                        live = false;
-                    }
-                }
-                next = min(end, next + (uint32_t)__popcll(mNeed));
-            }
-            const bool setup = live && ray >= 0 && !r.inB;
-            if (!__ballot(setup)) break;
-            if (setup) {
-                if (r.k >= nInst) {
-                    hitTUV[ray] = make_float4(r.depth, r.u, r.v, u2f(r.prim));
-                    hitInst[ray] = r.inst;
-                    ray = -1;
-                } else {
-                    r.hitThis = false;
-                    pEnter<false>(S, Tt, r, bottom, stride);
-                }
-            }
-        }
-        if (!__ballot(live)) break;
-        /* traversal phase */
-        for (;;) {
-            if (r.inB) pStep<false>(S, r, bottom, stride);
-            const unsigned long long waiting = __ballot(live && !r.inB);
-            if (__popcll(waiting) >= kRefill || !__ballot(r.inB)) break;
-        }
     }
 }
 
@@ -1522,45 +1185,6 @@ __device__ __forceinline__ void shadePath(const DevScene& S, const ShadeTables& 
     }
 }
 
-__device__ __forceinline__ uint32_t ldAgent(const uint32_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-/* Path-count bound of the long pools: k_shade reserves population before it
- * escapes a path (the rest of the wave's candidates stay in the wavefront). */
-__device__ __forceinline__ uint32_t reserveLong(Counters* C, uint32_t want, uint32_t cap) {
-    const uint32_t old = atomicAdd(&C->longPop, want);
-    const uint32_t room = old >= cap ? 0u : cap - old;
-    const uint32_t got = want < room ? want : room;
-    if (got < want) atomicSub(&C->longPop, want - got);
-    return got;
-}
-
-/* ---------------------------------------------------------- long-path escape
- * Wave-level append of the lanes with `want` set to escape queue q (one
- * atomic per wave); lanes beyond the queue's capacity stay in the wavefront.
- * Every lane of the wave calls it.  Returns whether this lane's path left. */
-template <class ShadeOutT>
-__device__ __forceinline__ bool escapeLong(Counters* C, const LongPools& LP, uint32_t q, bool want, const ShadeOutT& r) {
-    const unsigned long long m = __ballot(want);
-    if (!m) return false;
-    uint32_t base = 0, got = 0;
-    if (laneId() == 0) {
-        got = reserveLong(C, (uint32_t)__popcll(m), LP.lpCap);
-        if (got) base = atomicAdd(&C->escN[q], got);
-    }
-    base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
-    got = (uint32_t)__builtin_amdgcn_readfirstlane((int)got);
-    const uint32_t rank = rankBelow(m);
-    const uint32_t k = base + rank;
-    const bool esc = want && rank < got;        /* escCap == lpCap >= population: k < escCap */
-    if (esc) {
-        const EscQ& E = LP.esc[q];
-        E.o[k] = r.o; E.d[k] = r.d; E.T[k] = r.T; E.so[k] = r.so; E.sd[k] = r.sd;
-        E.sc[k] = make_float4(r.sc.x, r.sc.y, r.sc.z, r.shadow ? 1.0f : 0.0f);
-    }
-    return esc;
-}
-
 /* Frame completion: one atomic per distinct frame slot in the wave (lanes of a
  * wave almost always share one frame). */
 __device__ __forceinline__ void frameDoneAdd(uint32_t* frameDone, bool done, uint32_t slot) {
@@ -1578,7 +1202,7 @@ template <bool LDS_TABLES>
 __global__ __launch_bounds__(kBlock, SURF_SHADE_WAVES) void k_shade(DevScene S, Pool cur, Pool nxt, const float4* __restrict__ hitTUV,
                                                   const uint32_t* __restrict__ hitInst, ShadowQ Q,
                                                   float4* __restrict__ rad, uint32_t* __restrict__ frameDone,
-                                                  uint32_t npx, uint32_t window, Counters* C, int par, LongPools LP, uint32_t escQ,
+                                                  uint32_t npx, uint32_t window, Counters* C, int par,
                                                   const uint32_t* __restrict__ order) {
     if (blockIdx.x * blockDim.x >= C->nIn[par]) return;     /* nothing to shade in this block */
     __shared__ DevInstance sInst[LDS_TABLES ? kLdsInst : 1];
@@ -1595,7 +1219,6 @@ __global__ __launch_bounds__(kBlock, SURF_SHADE_WAVES) void k_shade(DevScene S, 
     __shared__ uint32_t sBase[2][2];
     const uint32_t n = C->nIn[par];
     const uint32_t maxSeg = C->maxSeg, zeroCutoff = C->zeroCutoff;
-    const uint32_t longThresh = C->longThresh;
     const uint32_t wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
     uint32_t it = 0;
     unsigned long long cHit = 0, cCont = 0, cSh = 0, cAcc = 0;
@@ -1615,10 +1238,7 @@ __global__ __launch_bounds__(kBlock, SURF_SHADE_WAVES) void k_shade(DevScene S, 
             shadePath(S, Tb, o4, ldS(&cur.d[j]), ldS(&cur.T[j]), ldS(&hitTUV[i]), hinst, maxSeg, zeroCutoff, r);
             if (r.addRad) addRadiance(rad, sid, r.radd);
         }
-        /* a path reaching longThresh segments leaves for the k_long worker,
-         * taking this bounce's shadow ray with it */
-        const bool esc = longThresh != 0u && escapeLong(C, LP, escQ, r.cont && r.seg + 1u >= longThresh, r);
-        const unsigned long long mCont = __ballot(r.cont && !esc), mSh = __ballot(r.shadow && !esc);
+        const unsigned long long mCont = __ballot(r.cont), mSh = __ballot(r.shadow);
         if (laneId() == 0) { sWave[it][wv][0] = (uint32_t)__popcll(mCont); sWave[it][wv][1] = (uint32_t)__popcll(mSh); }
         __syncthreads();
         if (threadIdx.x == 0) {
@@ -1632,11 +1252,11 @@ __global__ __launch_bounds__(kBlock, SURF_SHADE_WAVES) void k_shade(DevScene S, 
         for (uint32_t k = 0; k < wv; ++k) { jc += sWave[it][k][0]; js += sWave[it][k][1]; }
         jc += rankBelow(mCont);
         js += rankBelow(mSh);
-        if (r.cont && !esc) {
+        if (r.cont) {
             stS(&nxt.o[jc], r.o); stS(&nxt.d[jc], r.d); stS(&nxt.T[jc], r.T);
             nxt.key[jc] = poolKey(S, hinst, r.o, r.d);   /* starts on the instance it hit, from this quadrant */
         }
-        if (r.shadow && !esc) {
+        if (r.shadow) {
             stS(&Q.o[js], r.so); stS(&Q.d[js], r.sd); stS(&Q.c[js], r.sc);
             Q.key[js] = shadowKey(S, r.light, r.so);       /* toward the same light from the same octant of the scene */
         }
@@ -1741,6 +1361,7 @@ __global__ __launch_bounds__(kBlock) void k_regen(DevCamera cam, Pool nxt, float
         C->issued[nx] = iss + nnew;
         C->app[nx] = 0ull;             /* next phase's append cursors */
         C->ev[0] += cont + nnew;     /* extension rays of the next phase */
+        C->ev[8] += cont + nnew;     /* ... traced by k_extend unless the drain takes the pool */
     }
 }
 
@@ -1838,285 +1459,25 @@ __global__ __launch_bounds__(64, SURF_TAIL_WAVES) void k_tail(DevScene S, Pool c
             lds + threadIdx.x, blockDim.x, firstCounted);
 }
 
-/* Radiance add of the long-path worker: rad[sid] += c per channel, bit-exact
- * (an IEEE f32 add in the ALU, installed by compare-and-swap).  The worker is
- * the path's only writer, so the swap succeeds at once; it only has to be an
- * agent-scope atomic because the worker runs beside the wavefront kernels,
- * which write other samples of the same cache lines. */
-__device__ __forceinline__ void addExact(float* p, float c) {
-    unsigned int* u = reinterpret_cast<unsigned int*>(p);
-    unsigned int old = ldAgent(u);
-    for (;;) {
-        const unsigned int nv = __float_as_uint(__uint_as_float(old) + c);
-        const unsigned int prev = atomicCAS(u, old, nv);
-        if (prev == old) return;
-        old = prev;
-    }
-}
-__device__ __forceinline__ void addRadianceAtomic(float4* rad, uint32_t sid, V3 c) {
-    float* r = reinterpret_cast<float*>(rad + sid);
-    addExact(r + 0, c.x); addExact(r + 1, c.y); addExact(r + 2, c.z);
-}
-
-/* Long-path step (the second chain of the phase graph, running beside the
- * wavefront kernels): every path of lp[in] and of escape queue eq advances up
- * to Counters::longBudget segments in its lane (extend -> shade -> shadow ray,
- * the wavefront kernels' device functions); paths still alive are appended to
- * lp[in ^ 1].  An escaped path first resolves the shadow ray of the bounce it
- * escaped on.  Radiance adds are compare-and-swap (this kernel runs beside
- * wavefront kernels that write other samples of the same cache lines).  The
- * last block to finish resets the counts of the queues it consumed. */
-template <bool LDS_TABLES>
-__global__ __launch_bounds__(kBlock, 2) void k_long(DevScene S, LongPools LP, float4* __restrict__ rad,
-                                                 uint32_t* __restrict__ frameDone, uint32_t npx, uint32_t window,
-                                                 Counters* C, uint32_t in, uint32_t eq, uint32_t stackWords) {
-    extern __shared__ uint32_t lds[];
-    __shared__ DevInstance sInst[LDS_TABLES ? kLdsInst : 1];
-    __shared__ DevMaterial sMat[LDS_TABLES ? kLdsMats : 1];
-    __shared__ uint2 sLights[LDS_TABLES ? kLdsLights : 1];
-    const uint32_t nL = min(C->lpN[in], LP.lpCap), nE = min(C->escN[eq], LP.escCap), n = nL + nE;
-    if (blockIdx.x * blockDim.x < n) {
-        __builtin_amdgcn_s_setprio(2);     /* latency work beside the wavefront's throughput kernels */
-        const TraceTables Tt = traceTables<LDS_TABLES>(S, lds, stackWords);
-        ShadeTables Tb{S.inst, S.mats, S.lights};
-        if (LDS_TABLES) {
-            stageTables(S, sInst, sMat, sLights);
-            Tb = ShadeTables{sInst, sMat, sLights};
-        }
-        uint32_t* stk = lds + threadIdx.x;
-        const uint32_t stride = blockDim.x;
-        const uint32_t maxSeg = C->maxSeg, zeroCutoff = C->zeroCutoff, budget = C->longBudget;
-        const Pool src = LP.lp[in], dst = LP.lp[in ^ 1u];
-        const EscQ E = LP.esc[eq];
-        uint32_t* fd = frameDone + (blockIdx.x % kStripes) * window;
-        unsigned long long cExt = 0, cHit = 0, cCont = 0, cSh = 0, cAcc = 0, cUn = 0, cFin = 0;
-        for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
-            const uint32_t v = base + threadIdx.x;
-            const bool active = v < n;
-            float4 o4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), d4 = o4, T4 = o4;
-            bool alive = false;
-            uint32_t nExt = 0, nHit = 0, nCont = 0, nSh = 0, nAcc = 0, nUn = 0;
-            if (active) {
-                alive = true;
-                if (v < nL) {
-                    o4 = src.o[v]; d4 = src.d[v]; T4 = src.T[v];
-                } else {
-                    const uint32_t k = v - nL;
-                    o4 = E.o[k]; d4 = E.d[k]; T4 = E.T[k];
-                    const float4 sc = E.sc[k];
-                    if (sc.w != 0.0f) {
-                        /* the escaping bounce's shadow ray (n_shadow counted by k_shade) */
-                        const float4 so = E.so[k], sd = E.sd[k];
-                        float sdep = so.w, su = 0.0f, sv = 0.0f;
-                        uint32_t si = kUnset, sp = kUnset;
-                        if (!traceScene<true>(S, Tt, xyz(so), xyz(sd), sdep, su, sv, si, sp, stk, stride)) {
-                            addRadianceAtomic(rad, f2u(sd.w), xyz(sc));
-                            ++nUn; ++nAcc;
-                        }
-                    }
-                }
-                for (uint32_t sgm = 0; sgm < budget; ++sgm) {
-                    float depth = kFarAway, u = 0.0f, vv = 0.0f;
-                    uint32_t inst = kUnset, prim = kUnset;
-                    const bool hit = traceScene<false>(S, Tt, xyz(o4), xyz(d4), depth, u, vv, inst, prim, stk, stride);
-                    ++nExt;
-                    ShadeOut r;
-                    shadePath(S, Tb, o4, d4, T4, make_float4(depth, u, vv, u2f(prim)), hit ? inst : kUnset, maxSeg, zeroCutoff, r);
-                    if (r.addRad) addRadianceAtomic(rad, f2u(o4.w), r.radd);
-                    nHit += r.hitGeom; nAcc += r.accd;
-                    if (r.shadow) {
-                        ++nSh;
-                        float sdep = r.so.w, su = 0.0f, sv = 0.0f;
-                        uint32_t si = kUnset, sp = kUnset;
-                        if (!traceScene<true>(S, Tt, xyz(r.so), xyz(r.sd), sdep, su, sv, si, sp, stk, stride)) {
-                            addRadianceAtomic(rad, f2u(r.sd.w), xyz(r.sc));
-                            ++nUn; ++nAcc;
-                        }
-                    }
-                    if (r.capped) {
-                        const unsigned long long kc = atomicAdd(&C->ev[7], 1ull);
-                        if (kc < 64) C->capped[kc] = f2u(o4.w);
-                    }
-                    if (!r.cont) {
-                        atomicMax(&C->segMax, r.seg);
-                        alive = false;
-                        break;
-                    }
-                    ++nCont;
-                    o4 = r.o; d4 = r.d; T4 = r.T;
-                }
-            }
-            /* survivors to the other long pool (one atomic per wave; the
-             * population is bounded by lpCap where k_shade escapes) */
-            const unsigned long long mA = __ballot(alive);
-            if (mA) {
-                const uint32_t j = waveAppend(&C->lpN[in ^ 1u], mA);
-                if (alive) { dst.o[j] = o4; dst.d[j] = d4; dst.T[j] = T4; }
-            }
-            const bool fin = active && !alive;
-            frameDoneAdd(fd, fin, f2u(o4.w) / npx);
-            const unsigned long long mF = __ballot(fin);
-            if (laneId() == 0 && mF) atomicSub(&C->longPop, (uint32_t)__popcll(mF));
-            cExt += nExt; cHit += nHit; cCont += nCont; cSh += nSh; cAcc += nAcc; cUn += nUn; cFin += fin;
-        }
-        /* per-lane totals -> one atomic per counter per wave */
-        unsigned long long* ev = C->evS[blockIdx.x % kStripes];
-        const unsigned long long vals[7] = {cExt, cHit, cCont, cSh, cAcc, cUn, cFin};
-        const int idx[7] = {0, 1, 2, 3, 4, 5, 8};
-#pragma unroll
-        for (int q = 0; q < 7; ++q) {
-            unsigned long long t = vals[q];
-            for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off);
-            if (laneId() == 0 && t) atomicAdd(&ev[idx[q]], t);
-        }
-    }
-    /* last block out resets the consumed queues' counts (k_long(ph + 1) and
-     * k_shade(ph + 3) come after this launch in the graph) */
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __threadfence();
-        if (atomicAdd(&C->lpDone, 1u) == gridDim.x - 1u) {
-            atomicExch(&C->lpN[in], 0u);
-            atomicExch(&C->escN[eq], 0u);
-            atomicExch(&C->lpDone, 0u);
-        }
-    }
-}
-
-/* k_long with one path per 64-lane block (traceWave, the cooperative tail's
- * segment): same inputs, outputs, counters and queue protocol as k_long, for
- * long paths whose per-segment latency, not their number, is what matters.
- * LDS: the traversal's record stack (stackWords = 16 x depth), then the trace
- * tables.  Shading tables from global memory (wave-uniform reads). */
-__global__ __launch_bounds__(64, SURF_COOP_WAVES) void k_long_wave(DevScene S, LongPools LP, float4* __restrict__ rad,
-                                                                   uint32_t* __restrict__ frameDone, uint32_t npx, uint32_t window,
-                                                                   Counters* C, uint32_t in, uint32_t eq, uint32_t stackWords) {
-    extern __shared__ uint32_t lds[];
-    const uint32_t nL = min(C->lpN[in], LP.lpCap), nE = min(C->escN[eq], LP.escCap), n = nL + nE;
-    if (blockIdx.x < n) {
-        __builtin_amdgcn_s_setprio(2);
-        const TraceTables Tt = stageTrace(S, lds, stackWords);
-        const ShadeTables Tb{S.inst, S.mats, S.lights};
-        float* rstk = reinterpret_cast<float*>(lds);
-        const bool lead = threadIdx.x == 0;
-        const uint32_t maxSeg = C->maxSeg, zeroCutoff = C->zeroCutoff, budget = C->longBudget;
-        const Pool src = LP.lp[in], dst = LP.lp[in ^ 1u];
-        const EscQ E = LP.esc[eq];
-        uint32_t* fd = frameDone + (blockIdx.x % kStripes) * window;
-        unsigned long long cExt = 0, cHit = 0, cCont = 0, cSh = 0, cAcc = 0, cUn = 0, cFin = 0;
-        for (uint32_t v = blockIdx.x; v < n; v += gridDim.x) {
-            float4 o4, d4, T4;
-            if (v < nL) {
-                o4 = src.o[v]; d4 = src.d[v]; T4 = src.T[v];
-            } else {
-                const uint32_t k = v - nL;
-                o4 = E.o[k]; d4 = E.d[k]; T4 = E.T[k];
-                const float4 sc = E.sc[k];
-                if (sc.w != 0.0f) {
-                    /* the escaping bounce's shadow ray (n_shadow counted by k_shade) */
-                    const float4 so = E.so[k], sd = E.sd[k];
-                    float sdep = so.w, su = 0.0f, sv = 0.0f;
-                    uint32_t si = kUnset, sp = kUnset;
-                    if (!traceWave<true>(S, Tt, xyz(so), xyz(sd), sdep, su, sv, si, sp, rstk)) {
-                        if (lead) addRadianceAtomic(rad, f2u(sd.w), xyz(sc));
-                        ++cUn; ++cAcc;
-                    }
-                }
-            }
-            bool alive = true;
-            for (uint32_t sgm = 0; sgm < budget; ++sgm) {
-                float depth = kFarAway, u = 0.0f, vv = 0.0f;
-                uint32_t inst = kUnset, prim = kUnset;
-                const bool hit = traceWave<false>(S, Tt, xyz(o4), xyz(d4), depth, u, vv, inst, prim, rstk);
-                ++cExt;
-                ShadeOut r;
-                shadePath(S, Tb, o4, d4, T4, make_float4(depth, u, vv, u2f(prim)), hit ? inst : kUnset, maxSeg, zeroCutoff, r);
-                if (lead && r.addRad) addRadianceAtomic(rad, f2u(o4.w), r.radd);
-                cHit += r.hitGeom; cAcc += r.accd;
-                if (r.shadow) {
-                    ++cSh;
-                    float sdep = r.so.w, su = 0.0f, sv = 0.0f;
-                    uint32_t si = kUnset, sp = kUnset;
-                    if (!traceWave<true>(S, Tt, xyz(r.so), xyz(r.sd), sdep, su, sv, si, sp, rstk)) {
-                        if (lead) addRadianceAtomic(rad, f2u(r.sd.w), xyz(r.sc));
-                        ++cUn; ++cAcc;
-                    }
-                }
-                if (lead && r.capped) {
-                    const unsigned long long kc = atomicAdd(&C->ev[7], 1ull);
-                    if (kc < 64) C->capped[kc] = f2u(o4.w);
-                }
-                if (!r.cont) {
-                    if (lead) atomicMax(&C->segMax, r.seg);
-                    alive = false;
-                    break;
-                }
-                ++cCont;
-                o4 = r.o; d4 = r.d; T4 = r.T;
-            }
-            if (lead) {
-                if (alive) {
-                    const uint32_t j = atomicAdd(&C->lpN[in ^ 1u], 1u);
-                    dst.o[j] = o4; dst.d[j] = d4; dst.T[j] = T4;
-                } else {
-                    __threadfence();
-                    atomicAdd(&fd[f2u(o4.w) / npx], 1u);
-                    atomicSub(&C->longPop, 1u);
-                    ++cFin;
-                }
-            }
-        }
-        if (lead) {
-            unsigned long long* ev = C->evS[blockIdx.x % kStripes];
-            const unsigned long long vals[7] = {cExt, cHit, cCont, cSh, cAcc, cUn, cFin};
-            const int idx[7] = {0, 1, 2, 3, 4, 5, 8};
-#pragma unroll
-            for (int q = 0; q < 7; ++q)
-                if (vals[q]) atomicAdd(&ev[idx[q]], vals[q]);
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __threadfence();
-        if (atomicAdd(&C->lpDone, 1u) == gridDim.x - 1u) {
-            atomicExch(&C->lpN[in], 0u);
-            atomicExch(&C->escN[eq], 0u);
-            atomicExch(&C->lpDone, 0u);
-        }
-    }
-}
-
-/* Cooperative tail: one path per 64-lane wave (block), for the few very long
- * paths left at the end of a drain, whose single-lane segment latency bounds
- * the drain.  Each segment: closest hit with the instances traced in parallel
- * lanes (traceSceneCoop), shading evaluated redundantly by every lane (same
- * inputs, same results, no broadcast), shadow ray any-hit in parallel lanes;
- * lane 0 does the writes.  Identical results to k_tail.  LDS: traversal stack,
- * box-distance stack (stackWords words each), then the trace tables. */
-template <bool LDS_TABLES, bool WAVE>
-__global__ __launch_bounds__(64, LDS_TABLES ? 3 : SURF_COOP_WAVES) void k_tail_coop(DevScene S, Pool cur, uint32_t n, float4* __restrict__ rad,
+/* Cooperative tail: one path per 64-lane wave (block), for the long paths
+ * left at the end of a drain, whose single-lane segment latency bounds the
+ * drain.  Each segment: closest hit with the lanes-as-planes wave traversal
+ * (traceWave), shading evaluated redundantly by every lane (same inputs, same
+ * results, no broadcast), shadow ray any-hit with the same traversal; lane 0
+ * does the writes.  Identical results to k_tail.  LDS: the record stack
+ * (stackWords = 16 x depth words), then the trace tables; the shading tables
+ * are read from global memory (wave-uniform reads): LDS copies would cap the
+ * one-wave blocks at ~2 waves per SIMD. */
+__global__ __launch_bounds__(64, SURF_COOP_WAVES) void k_tail_coop(DevScene S, Pool cur, uint32_t n, float4* __restrict__ rad,
                                                   uint32_t* __restrict__ frameDone, uint32_t npx, uint32_t window, Counters* C,
                                                   uint32_t stackWords, uint32_t firstCounted) {
     extern __shared__ uint32_t lds[];
-    /* WAVE: the trace tables (instances x 180 B) always in LDS -- every lane of
-     * traceWave's prologue reads its own instance record; the shading tables
-     * (static, sized for 64 instances/materials) only with LDS_TABLES */
-    const TraceTables Tt = traceTables<LDS_TABLES || WAVE>(S, lds, 2u * stackWords);
-    __shared__ DevInstance sInst[LDS_TABLES ? kLdsInst : 1];
-    __shared__ DevMaterial sMat[LDS_TABLES ? kLdsMats : 1];
-    __shared__ uint2 sLights[LDS_TABLES ? kLdsLights : 1];
-    ShadeTables Tb{S.inst, S.mats, S.lights};
-    if (LDS_TABLES) {
-        stageTables(S, sInst, sMat, sLights);
-        Tb = ShadeTables{sInst, sMat, sLights};
-    }
+    const TraceTables Tt = stageTrace(S, lds, stackWords);
+    const ShadeTables Tb{S.inst, S.mats, S.lights};
     const uint32_t i = blockIdx.x;
     if (i >= n) return;
     const bool lead = threadIdx.x == 0;
-    uint32_t* stk = lds + threadIdx.x;
-    float* astk = reinterpret_cast<float*>(lds + stackWords) + threadIdx.x;
-    float* rstk = reinterpret_cast<float*>(lds);     /* WAVE: the record stack (16 words per entry) */
-    const uint32_t stride = blockDim.x;
+    float* rstk = reinterpret_cast<float*>(lds);     /* the record stack (16 words per entry) */
     const uint32_t maxSeg = C->maxSeg, zeroCutoff = C->zeroCutoff;
     float4 o4 = cur.o[i], d4 = cur.d[i], T4 = cur.T[i];
     const uint32_t slot = f2u(o4.w) / npx;
@@ -2134,8 +1495,7 @@ __global__ __launch_bounds__(64, LDS_TABLES ? 3 : SURF_COOP_WAVES) void k_tail_c
 #if SURF_SEG_TIMING
         const unsigned long long c0 = __builtin_readcyclecounter();
 #endif
-        const bool hit = WAVE ? traceWave<false>(S, Tt, xyz(o4), xyz(d4), depth, u, v, inst, prim, rstk, ssp)
-                              : traceSceneCoop(S, Tt, xyz(o4), xyz(d4), depth, u, v, inst, prim, stk, astk, stride);
+        const bool hit = traceWave<false>(S, Tt, xyz(o4), xyz(d4), depth, u, v, inst, prim, rstk, ssp);
         (void)ssp;
         ++nExt;
         ShadeOut r;
@@ -2152,14 +1512,9 @@ __global__ __launch_bounds__(64, LDS_TABLES ? 3 : SURF_COOP_WAVES) void k_tail_c
         nHit += r.hitGeom; nAcc += r.accd;
         if (r.shadow) {
             ++nSh;
-            bool occ;
-            if (WAVE) {
-                float sdep = r.so.w, su = 0.0f, sv = 0.0f;
-                uint32_t si = kUnset, sp = kUnset;
-                occ = traceWave<true>(S, Tt, xyz(r.so), xyz(r.sd), sdep, su, sv, si, sp, rstk);
-            } else {
-                occ = traceAnyCoop(S, Tt, xyz(r.so), xyz(r.sd), r.so.w, stk, stride);
-            }
+            float sdep = r.so.w, su = 0.0f, sv = 0.0f;
+            uint32_t si = kUnset, sp = kUnset;
+            const bool occ = traceWave<true>(S, Tt, xyz(r.so), xyz(r.sd), sdep, su, sv, si, sp, rstk);
             if (!occ) {
                 if (lead) addRadiance(rad, f2u(r.sd.w), xyz(r.sc));
                 ++nUn; ++nAcc;
@@ -2291,29 +1646,25 @@ __global__ __launch_bounds__(kBlock) void k_trace_any(DevScene S, const float* _
                               depth, u, v, inst, prim, lds + threadIdx.x, blockDim.x) ? 1 : 0;
 }
 
-/* Cooperative traversal entry points (one ray per 64-lane block): the same
- * results as k_trace_closest / k_trace_any, exposed for parity tests and
- * latency measurements of the cooperative tail's traversal. */
-template <bool WAVE>
+/* Cooperative traversal entry points (one ray per 64-lane block, the
+ * lanes-as-planes traversal of the cooperative tail): the same results as
+ * k_trace_closest / k_trace_any, for parity tests and latency measurements. */
 __global__ __launch_bounds__(64) void k_trace_closest_coop(DevScene S, const float* __restrict__ o, const float* __restrict__ d,
                                                            uint32_t n, float4* __restrict__ tuv, uint2* __restrict__ ip,
                                                            uint32_t stackWords) {
     extern __shared__ uint32_t lds[];
-    const TraceTables Tt = stageTrace(S, lds, 2u * stackWords);
+    const TraceTables Tt = stageTrace(S, lds, stackWords);
     const uint32_t i = blockIdx.x;
     if (i >= n) return;
     float depth = kFarAway, u = 0.0f, v = 0.0f;
     uint32_t inst = kUnset, prim = kUnset;
     const V3 ro = mk3(o[3 * i], o[3 * i + 1], o[3 * i + 2]), rdir = mk3(d[3 * i], d[3 * i + 1], d[3 * i + 2]);
-    const bool hit = WAVE ? traceWave<false>(S, Tt, ro, rdir, depth, u, v, inst, prim, reinterpret_cast<float*>(lds))
-                          : traceSceneCoop(S, Tt, ro, rdir, depth, u, v, inst, prim, lds + threadIdx.x,
-                                           reinterpret_cast<float*>(lds + stackWords) + threadIdx.x, blockDim.x);
+    const bool hit = traceWave<false>(S, Tt, ro, rdir, depth, u, v, inst, prim, reinterpret_cast<float*>(lds));
     if (threadIdx.x == 0) {
         tuv[i] = make_float4(depth, hit ? u : 0.0f, hit ? v : 0.0f, 0.0f);
         ip[i] = make_uint2(hit ? inst : kUnset, hit ? prim : kUnset);
     }
 }
-template <bool WAVE>
 __global__ __launch_bounds__(64) void k_trace_any_coop(DevScene S, const float* __restrict__ o, const float* __restrict__ d,
                                                        const float* __restrict__ tmaxv, uint32_t n, uint8_t* __restrict__ occ,
                                                        uint32_t stackWords) {
@@ -2322,14 +1673,9 @@ __global__ __launch_bounds__(64) void k_trace_any_coop(DevScene S, const float* 
     const uint32_t i = blockIdx.x;
     if (i >= n) return;
     const V3 ro = mk3(o[3 * i], o[3 * i + 1], o[3 * i + 2]), rdir = mk3(d[3 * i], d[3 * i + 1], d[3 * i + 2]);
-    bool oc;
-    if (WAVE) {
-        float depth = tmaxv[i], u = 0.0f, v = 0.0f;
-        uint32_t inst = kUnset, prim = kUnset;
-        oc = traceWave<true>(S, Tt, ro, rdir, depth, u, v, inst, prim, reinterpret_cast<float*>(lds));
-    } else {
-        oc = traceAnyCoop(S, Tt, ro, rdir, tmaxv[i], lds + threadIdx.x, blockDim.x);
-    }
+    float depth = tmaxv[i], u = 0.0f, v = 0.0f;
+    uint32_t inst = kUnset, prim = kUnset;
+    const bool oc = traceWave<true>(S, Tt, ro, rdir, depth, u, v, inst, prim, reinterpret_cast<float*>(lds));
     if (threadIdx.x == 0) occ[i] = oc ? 1 : 0;
 }
 

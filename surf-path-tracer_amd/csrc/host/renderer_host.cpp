@@ -3,8 +3,11 @@
  * the C-ABI.  render() keeps the reference's frame semantics: every call adds
  * config().samplesPerFrame samples per pixel, each seeded from the running
  * sample count (renderer.cpp:169, 983), and camera state is re-read per frame
- * (renderer.cpp:972-979).  Errors throw std::runtime_error (the reference
- * aborts through VK_CHECK).
+ * (renderer.cpp:972-979).  render() returns once the frame's samples are
+ * issued: consecutive frames form one sample stream on the device (no
+ * per-frame drain); reads (accumulator, images, frameInfo() with lumenOutput)
+ * drain it.  Errors throw std::runtime_error (the reference aborts through
+ * VK_CHECK).
  */
 #include "surf/surf_host.hpp"
 
@@ -34,6 +37,8 @@ WaveFrontRenderer::~WaveFrontRenderer() { surf_destroy(m_ctx); }
 void WaveFrontRenderer::clearAccumulator() {
     check(surf_clear_accumulator(m_ctx), m_ctx, "surf_clear_accumulator");
     m_totalSamples = 0;
+    m_frameInfo = FrameInstrumentationData{};
+    m_energyStale = false;
 }
 
 void WaveFrontRenderer::render(F32 /*deltaTime*/) {
@@ -51,11 +56,25 @@ void WaveFrontRenderer::render(F32 /*deltaTime*/) {
     const U32 spp = m_config.samplesPerFrame ? m_config.samplesPerFrame : 1u;
     check(surf_render(m_ctx, spp, m_totalSamples, m_config.maxSegments, 1), m_ctx, "surf_render");
     m_totalSamples += spp;
-    surf_stats st;
-    check(surf_get_stats(m_ctx, &st), m_ctx, "surf_get_stats");
-    m_frameInfo.energy = st.energy;
     m_frameInfo.totalSamples = m_totalSamples;
+    m_energyStale = true;       /* render() itself never waits for the stream (no per-frame drain) */
 }
+
+/* The reference computes the Lumen energy only with WF_LUMEN_OUTPUT
+ * (renderer.cpp:31, off by default; :955-969), from the accumulator of the
+ * frames rendered so far.  Here it is computed when asked for: the energy
+ * needs every rendered frame accumulated, which drains the sample stream. */
+const FrameInstrumentationData& WaveFrontRenderer::frameInfo() {
+    if (m_config.lumenOutput && m_energyStale && m_totalSamples) {
+        surf_stats st;
+        check(surf_get_stats(m_ctx, &st), m_ctx, "surf_get_stats");
+        m_frameInfo.energy = st.energy;
+        m_energyStale = false;
+    }
+    return m_frameInfo;
+}
+
+void WaveFrontRenderer::synchronize() { check(surf_synchronize(m_ctx), m_ctx, "surf_synchronize"); }
 
 std::vector<F32> WaveFrontRenderer::readAccumulator() {
     std::vector<F32> out((size_t)m_resolution.width * m_resolution.height * 4);

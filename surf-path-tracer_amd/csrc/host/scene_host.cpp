@@ -1116,6 +1116,26 @@ void buildIndoor(surf_scene& S, const std::string& dir, int variant) {
     inst.emplace_back(planeB, floorM, scale(rotate(translate(I, Float3(0.0f, 4.0f, -10.0f)), radians(90.0f), WORLD_RIGHT), Float3(10.0f, 10.0f, 5.0f)));
     inst.emplace_back(planeB, floorM, scale(rotate(translate(I, Float3(0.0f, 4.0f, 10.0f)), radians(90.0f), WORLD_RIGHT), Float3(10.0f, 10.0f, 5.0f)));
     if (lattice) inst.emplace_back(S.blases[4].get(), diffuse, I);
+    if (variant == 2 || variant == 3) {
+        /* general-TLAS test scenes (not in the reference's main.cpp): extra
+         * instances of the cube / Suzanne / lens meshes, sizes 0.3-0.9 and
+         * rotations varied so that BvhTLAS::build splits (bvh.cpp:780-993):
+         * 40 extras (51 instances, LDS tables) or 80 (91, global tables) */
+        BvhBLAS* meshes[3] = {cubeB, susB, lensB};
+        Material* mats[5] = {floorM, diffuse, specular, dielectric, wallGreen};
+        const int extra = variant == 2 ? 40 : 80;
+        for (int k = 0; k < extra; ++k) {
+            const F32 x = -8.5f + 1.0f * (F32)((k * 7) % 18);
+            const F32 y = -0.4f + 0.9f * (F32)((k * 5) % 10);
+            F32 z = -8.5f + 1.0f * (F32)((k * 11) % 18);
+            if (x > -2.5f && x < 2.5f && y < 2.5f && z < -4.5f) z = z + 6.0f;   /* keep clear of the camera (0, 0, -7) */
+            const F32 sc = 0.3f + 0.15f * (F32)(k % 5);
+            Mat4 X = translate(I, Float3(x, y, z));
+            if (k % 3 == 1) X = rotate(X, radians(17.0f * (F32)(k % 7)), WORLD_UP);
+            X = scale(X, Float3(sc, sc, sc));
+            inst.emplace_back(meshes[k % 3], mats[k % 5], X);
+        }
+    }
 
     SceneBackground bg;
     bg.type = BackgroundType::ColorGradient;
@@ -1131,7 +1151,7 @@ void buildIndoor(surf_scene& S, const std::string& dir, int variant) {
 extern "C" {
 
 int surf_scene_build_indoor(const char* assets_dir, int variant, surf_scene** out) {
-    if (!out || (variant != 0 && variant != 1)) return SURF_ERR_INVALID;
+    if (!out || variant < 0 || variant > 3) return SURF_ERR_INVALID;
     *out = nullptr;
     auto s = std::make_unique<surf_scene>();
     try {

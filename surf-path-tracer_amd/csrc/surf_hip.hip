@@ -30,6 +30,7 @@ using namespace surfdev;
 namespace {
 
 constexpr int kPhasesPerGraph = 8;          /* even: parity returns to 0 after a replay */
+constexpr int kPhaseEvents = 6;             /* profiling events per phase: sort, extend, shade, sort, connect, regen */
 constexpr uint32_t kMaxStack = 120;          /* LDS stack entries per ray (block 256 -> 120 KiB max) */
 constexpr uint64_t kMaxIterations = 1ull << 22;  /* safety net: a path longer than this is a bug */
 
@@ -60,7 +61,7 @@ struct surf_ctx {
 
     /* scene */
     bool hasScene = false;
-    uint32_t extBlock = 128;       /* k_extend workgroup size (SURF_EXTEND_BLOCK=128|256): 128 measured 5 % faster */
+    uint32_t extBlock = 128;       /* k_extend workgroup size (SURF_EXTEND_BLOCK=128|256): 128 measured 5 % faster on k_extend */
     bool connectGlobal = false;    /* k_connect reads its tables from global memory (SURF_CONNECT_GLOBAL=1, tuning) */
     bool ldsTables = false;        /* instance/material/light tables fit the per-workgroup LDS copy */
     DevScene S{};
@@ -110,24 +111,13 @@ struct surf_ctx {
     int drainReplays = 1;          /* graph replays per host poll while draining (SURF_DRAIN_REPLAYS) */
     bool coopEligible = false;     /* single-leaf TLAS of <= 64 instances, LDS tables */
     int traceMode = 0;             /* surf_trace_closest/_any: 0 one ray per lane, 1 one ray per wave */
-    bool persistent = false;       /* out-of-step lanes with per-wave ray ranges: measured 4x slower */
     bool sortRays = true;          /* order each phase's rays by start instance (SURF_SORT=0: off) */
-    bool moveRays = false;         /* sort by moving the records into srt/srtQ instead of indexing them (SURF_SORT_MOVE=1) */
-    Pool srt{};                    /* the phase's pool in sorted order (moveRays) */
-    ShadowQ srtQ{};                /* the phase's shadow queue in sorted order (moveRays) */
-    /* long paths: escape queues + long pools, advanced by the k_long chain of the graph (surf_set_long_paths) */
-    uint32_t longThresh = 0;       /* escape length (0 = off) */
-    uint32_t longBudget = 8;       /* segments per long path per phase */
-    bool longWave = false;         /* k_long_wave (one path per wave) instead of k_long (SURF_LONG_WAVE=1) */
-    uint32_t longBlocks = 0;       /* k_long_wave grid (SURF_LONG_BLOCKS; default 4 waves per CU) */
-    hipStream_t stream2 = nullptr; /* the k_long branch while the graph is captured */
-    hipEvent_t evFork = nullptr, evShade[kPhasesPerGraph] = {}, evLong[kPhasesPerGraph] = {};
-    LongPools LP{};
     /* ray order (k_bincount / k_binscan / k_binscatter each phase) */
     uint32_t* order = nullptr;
     uint32_t* binHist = nullptr;
     uint32_t tailLanes = 0;
     uint32_t segMaxBase = 0;       /* longest path of finished streams */
+    uint64_t tailFirstRays = 0;    /* first extension rays of drained paths: counted by regen, traced by the tail */
 
     /* graph */
     hipGraphExec_t graphExec = nullptr;
@@ -135,7 +125,7 @@ struct surf_ctx {
     uint32_t gridWork = 0, gridRegen = 0, gridExtend = 0, gridConnect = 0;
 
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    hipEvent_t pev[kPhasesPerGraph * 4 + 1] = {};
+    hipEvent_t pev[kPhasesPerGraph * kPhaseEvents + 1] = {};   /* profiling: kPhaseEvents per phase + the end */
     surf_stats stats{};
     unsigned long long evBase[kEvents] = {};   /* event counts of finished streams since the last clear */
 };
@@ -188,6 +178,10 @@ void destroyGraph(surf_ctx* c) {
 uint32_t stackWords(const surf_ctx* c, uint32_t block) { return c->stackDepth * block; }
 /* one-ray-per-wave traversal (traceWave): a stack of node records, 16 words per entry */
 uint32_t recStackWords(const surf_ctx* c) { return c->stackDepth * 16u; }
+/* Dynamic LDS of the one-ray-per-wave kernels: the record stack, then the trace tables. */
+size_t coopLds(const surf_ctx* c) {
+    return (size_t)recStackWords(c) * sizeof(float) + (size_t)c->nInstances * (sizeof(TraceInst) + sizeof(uint32_t));
+}
 size_t traversalLds(const surf_ctx* c, uint32_t block) {
     size_t b = (size_t)stackWords(c, block) * sizeof(uint32_t);
     if (c->ldsTables) b += (size_t)c->nInstances * (sizeof(TraceInst) + sizeof(uint32_t));
@@ -260,9 +254,14 @@ int allocWavefront(surf_ctx* c) {
         c->capacity = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(want, 65536), 1u << 22);
     }
     if (c->window == 0) {
-        /* default: 256 frames, radiance ring capped at 16 GiB of the 288 GB HBM */
-        const uint64_t maxFrames = (16ull << 30) / ((uint64_t)c->npx * sizeof(float4));
-        c->window = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(256, maxFrames));
+        /* default: the frames 32 GiB of radiance slots hold (of the 288 GB HBM;
+         * at most a quarter of the free memory), at most 4096 -- past the longest render (C4, 1024 frames), so a
+         * stream never waits for an old frame's long paths to free a slot */
+        uint64_t budget = 32ull << 30;
+        size_t freeB = 0, totalB = 0;
+        if (hipMemGetInfo(&freeB, &totalB) == hipSuccess && freeB > 0) budget = std::min<uint64_t>(budget, freeB / 4);
+        const uint64_t maxFrames = budget / ((uint64_t)c->npx * sizeof(float4));
+        c->window = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(4096, maxFrames));
     }
     const size_t cap = c->capacity;
     int rc;
@@ -273,29 +272,11 @@ int allocWavefront(surf_ctx* c) {
         if ((rc = devAlloc(c, c->wfAllocs, &c->pool[p].key, cap))) return rc;
     }
     if ((rc = devAlloc(c, c->wfAllocs, &c->order, cap))) return rc;
-    if (c->moveRays) {
-        if ((rc = devAlloc(c, c->wfAllocs, &c->srt.o, cap))) return rc;
-        if ((rc = devAlloc(c, c->wfAllocs, &c->srt.d, cap))) return rc;
-        if ((rc = devAlloc(c, c->wfAllocs, &c->srt.T, cap))) return rc;
-    }
     if ((rc = devAlloc(c, c->wfAllocs, &c->binHist, (size_t)kBins * kSortBlocks))) return rc;
     /* grid: 8 workgroups of 256 per CU saturate the 256-CU chip; grid-stride beyond */
     int cus = 256;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, c->device) == hipSuccess && prop.multiProcessorCount > 0) cus = prop.multiProcessorCount;
-    /* long pools: the population of escaped paths is bounded by lpCap (k_shade
-     * reserves it), so each escape queue (one phase's escapes) fits in lpCap too */
-    c->LP.lpCap = c->LP.escCap = (uint32_t)std::min<size_t>(std::max<size_t>(cap / 4, 65536), 1u << 20);
-    for (int q = 0; q < 2; ++q) {
-        if ((rc = devAlloc(c, c->wfAllocs, &c->LP.lp[q].o, c->LP.lpCap))) return rc;
-        if ((rc = devAlloc(c, c->wfAllocs, &c->LP.lp[q].d, c->LP.lpCap))) return rc;
-        if ((rc = devAlloc(c, c->wfAllocs, &c->LP.lp[q].T, c->LP.lpCap))) return rc;
-    }
-    for (int q = 0; q < 4; ++q) {
-        float4** f[6] = {&c->LP.esc[q].o, &c->LP.esc[q].d, &c->LP.esc[q].T, &c->LP.esc[q].so, &c->LP.esc[q].sd, &c->LP.esc[q].sc};
-        for (auto x : f)
-            if ((rc = devAlloc(c, c->wfAllocs, x, c->LP.escCap))) return rc;
-    }
     /* drain stages: survivors of a tail stage, ping-pong */
     c->survCap = (uint32_t)std::min<size_t>(std::max<size_t>(cap / 16, 4096), 1u << 18);
     for (int q = 0; q < 2; ++q) {
@@ -309,11 +290,6 @@ int allocWavefront(surf_ctx* c) {
     if ((rc = devAlloc(c, c->wfAllocs, &c->Q.d, cap))) return rc;
     if ((rc = devAlloc(c, c->wfAllocs, &c->Q.c, cap))) return rc;
     if ((rc = devAlloc(c, c->wfAllocs, &c->Q.key, cap))) return rc;
-    if (c->moveRays) {
-        if ((rc = devAlloc(c, c->wfAllocs, &c->srtQ.o, cap))) return rc;
-        if ((rc = devAlloc(c, c->wfAllocs, &c->srtQ.d, cap))) return rc;
-        if ((rc = devAlloc(c, c->wfAllocs, &c->srtQ.c, cap))) return rc;
-    }
     if ((rc = devAlloc(c, c->wfAllocs, &c->rad, (size_t)c->npx * c->window))) return rc;
     if ((rc = devAlloc(c, c->wfAllocs, &c->ctr, 1))) return rc;
     if ((rc = devAlloc(c, c->wfAllocs, &c->frameDone, (size_t)kStripes * c->window))) return rc;
@@ -332,15 +308,11 @@ int allocWavefront(surf_ctx* c) {
     uint64_t extPerCu = 48, conPerCu = 12;
     if (const char* e = std::getenv("SURF_GRID_EXTEND")) extPerCu = (uint64_t)std::max(1, std::atoi(e));
     if (const char* e = std::getenv("SURF_GRID_CONNECT")) conPerCu = (uint64_t)std::max(1, std::atoi(e));
-    if (const char* e = std::getenv("SURF_EXTEND_BLOCK")) c->extBlock = std::atoi(e) == 128 ? 128u : 256u;
     if (c->extBlock == 128) extPerCu *= 2;                 /* the same threads per CU in half-size workgroups */
     c->gridExtend = (uint32_t)std::min<uint64_t>((cap + c->extBlock - 1) / c->extBlock, (uint64_t)cus * extPerCu);
     c->gridConnect = (uint32_t)std::min<uint64_t>(maxBlocks, (uint64_t)cus * conPerCu);
     c->coopMax = (uint32_t)cus * 4 * SURF_TAIL_WAVES;
-    c->longBlocks = (uint32_t)cus * 4;
-    if (const char* e = std::getenv("SURF_LONG_BLOCKS")) c->longBlocks = std::max(1, std::atoi(e));
-    if (const char* e = std::getenv("SURF_LONG_WAVE")) c->longWave = std::atoi(e) != 0;   /* resident k_tail waves: lanes per wave = paths / this */
-    if (const char* e = std::getenv("SURF_DRAIN_REPLAYS")) c->drainReplays = std::max(1, std::atoi(e));    /* 3 waves per SIMD of the tail kernels (launch bounds) */
+    if (const char* e = std::getenv("SURF_DRAIN_REPLAYS")) c->drainReplays = std::max(1, std::atoi(e));
     c->gridRegen = (uint32_t)std::min<uint64_t>(maxBlocks, (uint64_t)cus * 8);
     c->allocated = true;
     return SURF_OK;
@@ -358,124 +330,57 @@ void launchSort(surf_ctx* c, const uint8_t* key, int par, int which) {
                        (const uint32_t*)c->binHist, c->order);
 }
 
-/* The same sort, moving the records: pool (which 0) -> c->srt, shadow queue (which 1) -> c->srtQ. */
-void launchMove(surf_ctx* c, int par, int which) {
-    const uint8_t* key = which ? c->Q.key : c->pool[par].key;
-    hipLaunchKernelGGL(k_bincount, dim3(kSortBlocks), dim3(kBlock), 0, c->stream, key, (const Counters*)c->ctr, par, which,
-                       c->binHist);
-    hipLaunchKernelGGL(k_binscan, dim3(1), dim3(1024), 0, c->stream, c->binHist, kBins * kSortBlocks);
-    const Rec3 src = which ? Rec3{c->Q.o, c->Q.d, c->Q.c} : Rec3{c->pool[par].o, c->pool[par].d, c->pool[par].T};
-    const Rec3w dst = which ? Rec3w{c->srtQ.o, c->srtQ.d, c->srtQ.c} : Rec3w{c->srt.o, c->srt.d, c->srt.T};
-    hipLaunchKernelGGL(k_binmove, dim3(kSortBlocks), dim3(kBlock), 0, c->stream, key, (const Counters*)c->ctr, par, which,
-                       (const uint32_t*)c->binHist, src, dst);
-}
-
-/* k_long for phase ph: lp[ph & 1] + esc[(ph - 1) % 4] -> lp[(ph + 1) & 1]. */
-bool waveEligible(const surf_ctx* c);
-void launchLong(surf_ctx* c, int ph, hipStream_t st) {
-    const uint32_t in = (uint32_t)ph & 1u, eq = ((uint32_t)ph + 3u) & 3u;
-    const size_t lds = traversalLds(c, kBlock);
-    if (c->longWave && c->coopEligible && waveEligible(c)) {
-        /* one path per wave: the long paths' segment latency (surf_set_long_paths) */
-        hipLaunchKernelGGL(k_long_wave, dim3(c->longBlocks), dim3(64),
-                           traversalLds(c, 64) - (size_t)stackWords(c, 64) * sizeof(uint32_t) + (size_t)recStackWords(c) * sizeof(float),
-                           st, c->S, c->LP, c->rad, c->frameDone, c->npx, c->window, c->ctr, in, eq, recStackWords(c));
-    } else if (c->ldsTables)
-        hipLaunchKernelGGL(k_long<true>, dim3(c->gridWork), dim3(kBlock), lds, st, c->S, c->LP, c->rad, c->frameDone, c->npx,
-                           c->window, c->ctr, in, eq, stackWords(c, kBlock));
-    else
-        hipLaunchKernelGGL(k_long<false>, dim3(c->gridWork), dim3(kBlock), lds, st, c->S, c->LP, c->rad, c->frameDone, c->npx,
-                           c->window, c->ctr, in, eq, stackWords(c, kBlock));
-}
-
-/* One wavefront phase (ph = 0..kPhasesPerGraph-1): extend -> shade -> connect
- * -> regen, plus -- when long paths escape -- that phase's k_long step.
- * Captured (graph): k_long(ph + 1) runs on stream2 after shade(ph), beside the
- * rest of the chain; shade(ph) waits for k_long(ph - 3), the last reader of
- * the escape queue it refills.  Direct launches (profiling): k_long(ph) runs
- * first, in stream order.  With ev != null, an event is recorded before each
- * wavefront kernel and after the last. */
-void launchPhase(surf_ctx* c, int ph, hipEvent_t* ev, bool capture) {
+/* One wavefront phase (ph = 0..kPhasesPerGraph-1): sort -> extend -> shade
+ * -> sort -> connect -> regen.  With ev != null, ev[0..5] are recorded before
+ * the pool sort, k_extend, k_shade, the shadow sort, k_connect and k_regen
+ * (the phase ends at the next phase's ev[0]). */
+void launchPhase(surf_ctx* c, int ph, hipEvent_t* ev) {
     const int par = ph & 1;
-    const size_t lds = traversalLds(c, kBlock);
     const uint32_t sw = stackWords(c, kBlock);
-    const bool lng = c->longThresh != 0;
-    if (lng && !capture) launchLong(c, ph, c->stream);
     if (ev) (void)hipEventRecord(ev[0], c->stream);
-    const bool persistent = c->persistent && c->ldsTables && c->S.tlasLeafCount > 0;
     const uint32_t* order = nullptr;
-    const bool sorted = c->sortRays && !persistent, move = sorted && c->moveRays;
-    Pool cur = c->pool[par];                     /* the pool k_extend / k_shade read */
-    if (move) {
-        launchMove(c, par, 0);
-        cur = c->srt;
-    } else if (sorted) {
+    if (c->sortRays) {
         launchSort(c, c->pool[par].key, par, 0);
         order = c->order;
     }
-    if (persistent)
-        hipLaunchKernelGGL(k_extend_p<true>, dim3(c->gridWork), dim3(kBlock), lds, c->stream, c->S, cur, c->hitTUV,
-                           c->hitInst, (const Counters*)c->ctr, par, sw);
-    else if (c->ldsTables)
+    if (ev) (void)hipEventRecord(ev[1], c->stream);
+    const Pool cur = c->pool[par];                 /* the pool k_extend / k_shade read */
+    if (c->ldsTables)
         hipLaunchKernelGGL(k_extend<true>, dim3(c->gridExtend), dim3(c->extBlock), traversalLds(c, c->extBlock), c->stream, c->S,
                            cur, c->hitTUV, c->hitInst, (const Counters*)c->ctr, par, stackWords(c, c->extBlock), order);
     else
         hipLaunchKernelGGL(k_extend<false>, dim3(c->gridExtend), dim3(c->extBlock), traversalLds(c, c->extBlock), c->stream, c->S,
                            cur, c->hitTUV, c->hitInst, (const Counters*)c->ctr, par, stackWords(c, c->extBlock), order);
-    if (ev) (void)hipEventRecord(ev[1], c->stream);
-    if (lng && capture && ph >= 3) (void)hipStreamWaitEvent(c->stream, c->evLong[ph - 3], 0);
-    const uint32_t escQ = (uint32_t)ph & 3u;
+    if (ev) (void)hipEventRecord(ev[2], c->stream);
     if (c->ldsTables)
         hipLaunchKernelGGL(k_shade<true>, dim3(c->gridWork), dim3(kBlock), 0, c->stream, c->S, cur, c->pool[par ^ 1],
-                           c->hitTUV, (const uint32_t*)c->hitInst, c->Q, c->rad, c->frameDone, c->npx, c->window, c->ctr, par,
-                           c->LP, escQ, order);
+                           c->hitTUV, (const uint32_t*)c->hitInst, c->Q, c->rad, c->frameDone, c->npx, c->window, c->ctr, par, order);
     else
         hipLaunchKernelGGL(k_shade<false>, dim3(c->gridWork), dim3(kBlock), 0, c->stream, c->S, cur, c->pool[par ^ 1],
-                           c->hitTUV, (const uint32_t*)c->hitInst, c->Q, c->rad, c->frameDone, c->npx, c->window, c->ctr, par,
-                           c->LP, escQ, order);
-    if (lng && capture && ph + 1 < kPhasesPerGraph) {
-        (void)hipEventRecord(c->evShade[ph], c->stream);
-        (void)hipStreamWaitEvent(c->stream2, c->evShade[ph], 0);
-        launchLong(c, ph + 1, c->stream2);
-        (void)hipEventRecord(c->evLong[ph + 1], c->stream2);
-    }
-    if (ev) (void)hipEventRecord(ev[2], c->stream);
+                           c->hitTUV, (const uint32_t*)c->hitInst, c->Q, c->rad, c->frameDone, c->npx, c->window, c->ctr, par, order);
+    if (ev) (void)hipEventRecord(ev[3], c->stream);
     /* shadow rays toward the same light together (the pool order no longer needed: reuse it) */
-    ShadowQ q = c->Q;
     const uint32_t* qorder = nullptr;
-    if (move) {
-        launchMove(c, par, 1);
-        q = c->srtQ;
-    } else if (sorted) {
+    if (c->sortRays) {
         launchSort(c, c->Q.key, par, 1);
         qorder = c->order;
     }
+    if (ev) (void)hipEventRecord(ev[4], c->stream);
     if (c->ldsTables && !c->connectGlobal)
-        hipLaunchKernelGGL(k_connect<true>, dim3(c->gridConnect), dim3(kBlock), lds, c->stream, c->S, q, c->rad, c->ctr, par, sw,
-                           qorder);
-    else
-        hipLaunchKernelGGL(k_connect<false>, dim3(c->gridConnect), dim3(kBlock), lds, c->stream, c->S, q, c->rad, c->ctr, par, sw,
-                           qorder);
-    if (ev) (void)hipEventRecord(ev[3], c->stream);
+        hipLaunchKernelGGL(k_connect<true>, dim3(c->gridConnect), dim3(kBlock), traversalLds(c, kBlock), c->stream, c->S, c->Q,
+                           c->rad, c->ctr, par, sw, qorder);
+    else   /* global tables: LDS holds only the traversal stack */
+        hipLaunchKernelGGL(k_connect<false>, dim3(c->gridConnect), dim3(kBlock), (size_t)sw * sizeof(uint32_t), c->stream, c->S,
+                           c->Q, c->rad, c->ctr, par, sw, qorder);
+    if (ev) (void)hipEventRecord(ev[5], c->stream);
     hipLaunchKernelGGL(k_regen, dim3(c->gridRegen), dim3(kBlock), 0, c->stream, c->cam, c->pool[par ^ 1], c->rad, c->ctr, par,
                        c->capacity, geom(c));
-    if (ev) (void)hipEventRecord(ev[4], c->stream);
 }
 
 int buildGraph(surf_ctx* c) {
     if (c->graphExec) return SURF_OK;
-    const bool lng = c->longThresh != 0;
     SURF_CHECK(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-    if (lng) {
-        /* fork: the k_long chain on stream2, k_long(0) first (it consumes the
-         * previous replay's last escapes; replays are serialized) */
-        (void)hipEventRecord(c->evFork, c->stream);
-        (void)hipStreamWaitEvent(c->stream2, c->evFork, 0);
-        launchLong(c, 0, c->stream2);
-        (void)hipEventRecord(c->evLong[0], c->stream2);
-    }
-    for (int ph = 0; ph < kPhasesPerGraph; ++ph) launchPhase(c, ph, nullptr, true);
-    if (lng) (void)hipStreamWaitEvent(c->stream, c->evLong[kPhasesPerGraph - 1], 0);   /* join */
+    for (int ph = 0; ph < kPhasesPerGraph; ++ph) launchPhase(c, ph, nullptr);
     hipError_t e = hipStreamEndCapture(c->stream, &c->graph);
     if (e != hipSuccess) return fail(c, SURF_ERR_HIP, std::string("graph capture: ") + hipGetErrorString(e));
     SURF_CHECK(c, hipGraphInstantiate(&c->graphExec, c->graph, nullptr, nullptr, 0));
@@ -484,14 +389,11 @@ int buildGraph(surf_ctx* c) {
 
 /* ---- sample stream ------------------------------------------------------ */
 int startStream(surf_ctx* c, uint64_t baseFrame, uint32_t maxSeg) {
-    SURF_CHECK(c, hipStreamSynchronize(c->stream2));     /* no worker of an older stream still runs */
     Counters h{};
     h.maxSeg = maxSeg;
     h.zeroCutoff = c->zeroCutoff ? 1u : 0u;
     h.baseFrame = baseFrame;
     h.survCap = c->survCap;
-    h.longThresh = c->longThresh;
-    h.longBudget = c->longBudget;
     *c->hctr = h;
     SURF_CHECK(c, hipMemcpyAsync(c->ctr, c->hctr, sizeof(Counters), hipMemcpyHostToDevice, c->stream));
     SURF_CHECK(c, hipMemsetAsync(c->frameDone, 0, (size_t)kStripes * c->window * sizeof(uint32_t), c->stream));
@@ -536,7 +438,18 @@ void streamEvents(const Counters& h, unsigned long long out[kEvents]) {
  * order, every leading frame whose samples have all finished. */
 int syncAndAccumulate(surf_ctx* c) {
     SURF_CHECK(c, hipMemcpyAsync(c->hctr, c->ctr, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
-    SURF_CHECK(c, hipMemcpyAsync(c->hFrameDone, c->frameDone, (size_t)kStripes * c->window * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+    /* completion counts of the open frames only ([accFrames, targetFrames),
+     * at most a window): a strided copy of their slots in each stripe row */
+    const uint64_t open = std::min<uint64_t>(c->targetFrames - std::min(c->accFrames, c->targetFrames), c->window);
+    const uint32_t s0 = (uint32_t)(c->accFrames % c->window);
+    const uint32_t n0 = (uint32_t)std::min<uint64_t>(open, c->window - s0);
+    const size_t pitch = (size_t)c->window * sizeof(uint32_t);
+    if (n0)
+        SURF_CHECK(c, hipMemcpy2DAsync(c->hFrameDone + s0, pitch, c->frameDone + s0, pitch, n0 * sizeof(uint32_t), kStripes,
+                                       hipMemcpyDeviceToHost, c->stream));
+    if (open > n0)
+        SURF_CHECK(c, hipMemcpy2DAsync(c->hFrameDone, pitch, c->frameDone, pitch, (open - n0) * sizeof(uint32_t), kStripes,
+                                       hipMemcpyDeviceToHost, c->stream));
     SURF_CHECK(c, hipStreamSynchronize(c->stream));
     /* a frame is complete when all its samples were issued and all finished; a
      * slot is reused only after its frame is accumulated, so frames beyond the
@@ -558,13 +471,16 @@ int syncAndAccumulate(surf_ctx* c) {
  * direct launches with per-kernel events when profiling). */
 int advance(surf_ctx* c) {
     if (c->profiling) {
-        for (int ph = 0; ph < kPhasesPerGraph; ++ph) launchPhase(c, ph, &c->pev[4 * ph], false);
+        for (int ph = 0; ph < kPhasesPerGraph; ++ph) launchPhase(c, ph, &c->pev[kPhaseEvents * ph]);
+        SURF_CHECK(c, hipEventRecord(c->pev[kPhaseEvents * kPhasesPerGraph], c->stream));
         SURF_CHECK(c, hipGetLastError());
-        SURF_CHECK(c, hipEventSynchronize(c->pev[4 * (kPhasesPerGraph - 1) + 4]));
+        SURF_CHECK(c, hipEventSynchronize(c->pev[kPhaseEvents * kPhasesPerGraph]));
         for (int ph = 0; ph < kPhasesPerGraph; ++ph) {
-            float t[4];
-            for (int k = 0; k < 4; ++k) (void)hipEventElapsedTime(&t[k], c->pev[4 * ph + k], c->pev[4 * ph + k + 1]);
-            c->stats.ms_extend += t[0]; c->stats.ms_shade += t[1]; c->stats.ms_connect += t[2]; c->stats.ms_regen += t[3];
+            float t[kPhaseEvents];
+            for (int k = 0; k < kPhaseEvents; ++k)
+                (void)hipEventElapsedTime(&t[k], c->pev[kPhaseEvents * ph + k], c->pev[kPhaseEvents * ph + k + 1]);
+            c->stats.ms_sort += t[0] + t[3];
+            c->stats.ms_extend += t[1]; c->stats.ms_shade += t[2]; c->stats.ms_connect += t[4]; c->stats.ms_regen += t[5];
             c->stats.launches_extend++;
         }
     } else {
@@ -596,23 +512,18 @@ void launchTail(surf_ctx* c, Pool in, uint32_t n, uint32_t lpw, uint32_t firstCo
  * reference's Russian-roulette survivors that run for thousands of segments),
  * the cooperative tail runs each on a whole wave, which cuts the latency of a
  * segment -- the quantity the last paths of a drain are bound by. */
-/* Cooperative drain with the lanes-as-planes wave traversal (traceWave):
- * single-leaf TLAS, stack in one VGPR's 64 lanes (SURF_COOP_WAVE=0: the
- * instance-parallel variant instead, for comparison). */
-bool waveEligible(const surf_ctx* c) {
-    static const bool off = [] { const char* e = std::getenv("SURF_COOP_WAVE"); return e && e[0] == '0'; }();
-    return !off && c->coopEligible && c->stackDepth <= 64;
-}
+/* The cooperative drain uses the lanes-as-planes wave traversal (traceWave):
+ * single-leaf TLAS of <= 64 instances, stack of node records in 64 lanes. */
+bool waveEligible(const surf_ctx* c) { return c->coopEligible && c->stackDepth <= 64; }
 
-/* longPool: finish the long pool lp[0] (the wavefront is empty and no
- * escape is pending; their next extension ray is not counted yet), else
- * pool 0 (regen counted each path's next extension ray). */
-int runTail(surf_ctx* c, bool longPool) {
-    const uint32_t n = longPool ? std::min(c->hctr->lpN[0], c->LP.lpCap) : c->hctr->nIn[0];
+/* Regen counted each pool-0 path's next extension ray (firstCounted). */
+int runTail(surf_ctx* c) {
+    const uint32_t n = c->hctr->nIn[0];
     if (n == 0) return SURF_OK;
     if (c->profiling) SURF_CHECK(c, hipEventRecord(c->pev[0], c->stream));
-    Pool in = longPool ? c->LP.lp[0] : c->pool[0];
-    uint32_t cnt = n, firstCounted = longPool ? 0u : 1u;
+    Pool in = c->pool[0];
+    uint32_t cnt = n, firstCounted = 1u;
+    c->tailFirstRays += n;
     int buf = 0;
     static const bool dbg = std::getenv("SURF_DEBUG_TAIL") != nullptr;   /* diagnostics: per-stage log on stderr */
     auto t0 = std::chrono::steady_clock::now();
@@ -622,22 +533,9 @@ int runTail(surf_ctx* c, bool longPool) {
             const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
             std::fprintf(stderr, "[surf tail] stage %d: %u paths at %.2f ms\n", stage, cnt, ms);
         }
-        if (c->coopEligible && cnt <= c->coopAll) {
-            /* the wave traversal keeps no stack in LDS: only the trace tables */
-            /* tables from global memory (wave-uniform reads): the LDS copies would
-             * cap the one-wave blocks at ~2 waves per SIMD (SURF_COOP_LDS=1: A/B) */
-            static const bool coopLds = std::getenv("SURF_COOP_LDS") && std::atoi(std::getenv("SURF_COOP_LDS")) != 0;
-            if (waveEligible(c) && !coopLds)
-                hipLaunchKernelGGL((k_tail_coop<false, true>), dim3(cnt), dim3(64),
-                                   traversalLds(c, 64) - (size_t)stackWords(c, 64) * sizeof(uint32_t) + (size_t)recStackWords(c) * sizeof(float),
-                                   c->stream, c->S, in, cnt, c->rad, c->frameDone, c->npx, c->window, c->ctr, recStackWords(c) / 2u, firstCounted);
-            else if (waveEligible(c))
-                hipLaunchKernelGGL((k_tail_coop<true, true>), dim3(cnt), dim3(64),
-                                   traversalLds(c, 64) - (size_t)stackWords(c, 64) * sizeof(uint32_t) + (size_t)recStackWords(c) * sizeof(float),
-                                   c->stream, c->S, in, cnt, c->rad, c->frameDone, c->npx, c->window, c->ctr, recStackWords(c) / 2u, firstCounted);
-            else
-                hipLaunchKernelGGL((k_tail_coop<true, false>), dim3(cnt), dim3(64), traversalLds(c, 64) + (size_t)stackWords(c, 64) * sizeof(float),
-                                   c->stream, c->S, in, cnt, c->rad, c->frameDone, c->npx, c->window, c->ctr, stackWords(c, 64), firstCounted);
+        if (waveEligible(c) && cnt <= c->coopAll) {
+            hipLaunchKernelGGL(k_tail_coop, dim3(cnt), dim3(64), coopLds(c), c->stream, c->S, in, cnt, c->rad, c->frameDone,
+                               c->npx, c->window, c->ctr, recStackWords(c), firstCounted);
             SURF_CHECK(c, hipGetLastError());
             c->stats.tail_survivors += cnt;
             break;
@@ -679,17 +577,9 @@ int runTail(surf_ctx* c, bool longPool) {
                      h[0] / ns, h[1] / ns, h[2] / ns, h[3] / ns, h[4] / ns, h[5] / ns, h[6] / ns, h[7] / ns);
     }
 #endif
-    if (longPool) {
-        /* every escaped path has finished */
-        c->hctr->lpN[0] = 0;
-        c->hctr->longPop = 0;
-        SURF_CHECK(c, hipMemcpyAsync(&c->ctr->lpN[0], &c->hctr->lpN[0], sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
-        SURF_CHECK(c, hipMemcpyAsync(&c->ctr->longPop, &c->hctr->longPop, sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
-    } else {
-        /* pool 0 is now empty: the next phase starts from regen's refill */
-        c->hctr->nIn[0] = 0;
-        SURF_CHECK(c, hipMemcpyAsync(&c->ctr->nIn[0], &c->hctr->nIn[0], sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
-    }
+    /* pool 0 is now empty: the next phase starts from regen's refill */
+    c->hctr->nIn[0] = 0;
+    SURF_CHECK(c, hipMemcpyAsync(&c->ctr->nIn[0], &c->hctr->nIn[0], sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
     SURF_CHECK(c, hipStreamSynchronize(c->stream));
     return SURF_OK;
 }
@@ -704,12 +594,8 @@ int pump(surf_ctx* c, bool drain) {
     const uint64_t target = c->targetFrames * (uint64_t)c->npx;
     for (;;) {
         const uint64_t issued = c->hctr->issued[0];
-        /* in flight at a replay boundary: the wavefront pool, the long pool
-         * k_long(0) reads next, and the escapes of the last phase */
-        const uint32_t nW = c->hctr->nIn[0];
-        const uint32_t nL = c->longThresh ? std::min(c->hctr->lpN[0], c->LP.lpCap) : 0u;
-        const uint32_t nE = c->longThresh ? std::min(c->hctr->escN[3], c->LP.escCap) : 0u;
-        const uint64_t inflight = (uint64_t)nW + nL + nE;
+        /* in flight at a replay boundary: the pool the next phase extends */
+        const uint32_t inflight = c->hctr->nIn[0];
         if (!drain && issued >= target) return SURF_OK;
         if (drain && c->accFrames >= c->targetFrames) return SURF_OK;
         const bool starved = issued >= c->pushedLimit;     /* nothing more may be issued right now */
@@ -717,16 +603,13 @@ int pump(surf_ctx* c, bool drain) {
         static const bool dbgDrain = std::getenv("SURF_DEBUG_DRAIN") != nullptr;   /* diagnostics: drain timeline */
         if (dbgDrain && starved) {
             static auto tS = std::chrono::steady_clock::now();
-            std::fprintf(stderr, "[surf drain] iteration %llu: %u wavefront + %u long + %u escaped, %llu/%llu frames at %.3f ms\n",
-                         (unsigned long long)c->stats.iterations, nW, nL, nE, (unsigned long long)c->accFrames,
+            std::fprintf(stderr, "[surf drain] iteration %llu: %u paths in flight, %llu/%llu frames at %.3f ms\n",
+                         (unsigned long long)c->stats.iterations, inflight, (unsigned long long)c->accFrames,
                          (unsigned long long)c->targetFrames,
                          std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tS).count());
         }
-        if (starved && inflight > 0 && nW == 0 && nE == 0) {
-            /* only long paths left: the staged tail finishes them */
-            if ((rc = runTail(c, true))) return rc;
-        } else if (starved && nL == 0 && nE == 0 && nW > 0 && nW <= tailThreshold(c)) {
-            if ((rc = runTail(c, false))) return rc;
+        if (starved && inflight > 0 && inflight <= tailThreshold(c)) {
+            if ((rc = runTail(c))) return rc;
         } else if (starved && inflight == 0) {
             /* every issued sample finished: accumulating re-opens the window */
         } else {
@@ -764,7 +647,6 @@ int ensureDrained(surf_ctx* c) {
 int endStream(surf_ctx* c) {
     int rc = ensureDrained(c);
     if (rc) return rc;
-    if (c->stream2) SURF_CHECK(c, hipStreamSynchronize(c->stream2));
     if (c->streamActive) {
         unsigned long long e[kEvents];
         streamEvents(*c->hctr, e);
@@ -799,23 +681,23 @@ int createCtx(int dev, uint32_t w, uint32_t h, std::vector<uint32_t> rows, surf_
     if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return fail(nullptr, SURF_ERR_NO_DEVICE, "hipGetDeviceProperties failed");
     if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos)
         return fail(nullptr, SURF_ERR_NO_DEVICE, std::string("device is ") + prop.gcnArchName + ", this build targets gfx950");
+    /* tuning knobs (A/B runs): read once per context, invalid values refused */
+    uint32_t extBlock = 128;
+    if (const char* e = std::getenv("SURF_EXTEND_BLOCK")) {
+        const int b = std::atoi(e);
+        if (b != 128 && b != 256) return fail(nullptr, SURF_ERR_INVALID, std::string("SURF_EXTEND_BLOCK must be 128 or 256, not ") + e);
+        extBlock = (uint32_t)b;
+    }
     auto* c = new surf_ctx();
     c->device = dev;
+    c->extBlock = extBlock;
     if (const char* e = std::getenv("SURF_SORT")) c->sortRays = e[0] != '0';
-    if (const char* e = std::getenv("SURF_SORT_MOVE")) c->moveRays = e[0] != '0';
     if (const char* e = std::getenv("SURF_CONNECT_GLOBAL")) c->connectGlobal = e[0] != '0';
     c->width = w;
     c->height = h;
     c->rows = std::move(rows);
     c->npx = (uint32_t)(w * c->rows.size());
-    bool evOk = true;
-    if (hipSetDevice(dev) == hipSuccess) {
-        evOk = hipEventCreateWithFlags(&c->evFork, hipEventDisableTiming) == hipSuccess;
-        for (auto& e : c->evShade) evOk = evOk && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
-        for (auto& e : c->evLong) evOk = evOk && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
-    }
-    if (!evOk || hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
+    if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
         delete c;
         return fail(nullptr, SURF_ERR_HIP, "stream/event creation failed");
@@ -859,8 +741,6 @@ int surf_create_sharded(int dev, uint32_t w, uint32_t h, uint32_t shard, uint32_
 void surf_destroy(surf_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    /* long-path workers end within their lifetime; nothing may be freed under them */
-    if (c->stream2) (void)hipStreamSynchronize(c->stream2);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     destroyGraph(c);
     freeList(c->sceneAllocs);
@@ -872,12 +752,7 @@ void surf_destroy(surf_ctx* c) {
     if (c->dRows) (void)hipFree(c->dRows);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
-    if (c->stream2) (void)hipStreamSynchronize(c->stream2);
     if (c->stream) (void)hipStreamDestroy(c->stream);
-    if (c->stream2) (void)hipStreamDestroy(c->stream2);
-    if (c->evFork) (void)hipEventDestroy(c->evFork);
-    for (auto& e : c->evShade) if (e) (void)hipEventDestroy(e);
-    for (auto& e : c->evLong) if (e) (void)hipEventDestroy(e);
     delete c;
 }
 
@@ -943,33 +818,11 @@ int surf_set_tail_coop(surf_ctx* c, uint32_t max_paths) {
     return SURF_OK;
 }
 
-int surf_set_long_paths(surf_ctx* c, uint32_t escape_segments, uint32_t segments_per_phase) {
-    if (!c) return fail(nullptr, SURF_ERR_INVALID, "ctx is NULL");
-    if (escape_segments != 0 && (segments_per_phase == 0 || segments_per_phase > 4096))
-        return fail(c, SURF_ERR_INVALID, "segments_per_phase must be 1..4096");
-    SURF_CHECK(c, hipSetDevice(c->device));
-    const int rc = endStream(c);
-    if (rc) return rc;
-    c->longThresh = escape_segments;
-    if (escape_segments) c->longBudget = segments_per_phase;
-    destroyGraph(c);                  /* the graph's shape (the k_long chain) changes */
-    return SURF_OK;
-}
-int surf_set_persistent(surf_ctx* c, int enabled) {
-    if (!c) return fail(nullptr, SURF_ERR_INVALID, "ctx is NULL");
-    SURF_CHECK(c, hipSetDevice(c->device));
-    const int rc = endStream(c);
-    if (rc) return rc;
-    c->persistent = enabled != 0;
-    destroyGraph(c);
-    return SURF_OK;
-}
-
 int surf_set_trace_mode(surf_ctx* c, int mode) {
     if (!c) return fail(nullptr, SURF_ERR_INVALID, "ctx is NULL");
-    if (mode < 0 || mode > 2) return fail(c, SURF_ERR_INVALID, "trace mode must be 0, 1 or 2");
-    if (mode >= 1 && !c->coopEligible) return fail(c, SURF_ERR_INVALID, "cooperative traversal needs a single-leaf TLAS of <= 64 instances");
-    if (mode == 2 && c->stackDepth > 64) return fail(c, SURF_ERR_INVALID, "wave traversal keeps its stack in 64 lanes: BVH too deep");
+    if (mode < 0 || mode > 1) return fail(c, SURF_ERR_INVALID, "trace mode must be 0 or 1");
+    if (mode == 1 && !waveEligible(c))
+        return fail(c, SURF_ERR_INVALID, "one-ray-per-wave traversal needs a single-leaf TLAS of <= 64 instances and a BVH stack <= 64");
     c->traceMode = mode;
     return SURF_OK;
 }
@@ -1345,6 +1198,7 @@ int surf_clear_accumulator(surf_ctx* c) {
     std::memset(&c->stats, 0, sizeof c->stats);
     std::memset(c->evBase, 0, sizeof c->evBase);
     c->segMaxBase = 0;
+    c->tailFirstRays = 0;
     return SURF_OK;
 }
 
@@ -1411,7 +1265,7 @@ int surf_get_stats(surf_ctx* c, surf_stats* out) {
     for (int k = 0; k < kEvents; ++k) ev[k] = c->evBase[k] + cur[k];
     s.n_ext = ev[0]; s.n_hit = ev[1]; s.n_cont = ev[2]; s.n_shadow = ev[3]; s.n_acc = ev[4]; s.n_unocc = ev[5];
     s.tail_paths = ev[6];
-    s.long_paths = ev[8];
+    s.n_ext_wavefront = ev[8] - c->tailFirstRays;
     s.max_segments = std::max(c->segMaxBase, (c->streamActive && c->hctr) ? c->hctr->segMax : 0u);
     s.stack_depth = c->stackDepth;
     s.pool_capacity = c->capacity;
@@ -1449,6 +1303,7 @@ int surf_trace_closest(surf_ctx* c, uint32_t n, const float* o, const float* d, 
     if (!c || (n && (!o || !d || !ot || !ou || !ov || !oi || !op))) return SURF_ERR_INVALID;
     if (!c->hasScene) return fail(c, SURF_ERR_NO_SCENE, "no scene uploaded");
     if (n == 0) return SURF_OK;
+    if (c->traceMode == 1 && !waveEligible(c)) return fail(c, SURF_ERR_INVALID, "scene no longer fits the one-ray-per-wave traversal");
     SURF_CHECK(c, hipSetDevice(c->device));
     std::vector<void*> tmp;
     float *dO, *dD; float4* dT; uint2* dI;
@@ -1458,11 +1313,8 @@ int surf_trace_closest(surf_ctx* c, uint32_t n, const float* o, const float* d, 
     (void)hipMemcpyAsync(dO, o, 12 * (size_t)n, hipMemcpyHostToDevice, c->stream);
     (void)hipMemcpyAsync(dD, d, 12 * (size_t)n, hipMemcpyHostToDevice, c->stream);
     if (c->traceMode == 1)
-        hipLaunchKernelGGL(k_trace_closest_coop<false>, dim3(n), dim3(64), traversalLds(c, 64) + (size_t)stackWords(c, 64) * sizeof(float),
-                           c->stream, c->S, (const float*)dO, (const float*)dD, n, dT, dI, stackWords(c, 64));
-    else if (c->traceMode == 2)
-        hipLaunchKernelGGL(k_trace_closest_coop<true>, dim3(n), dim3(64), traversalLds(c, 64) + (size_t)stackWords(c, 64) * sizeof(float),
-                           c->stream, c->S, (const float*)dO, (const float*)dD, n, dT, dI, stackWords(c, 64));
+        hipLaunchKernelGGL(k_trace_closest_coop, dim3(n), dim3(64), coopLds(c), c->stream, c->S, (const float*)dO, (const float*)dD,
+                           n, dT, dI, recStackWords(c));
     else if (c->ldsTables)
         hipLaunchKernelGGL(k_trace_closest<true>, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), traversalLds(c, kBlock), c->stream,
                            c->S, (const float*)dO, (const float*)dD, n, dT, dI, stackWords(c, kBlock));
@@ -1484,6 +1336,7 @@ int surf_trace_any(surf_ctx* c, uint32_t n, const float* o, const float* d, cons
     if (!c || (n && (!o || !d || !tm || !occ))) return SURF_ERR_INVALID;
     if (!c->hasScene) return fail(c, SURF_ERR_NO_SCENE, "no scene uploaded");
     if (n == 0) return SURF_OK;
+    if (c->traceMode == 1 && !waveEligible(c)) return fail(c, SURF_ERR_INVALID, "scene no longer fits the one-ray-per-wave traversal");
     SURF_CHECK(c, hipSetDevice(c->device));
     std::vector<void*> tmp;
     float *dO, *dD, *dM; uint8_t* dR;
@@ -1493,10 +1346,9 @@ int surf_trace_any(surf_ctx* c, uint32_t n, const float* o, const float* d, cons
     (void)hipMemcpyAsync(dO, o, 12 * (size_t)n, hipMemcpyHostToDevice, c->stream);
     (void)hipMemcpyAsync(dD, d, 12 * (size_t)n, hipMemcpyHostToDevice, c->stream);
     (void)hipMemcpyAsync(dM, tm, 4 * (size_t)n, hipMemcpyHostToDevice, c->stream);
-    if (c->traceMode == 1 || c->traceMode == 2)
-        hipLaunchKernelGGL(c->traceMode == 2 ? k_trace_any_coop<true> : k_trace_any_coop<false>, dim3(n), dim3(64),
-                           traversalLds(c, 64), c->stream, c->S, (const float*)dO,
-                           (const float*)dD, (const float*)dM, n, dR, stackWords(c, 64));
+    if (c->traceMode == 1)
+        hipLaunchKernelGGL(k_trace_any_coop, dim3(n), dim3(64), coopLds(c), c->stream, c->S, (const float*)dO, (const float*)dD,
+                           (const float*)dM, n, dR, recStackWords(c));
     else if (c->ldsTables)
         hipLaunchKernelGGL(k_trace_any<true>, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), traversalLds(c, kBlock), c->stream,
                            c->S, (const float*)dO, (const float*)dD, (const float*)dM, n, dR, stackWords(c, kBlock));

@@ -6,9 +6,11 @@
  * application builds them, with RenderContext holding a HIP device instead of
  * a Vulkan context and no UIManager.
  *
- * usage: render_indoor ASSETS_DIR WIDTH HEIGHT FRAMES OUT.(ppm|png)
- * Prints the reference's per-frame line (ms, Mrays/s, samples, Lumen) and
- * writes the image as the reference presents it: the RGBA8 finalize image
+ * usage: render_indoor ASSETS_DIR WIDTH HEIGHT FRAMES OUT.(ppm|png) [--lumen]
+ * Prints the reference's per-frame line (ms, Mrays/s, samples, Lumen; the
+ * energy only with --lumen, the reference's WF_LUMEN_OUTPUT, which drains the
+ * stream every frame), then one JSON line with the loop's wall time including
+ * the final drain, and writes the image as the reference presents it: the RGBA8 finalize image
  * (wavefront_finalize.comp) through fs_quad.frag's sqrt gamma, 8 bits per
  * channel (displayRGBA8), as PPM or PNG by extension.
  */
@@ -70,19 +72,25 @@ int main(int argc, char** argv) {
         GPUScene scene(&context, background, instances);
 
         RendererConfig config;            /* samplesPerFrame 1 (ui_manager.h:26), unbounded + RR */
+        config.lumenOutput = argc > 6 && std::string(argv[6]) == "--lumen";
         WaveFrontRenderer renderer(&context, nullptr, config, FramebufferSize{W, H}, worldCam, scene);
 
+        const auto tLoop = std::chrono::steady_clock::now();
         for (U32 f = 0; f < frames; ++f) {
             const auto t0 = std::chrono::steady_clock::now();
-            renderer.render(0.0f);        /* frameInfo() reads the accumulator: the frame is complete */
-            const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+            renderer.render(0.0f);        /* returns once the frame's samples are issued (lumenOutput: frameInfo() drains) */
             const FrameInstrumentationData& info = renderer.frameInfo();
+            const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
             /* main.cpp:431-442 */
             std::printf("%08.2fms (%05.1f fps) - %08.2fMrays/s - %05u samples (%u spp) - %010.2f Lumen\n", ms, 1000.0 / ms,
                         (double)W * H * renderer.config().samplesPerFrame / ms / 1000.0, info.totalSamples,
                         renderer.config().samplesPerFrame, info.energy);
         }
 
+        renderer.synchronize();           /* every frame accumulated */
+        const double loopMs = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tLoop).count();
+        std::printf("{\"frames\": %u, \"width\": %u, \"height\": %u, \"loop_ms\": %.3f, \"mrays_per_s\": %.3f, \"lumen_output\": %s}\n",
+                    frames, W, H, loopMs, (double)W * H * frames / loopMs / 1000.0, config.lumenOutput ? "true" : "false");
         const std::vector<U32> img = renderer.displayRGBA8();
         const std::string path = argv[5];
         const bool png = path.size() > 4 && path.compare(path.size() - 4, 4, ".png") == 0;

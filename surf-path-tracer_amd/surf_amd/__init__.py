@@ -60,11 +60,10 @@ class Stats(C.Structure):
         ("n_shadow", C.c_uint64), ("n_acc", C.c_uint64), ("n_unocc", C.c_uint64), ("iterations", C.c_uint64),
         ("tail_paths", C.c_uint64),
         ("ms_total", C.c_double), ("ms_extend", C.c_double), ("ms_shade", C.c_double), ("ms_connect", C.c_double),
-        ("ms_regen", C.c_double), ("ms_tail", C.c_double), ("ms_accum", C.c_double),
-        ("launches_extend", C.c_uint64),
+        ("ms_regen", C.c_double), ("ms_tail", C.c_double), ("ms_accum", C.c_double), ("ms_sort", C.c_double),
+        ("launches_extend", C.c_uint64), ("n_ext_wavefront", C.c_uint64),
         ("stack_depth", C.c_uint32), ("pool_capacity", C.c_uint32),
         ("energy", C.c_float), ("max_segments", C.c_uint32), ("tail_survivors", C.c_uint64),
-        ("long_paths", C.c_uint64),
     ]
 
     def as_dict(self) -> dict:
@@ -97,7 +96,7 @@ def load() -> C.CDLL:
         "surf_destroy": ([P], None), "surf_last_error": ([P], C.c_char_p),
         "surf_shard_rows": ([P, P, C.POINTER(U32)], I32),
         "surf_set_pool_capacity": ([P, U32], I32), "surf_set_frame_batch": ([P, U32], I32),
-        "surf_set_profiling": ([P, I32], I32), "surf_set_zero_cutoff": ([P, I32], I32), "surf_set_trace_mode": ([P, I32], I32), "surf_set_persistent": ([P, I32], I32), "surf_set_long_paths": ([P, U32, U32], I32), "surf_set_tail_policy": ([P, U32, U32, U32], I32), "surf_set_tail_coop": ([P, U32], I32),
+        "surf_set_profiling": ([P, I32], I32), "surf_set_zero_cutoff": ([P, I32], I32), "surf_set_trace_mode": ([P, I32], I32), "surf_set_tail_policy": ([P, U32, U32, U32], I32), "surf_set_tail_coop": ([P, U32], I32),
         "surf_debug_capped": ([P, P, U32, C.POINTER(C.c_uint64)], I32),
         "surf_upload_scene": ([P, C.POINTER(SceneDesc)], I32),
         "surf_set_camera": ([P, P], I32),
@@ -328,17 +327,9 @@ class Renderer:
         """Single-stage drain as the cooperative tail when <= max_paths paths remain (0 = never)."""
         _check(load().surf_set_tail_coop(self._h, max_paths), "surf_set_tail_coop", self._h)
 
-    def set_long_paths(self, escape_segments: int = 16, segments_per_phase: int = 8):
-        """Paths reaching escape_segments leave the wavefront for the long pool, advanced
-        segments_per_phase segments per phase beside it (escape_segments 0 = off)."""
-        _check(load().surf_set_long_paths(self._h, escape_segments, segments_per_phase), "surf_set_long_paths", self._h)
-
-    def set_persistent(self, on: bool):
-        """Out-of-step (persistent) wavefront traversal on/off (identical results)."""
-        _check(load().surf_set_persistent(self._h, 1 if on else 0), "surf_set_persistent", self._h)
-
     def set_trace_mode(self, mode: int):
-        """0: one ray per lane; 1: one ray per wave (cooperative), for trace_closest/trace_any."""
+        """0: one ray per lane; 1: one ray per wave (lanes as planes, the cooperative tail's traversal),
+        for trace_closest/trace_any."""
         _check(load().surf_set_trace_mode(self._h, mode), "surf_set_trace_mode", self._h)
 
     def set_profiling(self, on: bool):

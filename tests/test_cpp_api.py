@@ -48,3 +48,24 @@ def test_cpp_api_render_matches_oracle(oracle_scene, tmp_path):
     assert len(lines) == F and f"{F:05d} samples" in lines[-1]
     acc, _, _ = oracle_scene.render(W, H, F)
     assert np.array_equal(read_ppm(out), present(acc, F))
+    loop = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(loop) == 1 and '"frames": %d' % F in loop[0] and '"lumen_output": false' in loop[0]
+
+
+@pytest.mark.gpu
+def test_cpp_api_lumen_output(oracle_scene, tmp_path):
+    """WF_LUMEN_OUTPUT (renderer.cpp:31,955-969): with lumenOutput, frameInfo()
+    reports the serial pixel-order energy of the frames rendered so far."""
+    W, H, F = 48, 32, 3
+    out = tmp_path / "indoor.ppm"
+    r = subprocess.run([EXE, os.path.join(REPO, "assets"), str(W), str(H), str(F), str(out), "--lumen"],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    lines = [l for l in r.stdout.splitlines() if "Mrays/s" in l]
+    assert len(lines) == F
+    for f, line in enumerate(lines, start=1):
+        acc, _, _ = oracle_scene.render(W, H, f)
+        e = np.float32(0.0)
+        for p in acc.reshape(-1, 4) * (np.float32(1.0) / np.float32(f)):
+            e = np.float32(e + np.float32(np.float32(p[0] + p[1]) + p[2]))
+        assert line.endswith("%010.2f Lumen" % e), (line, e)

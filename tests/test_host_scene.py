@@ -96,3 +96,30 @@ def test_c5_deep_scene_identical():
     finally:
         o.close()
         p.close()
+
+
+@pytest.mark.parametrize("variant,n_inst", [(2, 51), (3, 91)], ids=["tlas-51", "tlas-91"])
+def test_general_tlas_scenes_identical(variant, n_inst):
+    """The general-TLAS test scenes (scattered extra instances): the product's
+    build equals the oracle's buffer for buffer, and the TLAS really splits
+    (depth > 0), so the GPU tests of these scenes exercise the interior-node
+    TLAS walk (bvh.cpp:654-778) rather than the single-leaf fast path."""
+    import surf_amd
+    o = oracle.OracleScene(variant=variant)
+    p = surf_amd.Scene.indoor(variant=variant)
+    try:
+        assert o.instance_count() == n_inst
+        a, b = o.export(), p.buffers()
+        for buf, (rec, ranges) in MASK.items():
+            assert len(a[buf]) == len(b[buf]), buf
+            x = np.frombuffer(a[buf], np.uint8).reshape(-1, rec)
+            y = np.frombuffer(b[buf], np.uint8).reshape(-1, rec)
+            for lo, hi in ranges:
+                assert np.array_equal(x[:, lo:hi], y[:, lo:hi]), f"{buf} bytes {lo}:{hi}"
+        tlas_depth, blas_depth = p.bvh_depths()
+        assert tlas_depth > 0 and o.bvh_depths()[0] == tlas_depth
+        nodes = np.frombuffer(b["tlas_nodes"], np.uint32).reshape(-1, 12)
+        assert nodes[0, 1] == 0, "TLAS root must be an interior node"
+    finally:
+        o.close()
+        p.close()

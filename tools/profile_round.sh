@@ -1,18 +1,22 @@
 #!/bin/bash
-# Collects the rocprofv3 evidence for one round on the GPU box:
-#   trace/  kernel trace + stats of the bench command
-#   fetch/  FETCH_SIZE pass, write/  WRITE_SIZE pass (separate passes:
-#           TCC slots, MI355X_MICROARCH.md "rocprofv3 PMC slots")
-# usage: tools/profile_round.sh OUTDIR [STEPS]
+# Collects the rocprofv3 evidence of one bench workload on the GPU box:
+#   trace/  kernel trace + stats of the bench command (graph replays, as timed)
+#   fetch/  FETCH_SIZE pass, write/  WRITE_SIZE pass (separate passes: TCC
+#           slots, MI355X_MICROARCH.md "rocprofv3 PMC slots")
+# then tools/summarize_profile.py writes OUTDIR/summary.json.
+# usage: tools/profile_round.sh OUTDIR [WORKLOAD [STEPS]]
 set -e
 OUT=${1:-gpurun_out/prof}
-STEPS=${2:-16}
+WL=${2:-C3}
+STEPS=${3:-2}
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+CMD="bench.py --workload $WL --steps $STEPS --warmup 1 --no-cpu --profile-pass 0"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
-    python3 bench.py --steps "$STEPS" --warmup 1 --no-cpu > "$OUT/bench_traced.json" 2> "$OUT/trace.err"
+    python3 $CMD > "$OUT/bench_traced.json" 2> "$OUT/trace.err"
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- \
-    python3 bench.py --steps "$STEPS" --warmup 1 --no-cpu --profile-pass 0 > "$OUT/bench_fetch.json" 2> "$OUT/fetch.err"
+    python3 $CMD > "$OUT/bench_fetch.json" 2> "$OUT/fetch.err"
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- \
-    python3 bench.py --steps "$STEPS" --warmup 1 --no-cpu --profile-pass 0 > "$OUT/bench_write.json" 2> "$OUT/write.err"
+    python3 $CMD > "$OUT/bench_write.json" 2> "$OUT/write.err"
+python3 tools/summarize_profile.py "$OUT" "$OUT/summary.json" "python3 $CMD" "$WL" > /dev/null
 echo done

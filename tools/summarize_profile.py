@@ -5,7 +5,7 @@ FETCH_SIZE / WRITE_SIZE are in KiB.  gfx950 correction (MI355X_MICROARCH.md
 §HBM): FETCH_SIZE counts half the bytes of a wide (16 B/lane) coalesced read,
 so the read side is doubled; WRITE_SIZE is exact for 16-B stores.  The
 traversal's node/triangle fetches are 16-B vector loads too.
-usage: python tools/summarize_profile.py DIR OUT.json
+usage: python tools/summarize_profile.py DIR OUT.json [COMMAND [WORKLOAD]]
 """
 import csv
 import json
@@ -36,13 +36,15 @@ def counter(path, kernel, name):
 
 def main():
     d, out = sys.argv[1], sys.argv[2]
+    cmd = sys.argv[3] if len(sys.argv) > 3 else "python3 bench.py --steps 16 --warmup 1 --no-cpu"
+    workload = sys.argv[4] if len(sys.argv) > 4 else "C3"
     ks = kernel_stats(f"{d}/trace/run_kernel_stats.csv")
     fetch = counter(f"{d}/fetch/run_counter_collection.csv", "k_extend", "FETCH_SIZE")
     write = counter(f"{d}/write/run_counter_collection.csv", "k_extend", "WRITE_SIZE")
     bench = json.loads(open(f"{d}/bench_traced.json").read().strip().splitlines()[-1])
     res = {
-        "command": "python3 bench.py --steps 16 --warmup 1 --no-cpu  (under rocprofv3 --kernel-trace --stats); "
-                   "PMC passes: same command with --profile-pass 0, one counter per pass",
+        "command": cmd + "  (under rocprofv3 --kernel-trace --stats; PMC passes: the same command, one counter per pass)",
+        "workload": workload,
         "kernels": ks,
         "bench_value_traced": bench["value"],
         "k_extend_pmc": {
