@@ -185,8 +185,11 @@ int surf_set_zero_cutoff(surf_ctx* ctx, int enabled);
  * stage to the end; default 16).  Results do not depend on the policy.
  * Drains the context first. */
 int surf_set_tail_policy(surf_ctx* ctx, uint32_t threshold_paths, uint32_t lanes_per_wave, uint32_t stage_segments);
-/* Drain paths handed to the cooperative tail (one path per 64-lane wave, the
- * lanes-as-planes traversal; default 60000, 0 = never).  Identical results. */
+/* Drain paths handed to the cooperative tail (default 60000, 0 = never): one
+ * path per 64-lane wave with the lanes-as-planes traversal (single-leaf TLAS of
+ * <= 64 instances); with SURF_TAIL_ROWS=1 in the environment at surf_create,
+ * four paths per wave (one per 16-lane row, a path queue; <= 16 instances).
+ * Identical results. */
 int surf_set_tail_coop(surf_ctx* ctx, uint32_t max_paths);
 /* Diagnostics: how many paths the segment cap ended in the current sample
  * stream, and the sample ids (frame slot * shard pixels + pixel) of the first
@@ -242,9 +245,10 @@ int surf_trace_closest(surf_ctx* ctx, uint32_t n, const float* o, const float* d
 int surf_trace_any(surf_ctx* ctx, uint32_t n, const float* o, const float* d, const float* tmax,
                    uint8_t* occluded);
 /* 0: one ray per lane (the wavefront kernels' traversal); 1: one ray per
- * 64-lane wave, lanes as the node record's planes (the cooperative tail's
- * traversal; needs a single-leaf TLAS of <= 64 instances and a BVH stack of
- * <= 64 entries).  Results are identical; selects what surf_trace_* run. */
+ * 64-lane wave, lanes as the node record's planes (needs a single-leaf TLAS of
+ * <= 64 instances and a BVH stack of <= 64 entries); 2: one ray per 16-lane
+ * row, four per wave (the drain's traversal; single-leaf TLAS of <= 16
+ * instances, stack <= 64).  Results are identical; selects what surf_trace_* run. */
 int surf_set_trace_mode(surf_ctx* ctx, int mode);
 
 /* ---- host scene build (the reference's main.cpp scene, OBJ assets) ----

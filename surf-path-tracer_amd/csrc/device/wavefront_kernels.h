@@ -122,7 +122,8 @@ struct Counters {
     uint32_t segMax;                 /* longest finished path (extension rays), diagnostics */
     uint32_t survN;                  /* k_tail survivors appended (may exceed survCap) */
     uint32_t survCap;
-    uint32_t _pad2[3];
+    uint32_t rowNext;                /* k_tail_rows work queue: next path to hand out */
+    uint32_t _pad2[2];
     unsigned long long issued[2];    /* stream samples issued, per parity */
     unsigned long long limit;        /* host-written issue limit (frame window) */
     unsigned long long baseFrame;    /* absolute frame index of stream frame 0 */
@@ -510,6 +511,28 @@ __device__ __forceinline__ bool leafWave(const float4* tri, uint32_t lf, uint32_
 __device__ unsigned long long g_segStats[8];
 #endif
 struct SegStats { unsigned long long cycInst, cycLoop, visits, leaves, tris, entered, cycWait, cycLeaf; };
+
+/* SURF_DRAIN_TRACE builds: (end time, segments, start time, state at the
+ * start: age | inMedium << 16 | lastSpecular << 17 | 255 max(T) << 24) of every
+ * path the cooperative drain kernels finish, real-time clock (diagnostics). */
+#ifndef SURF_DRAIN_TRACE
+#define SURF_DRAIN_TRACE 0
+#endif
+#if SURF_DRAIN_TRACE
+constexpr uint32_t kDrainTraceCap = 1u << 18;
+__device__ uint4 g_drainEnd[kDrainTraceCap];
+__device__ uint32_t g_drainEndN;
+__device__ __forceinline__ uint32_t drainState(float4 d4, float4 T4) {
+    const uint32_t fl = f2u(d4.w);
+    const float m = fminf(fmaxf(fmaxf(T4.x, T4.y), T4.z), 1.0f);
+    return min(fl >> 2, 0xffffu) | ((fl & 3u) << 16) | ((uint32_t)(m * 255.0f) << 24);
+}
+__device__ __forceinline__ void drainTraceEnd(unsigned long long t0, uint32_t seg, uint32_t state) {
+    const unsigned long long t = wall_clock64();
+    const uint32_t k = atomicAdd(&g_drainEndN, 1u);
+    if (k < kDrainTraceCap) g_drainEnd[k] = make_uint4((uint32_t)t, state, seg, (uint32_t)t0);
+}
+#endif
 
 /* Lanes-as-planes slab distances of the record held in row `row` (lanes
  * 16 row .. 16 row + 13) of v: the DPP moves of slabPair stay inside a row of
@@ -1482,6 +1505,10 @@ __global__ __launch_bounds__(64, SURF_COOP_WAVES) void k_tail_coop(DevScene S, P
     float4 o4 = cur.o[i], d4 = cur.d[i], T4 = cur.T[i];
     const uint32_t slot = f2u(o4.w) / npx;
     unsigned long long nExt = 0, nHit = 0, nCont = 0, nSh = 0, nAcc = 0, nUn = 0;
+#if SURF_DRAIN_TRACE
+    const unsigned long long tStart = wall_clock64();
+    const uint32_t state0 = drainState(d4, T4);
+#endif
 #if SURF_SEG_TIMING
     unsigned long long cyc[3] = {0, 0, 0};
     SegStats ss{0, 0, 0, 0, 0, 0, 0, 0};
@@ -1537,6 +1564,9 @@ __global__ __launch_bounds__(64, SURF_COOP_WAVES) void k_tail_coop(DevScene S, P
         o4 = r.o; d4 = r.d; T4 = r.T;
     }
     if (lead) {
+#if SURF_DRAIN_TRACE
+        drainTraceEnd(tStart, (uint32_t)nExt, state0);
+#endif
         const uint32_t st = blockIdx.x % kStripes;
         unsigned long long* ev = C->evS[st];
         __threadfence();

@@ -24,6 +24,7 @@
 
 #include "surf_hip.h"
 #include "device/wavefront_kernels.h"
+#include "device/rows_tail.h"
 
 using namespace surfdev;
 
@@ -110,7 +111,8 @@ struct surf_ctx {
     uint32_t coopAll = 60000;      /* drain paths left to the cooperative (one path per wave) tail (surf_set_tail_coop) */
     int drainReplays = 1;          /* graph replays per host poll while draining (SURF_DRAIN_REPLAYS) */
     bool coopEligible = false;     /* single-leaf TLAS of <= 64 instances, LDS tables */
-    int traceMode = 0;             /* surf_trace_closest/_any: 0 one ray per lane, 1 one ray per wave */
+    int traceMode = 0;             /* surf_trace_closest/_any: 0 one ray per lane, 1 one ray per wave, 2 one ray per 16-lane row */
+    bool tailRows = false;         /* drain on k_tail_rows (four paths per wave; SURF_TAIL_ROWS=1) instead of k_tail_coop */
     bool sortRays = true;          /* order each phase's rays by start instance (SURF_SORT=0: off) */
     /* ray order (k_bincount / k_binscan / k_binscatter each phase) */
     uint32_t* order = nullptr;
@@ -178,6 +180,10 @@ void destroyGraph(surf_ctx* c) {
 uint32_t stackWords(const surf_ctx* c, uint32_t block) { return c->stackDepth * block; }
 /* one-ray-per-wave traversal (traceWave): a stack of node records, 16 words per entry */
 uint32_t recStackWords(const surf_ctx* c) { return c->stackDepth * 16u; }
+/* Dynamic LDS of the four-rows kernels: four record stacks, then the trace tables. */
+size_t rowsLds(const surf_ctx* c) {
+    return ((size_t)4 * recStackWords(c) + kRowProWords) * sizeof(float) + (size_t)c->nInstances * (sizeof(TraceInst) + sizeof(uint32_t));
+}
 /* Dynamic LDS of the one-ray-per-wave kernels: the record stack, then the trace tables. */
 size_t coopLds(const surf_ctx* c) {
     return (size_t)recStackWords(c) * sizeof(float) + (size_t)c->nInstances * (sizeof(TraceInst) + sizeof(uint32_t));
@@ -515,6 +521,8 @@ void launchTail(surf_ctx* c, Pool in, uint32_t n, uint32_t lpw, uint32_t firstCo
 /* The cooperative drain uses the lanes-as-planes wave traversal (traceWave):
  * single-leaf TLAS of <= 64 instances, stack of node records in 64 lanes. */
 bool waveEligible(const surf_ctx* c) { return c->coopEligible && c->stackDepth <= 64; }
+/* The four-rows traversal: as the wave traversal, with at most one instance per lane of a row. */
+bool rowsEligible(const surf_ctx* c) { return waveEligible(c) && c->S.tlasLeafCount <= kRowInst; }
 
 /* Regen counted each pool-0 path's next extension ray (firstCounted). */
 int runTail(surf_ctx* c) {
@@ -532,6 +540,21 @@ int runTail(surf_ctx* c) {
             SURF_CHECK(c, hipStreamSynchronize(c->stream));
             const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
             std::fprintf(stderr, "[surf tail] stage %d: %u paths at %.2f ms\n", stage, cnt, ms);
+        }
+        if (c->tailRows && rowsEligible(c) && cnt <= c->coopAll) {
+            /* every remaining path through the row queue: as many four-row
+             * waves as are resident at once, each row taking the next path
+             * when its own ends */
+            int cus = 256;
+            hipDeviceProp_t prop;
+            if (hipGetDeviceProperties(&prop, c->device) == hipSuccess && prop.multiProcessorCount > 0) cus = prop.multiProcessorCount;
+            const uint32_t blocks = std::min<uint32_t>((cnt + 3u) / 4u, (uint32_t)cus * 4u * SURF_ROWS_WAVES);
+            SURF_CHECK(c, hipMemsetAsync(&c->ctr->rowNext, 0, sizeof(uint32_t), c->stream));
+            hipLaunchKernelGGL(k_tail_rows, dim3(blocks), dim3(64), rowsLds(c), c->stream, c->S, in, cnt, c->rad, c->frameDone,
+                               c->npx, c->window, c->ctr, recStackWords(c), firstCounted);
+            SURF_CHECK(c, hipGetLastError());
+            c->stats.tail_survivors += cnt;
+            break;
         }
         if (waveEligible(c) && cnt <= c->coopAll) {
             hipLaunchKernelGGL(k_tail_coop, dim3(cnt), dim3(64), coopLds(c), c->stream, c->S, in, cnt, c->rad, c->frameDone,
@@ -562,6 +585,26 @@ int runTail(surf_ctx* c) {
         float t; (void)hipEventElapsedTime(&t, c->pev[0], c->pev[1]);
         c->stats.ms_tail += t;
     }
+#if SURF_DRAIN_TRACE
+    if (const char* path = std::getenv("SURF_DRAIN_TRACE_FILE")) {
+        /* diagnostics: one line per path the cooperative drain finished */
+        SURF_CHECK(c, hipStreamSynchronize(c->stream));
+        uint32_t nrec = 0;
+        SURF_CHECK(c, hipMemcpyFromSymbol(&nrec, HIP_SYMBOL(g_drainEndN), sizeof nrec));
+        nrec = std::min(nrec, kDrainTraceCap);
+        std::vector<uint4> rec(nrec);
+        if (nrec) SURF_CHECK(c, hipMemcpyFromSymbol(rec.data(), HIP_SYMBOL(g_drainEnd), nrec * sizeof(uint4)));
+        int khz = 0;
+        (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device);
+        if (FILE* f = std::fopen(path, "a")) {
+            std::fprintf(f, "# drain %u paths, clock %d kHz: end_lo state segments start_lo\n", n, khz);
+            for (const uint4& r : rec) std::fprintf(f, "%u %u %u %u\n", r.x, r.y, r.z, r.w);
+            std::fclose(f);
+        }
+        const uint32_t zero = 0;
+        SURF_CHECK(c, hipMemcpyToSymbol(HIP_SYMBOL(g_drainEndN), &zero, sizeof zero));
+    }
+#endif
 #if SURF_SEG_TIMING
     if (dbg) {
         SURF_CHECK(c, hipMemcpyAsync(c->hctr, c->ctr, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
@@ -693,6 +736,7 @@ int createCtx(int dev, uint32_t w, uint32_t h, std::vector<uint32_t> rows, surf_
     c->extBlock = extBlock;
     if (const char* e = std::getenv("SURF_SORT")) c->sortRays = e[0] != '0';
     if (const char* e = std::getenv("SURF_CONNECT_GLOBAL")) c->connectGlobal = e[0] != '0';
+    if (const char* e = std::getenv("SURF_TAIL_ROWS")) c->tailRows = e[0] == '1';
     c->width = w;
     c->height = h;
     c->rows = std::move(rows);
@@ -820,9 +864,11 @@ int surf_set_tail_coop(surf_ctx* c, uint32_t max_paths) {
 
 int surf_set_trace_mode(surf_ctx* c, int mode) {
     if (!c) return fail(nullptr, SURF_ERR_INVALID, "ctx is NULL");
-    if (mode < 0 || mode > 1) return fail(c, SURF_ERR_INVALID, "trace mode must be 0 or 1");
+    if (mode < 0 || mode > 2) return fail(c, SURF_ERR_INVALID, "trace mode must be 0, 1 or 2");
     if (mode == 1 && !waveEligible(c))
         return fail(c, SURF_ERR_INVALID, "one-ray-per-wave traversal needs a single-leaf TLAS of <= 64 instances and a BVH stack <= 64");
+    if (mode == 2 && !rowsEligible(c))
+        return fail(c, SURF_ERR_INVALID, "one-ray-per-row traversal needs a single-leaf TLAS of <= 16 instances and a BVH stack <= 64");
     c->traceMode = mode;
     return SURF_OK;
 }
@@ -1303,7 +1349,8 @@ int surf_trace_closest(surf_ctx* c, uint32_t n, const float* o, const float* d, 
     if (!c || (n && (!o || !d || !ot || !ou || !ov || !oi || !op))) return SURF_ERR_INVALID;
     if (!c->hasScene) return fail(c, SURF_ERR_NO_SCENE, "no scene uploaded");
     if (n == 0) return SURF_OK;
-    if (c->traceMode == 1 && !waveEligible(c)) return fail(c, SURF_ERR_INVALID, "scene no longer fits the one-ray-per-wave traversal");
+    if ((c->traceMode == 1 && !waveEligible(c)) || (c->traceMode == 2 && !rowsEligible(c)))
+        return fail(c, SURF_ERR_INVALID, "scene no longer fits the selected cooperative traversal");
     SURF_CHECK(c, hipSetDevice(c->device));
     std::vector<void*> tmp;
     float *dO, *dD; float4* dT; uint2* dI;
@@ -1312,7 +1359,10 @@ int surf_trace_closest(surf_ctx* c, uint32_t n, const float* o, const float* d, 
         (rc = devAlloc(c, tmp, &dT, n)) || (rc = devAlloc(c, tmp, &dI, n))) { freeList(tmp); return rc; }
     (void)hipMemcpyAsync(dO, o, 12 * (size_t)n, hipMemcpyHostToDevice, c->stream);
     (void)hipMemcpyAsync(dD, d, 12 * (size_t)n, hipMemcpyHostToDevice, c->stream);
-    if (c->traceMode == 1)
+    if (c->traceMode == 2)
+        hipLaunchKernelGGL(k_trace_closest_rows, dim3((n + 3) / 4), dim3(64), rowsLds(c), c->stream, c->S, (const float*)dO,
+                           (const float*)dD, n, dT, dI, recStackWords(c));
+    else if (c->traceMode == 1)
         hipLaunchKernelGGL(k_trace_closest_coop, dim3(n), dim3(64), coopLds(c), c->stream, c->S, (const float*)dO, (const float*)dD,
                            n, dT, dI, recStackWords(c));
     else if (c->ldsTables)
@@ -1336,7 +1386,8 @@ int surf_trace_any(surf_ctx* c, uint32_t n, const float* o, const float* d, cons
     if (!c || (n && (!o || !d || !tm || !occ))) return SURF_ERR_INVALID;
     if (!c->hasScene) return fail(c, SURF_ERR_NO_SCENE, "no scene uploaded");
     if (n == 0) return SURF_OK;
-    if (c->traceMode == 1 && !waveEligible(c)) return fail(c, SURF_ERR_INVALID, "scene no longer fits the one-ray-per-wave traversal");
+    if ((c->traceMode == 1 && !waveEligible(c)) || (c->traceMode == 2 && !rowsEligible(c)))
+        return fail(c, SURF_ERR_INVALID, "scene no longer fits the selected cooperative traversal");
     SURF_CHECK(c, hipSetDevice(c->device));
     std::vector<void*> tmp;
     float *dO, *dD, *dM; uint8_t* dR;
@@ -1346,7 +1397,10 @@ int surf_trace_any(surf_ctx* c, uint32_t n, const float* o, const float* d, cons
     (void)hipMemcpyAsync(dO, o, 12 * (size_t)n, hipMemcpyHostToDevice, c->stream);
     (void)hipMemcpyAsync(dD, d, 12 * (size_t)n, hipMemcpyHostToDevice, c->stream);
     (void)hipMemcpyAsync(dM, tm, 4 * (size_t)n, hipMemcpyHostToDevice, c->stream);
-    if (c->traceMode == 1)
+    if (c->traceMode == 2)
+        hipLaunchKernelGGL(k_trace_any_rows, dim3((n + 3) / 4), dim3(64), rowsLds(c), c->stream, c->S, (const float*)dO,
+                           (const float*)dD, (const float*)dM, n, dR, recStackWords(c));
+    else if (c->traceMode == 1)
         hipLaunchKernelGGL(k_trace_any_coop, dim3(n), dim3(64), coopLds(c), c->stream, c->S, (const float*)dO, (const float*)dD,
                            (const float*)dM, n, dR, recStackWords(c));
     else if (c->ldsTables)

@@ -30,7 +30,7 @@ def l2_report(a, b):
     return float(np.sqrt((per ** 2).mean())), float(per.max()), float((per > 1e-3).mean())
 
 
-@pytest.mark.parametrize("mode", [0, 1], ids=["lane-per-ray", "wave-lanes-as-planes"])
+@pytest.mark.parametrize("mode", [0, 1, 2], ids=["lane-per-ray", "wave-lanes-as-planes", "row-per-ray"])
 def test_closest_hit_records_bitexact(oracle_scene, product_scene, mode):
     W = H = 96
     (eo, ed), (so, sd, st) = oracle_scene.record_rays(W, H, 0, 0, W * H)
@@ -72,7 +72,7 @@ def test_boundary_rays_bitexact(oracle_scene, product_scene):
     o = np.concatenate([src, ao]).astype(np.float32)
     d = np.concatenate([dn, axis]).astype(np.float32)
     r = surf_amd.Renderer(product_scene, W, H)
-    for mode in (0, 1):
+    for mode in (0, 1, 2):
         r.set_trace_mode(mode)
         gpu = r.trace_closest(o, d)
         cpu = oracle_scene.trace_closest(o, d)
@@ -84,7 +84,7 @@ def test_boundary_rays_bitexact(oracle_scene, product_scene):
             assert np.array_equal(r.trace_any(o, d, tmax), oracle_scene.trace_any(o, d, tmax)), f"mode {mode}"
 
 
-@pytest.mark.parametrize("mode", [0, 1], ids=["lane-per-ray", "wave-lanes-as-planes"])
+@pytest.mark.parametrize("mode", [0, 1, 2], ids=["lane-per-ray", "wave-lanes-as-planes", "row-per-ray"])
 def test_any_hit_bitexact(oracle_scene, product_scene, mode):
     W = H = 96
     _, (so, sd, st) = oracle_scene.record_rays(W, H, 1, 0, W * H)
@@ -133,14 +133,18 @@ def test_render_64x64x4_bitexact(oracle_scene, product_scene):
     _assert_counts(stats, cnt)
 
 
-@pytest.mark.parametrize("policy", [(0, 0, 16), (0, 8, 4), (1 << 30, 0, 8), (1, 0, 0)],
-                         ids=["staged+coop", "8-lanes-staged", "tail-from-start", "wavefront-to-end"])
-def test_drain_policies_bitexact(oracle_scene, product_scene, policy):
-    """Every drain schedule (lane stages with survivor hand-off, the cooperative
-    one-path-per-wave tail, tail from the first phase, wavefront to the end)
-    gives the same radiance and event counts."""
+@pytest.mark.parametrize("policy,coop,rows", [((0, 0, 16), 60000, "1"), ((0, 0, 16), 60000, "0"), ((0, 8, 4), 0, "1"),
+                                              ((1 << 30, 0, 8), 1 << 30, "1"), ((1 << 30, 0, 8), 1 << 30, "0"), ((1, 0, 0), 0, "1")],
+                         ids=["staged+rows", "staged+coop", "8-lanes-staged", "rows-from-start", "coop-from-start",
+                              "wavefront-to-end"])
+def test_drain_policies_bitexact(oracle_scene, product_scene, policy, coop, rows, monkeypatch):
+    """Every drain schedule (lane stages with survivor hand-off, the four-rows
+    tail with its path queue, the one-path-per-wave tail, tail from the first
+    phase, wavefront to the end) gives the same radiance and event counts."""
+    monkeypatch.setenv("SURF_TAIL_ROWS", rows)
     r0 = surf_amd.Renderer(product_scene, 96, 64)
     r0.set_tail_policy(*policy)
+    r0.set_tail_coop(coop)
     r0.render(4, 0, 0)
     g = r0.accumulator()
     st = r0.stats()
@@ -353,8 +357,9 @@ def test_general_tlas_bitexact(variant):
         assert p.bvh_depths()[0] > 0, "TLAS did not split"
         W, H = 64, 48
         r = surf_amd.Renderer(p, W, H, frame_batch=16)
-        with pytest.raises(surf_amd.SurfError):
-            r.set_trace_mode(1)           # the one-ray-per-wave traversal needs a single-leaf TLAS
+        for mode in (1, 2):
+            with pytest.raises(surf_amd.SurfError):
+                r.set_trace_mode(mode)    # the cooperative traversals need a single-leaf TLAS
         (eo, ed), (so, sd, st) = o.record_rays(W, H, 0, 0, W * H)
         rng = np.random.default_rng(7)
         ro = rng.uniform([-9, -0.9, -9], [9, 8.9, 9], size=(20000, 3)).astype(np.float32)
