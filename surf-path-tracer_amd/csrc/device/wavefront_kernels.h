@@ -604,12 +604,20 @@ __device__ __forceinline__ uint32_t slabDecide(float v, float oA, float rdA, flo
         m0 = tmax(tmax(t0x, t0y), t0a);
         m1 = tmin(tmin(t1x, t1y), t1a);
     }
-    const float dist = (m1 >= m0 && m0 < depth && m1 > 0.0f) ? m0 : kFarAway;   /* never NaN */
-    const float d0 = dppMov<kDppShr6>(dist);          /* lane 10 <- lane 4: box 0 */
-    const bool sw = d0 > dist;                          /* if (dn > df) swap */
-    const float nearD = sw ? dist : d0, farD = sw ? d0 : dist;
-    const uint32_t bits = (sw ? 1u : 0u) | (nearD != kFarAway ? 2u : 0u) | (farD != kFarAway ? 4u : 0u);
-    return (uint32_t)__builtin_amdgcn_readlane((int)bits, (int)(10u + 16u * row));
+    /* blasTrace: dist_b = hit_b ? m0_b : kFarAway, swap when dn > df.  With
+     * hit_b = (m1 >= m0 && m0 < depth && m1 > 0) (false on NaN) and m0 < depth
+     * <= kFarAway for a hit: swap = hit1 && (!hit0 || m0_0 > m0_1).  The three
+     * facts come out of the compares as lane masks (SGPRs) and the choice is
+     * scalar: no select / readlane chain in the vector unit. */
+    const unsigned long long H = __ballot(m1 >= m0 && m0 < depth && m1 > 0.0f);   /* lanes 4 / 10: box 0 / box 1 hit */
+    const float mp = dppMov<kDppShr6>(m0);              /* lane 10 <- lane 4 */
+    const unsigned long long G = __ballot(mp > m0);      /* lane 10: m0 of box 0 > m0 of box 1 */
+    const uint32_t sh = 16u * row;
+    const uint32_t hit0 = (uint32_t)(H >> (4u + sh)) & 1u, hit1 = (uint32_t)(H >> (10u + sh)) & 1u;
+    const uint32_t gt = (uint32_t)(G >> (10u + sh)) & 1u;
+    const uint32_t sw = hit1 & (gt | (hit0 ^ 1u));
+    const uint32_t farHit = sw ? hit0 : hit1;
+    return sw | ((sw | hit0) << 1) | (farHit << 2);
 }
 __device__ __forceinline__ void waitLoadsAfterBits(float& v, uint32_t bits) {
     asm volatile("s_waitcnt vmcnt(0)" : "+v"(v) : "s"(bits));
@@ -639,6 +647,13 @@ __device__ __forceinline__ float loadEarly(const float* p) {
     return v;
 }
 __device__ __forceinline__ void waitLoads(float& v) { asm volatile("s_waitcnt vmcnt(0)" : "+v"(v)); }
+/* loadEarly with a wave-uniform base in SGPRs and a per-lane byte offset (the
+ * saddr form: no per-visit 64-bit address arithmetic in the vector unit). */
+__device__ __forceinline__ float loadEarlyS(const float* base, uint32_t offBytes) {
+    float v;
+    asm volatile("global_load_dword %0, %1, %2" : "=v"(v) : "v"(offBytes), "s"(base));
+    return v;
+}
 /* ... and not before a and b are computed (the scheduler would hoist it). */
 __device__ __forceinline__ void waitLoadsAfter(float& v, float a, float b) {
     asm volatile("s_waitcnt vmcnt(0)" : "+v"(v) : "s"(a), "s"(b));
@@ -659,6 +674,7 @@ __device__ __forceinline__ bool blasWalk(const DevScene& S, uint32_t nodeOff, co
     const uint32_t half = (lane >> 4) & 1u;
     const float oA = pick3(o, ax), rdA = pick3(rd, ax);
     const float* nodesF = reinterpret_cast<const float*>(S.nodes);
+    const uint32_t laneOff = 4u * (16u * half + dw);     /* byte offset of this lane's word in a record pair */
     /* the root's children: both records (rows 0/1), the far one to the stack */
     const uint32_t cmin = cn < cf ? cn : cf;
     float cur = nodesF[16u * (cmin + half) + dw];
@@ -695,7 +711,7 @@ __device__ __forceinline__ bool blasWalk(const DevScene& S, uint32_t nodeOff, co
             continue;
         }
         const uint32_t c0 = nodeOff + lf;
-        float nxt = loadEarly(nodesF + 16u * (c0 + half) + dw);
+        float nxt = loadEarlyS(nodesF + 16u * c0, laneOff);
         const uint32_t bits = slabDecide<FIN>(cur, oA, rdA, depth, row);
         const uint32_t nearRow = bits & 1u;
 #if SURF_SEG_TIMING
@@ -751,9 +767,10 @@ __device__ __forceinline__ bool blasWave(const DevScene& S, const TraceInst& I, 
  * order, each applying the depth test to its ranges at its turn (with the
  * depth the earlier instances left), so a missed instance costs a few
  * readlanes instead of a serial transform, three divisions and a slab test. */
+constexpr uint32_t kProWords = 64u * 16u;   /* LDS prologue table of the wave traversal: 16 floats per lane */
 template <bool ANY>
 __device__ __forceinline__ bool traceWave(const DevScene& S, const TraceTables& Tt, V3 o, V3 d, float& depth, float& hu,
-                                          float& hv, uint32_t& hinst, uint32_t& hprim, float* rs, SegStats* ss = nullptr) {
+                                          float& hv, uint32_t& hinst, uint32_t& hprim, float* rs, float4* pro, SegStats* ss = nullptr) {
     bool any = false;
     const uint32_t nI = S.tlasLeafCount;
     if (nI > 64u) {
@@ -775,22 +792,28 @@ __device__ __forceinline__ bool traceWave(const DevScene& S, const TraceTables& 
     unsigned long long t0 = __builtin_readcyclecounter();
 #endif
     const uint32_t lane = __lane_id();
-    V3 oo = mk3(0.0f, 0.0f, 0.0f), dd = oo, rd = oo;
-    float a0 = 0.0f, a1 = 0.0f, b0 = 0.0f, b1 = 0.0f;
+    /* lane k: instance k's object-space ray, 1/d and root-children ranges, kept
+     * in the LDS prologue table (not in registers through the walk) */
+    bool keep = false;
     if (lane < nI) {
         const TraceInst& I = Tt.inst[Tt.order[lane]];
-        oo = mk3(rowDot(I.m0, o.x, o.y, o.z, 1.0f), rowDot(I.m1, o.x, o.y, o.z, 1.0f), rowDot(I.m2, o.x, o.y, o.z, 1.0f));
+        V3 oo = mk3(rowDot(I.m0, o.x, o.y, o.z, 1.0f), rowDot(I.m1, o.x, o.y, o.z, 1.0f), rowDot(I.m2, o.x, o.y, o.z, 1.0f));
         if (!I.meta.z) oo = divs(oo, rowDot(I.m3, o.x, o.y, o.z, 1.0f));
-        dd = mk3(rowDot(I.m0, d.x, d.y, d.z, 0.0f), rowDot(I.m1, d.x, d.y, d.z, 0.0f), rowDot(I.m2, d.x, d.y, d.z, 0.0f));
-        rd = mk3(1.0f / dd.x, 1.0f / dd.y, 1.0f / dd.z);
+        const V3 dd = mk3(rowDot(I.m0, d.x, d.y, d.z, 0.0f), rowDot(I.m1, d.x, d.y, d.z, 0.0f), rowDot(I.m2, d.x, d.y, d.z, 0.0f));
+        const V3 rd = mk3(1.0f / dd.x, 1.0f / dd.y, 1.0f / dd.z);
+        float a0, a1, b0, b1;
         slabRange(I.r0, I.r1, oo, rd, a0, a1);
         slabRange(I.r2, I.r3, oo, rd, b0, b1);
+        /* candidates: a root child that misses at the entry depth misses at
+         * every later (smaller) depth too; root leaves are always taken */
+        keep = f2u(I.r1.w) != 0u || slabHit(a0, a1, depth) != kFarAway || slabHit(b0, b1, depth) != kFarAway;
+        float4* p = pro + 4u * lane;
+        p[0] = make_float4(oo.x, oo.y, oo.z, a0);
+        p[1] = make_float4(dd.x, dd.y, dd.z, a1);
+        p[2] = make_float4(rd.x, rd.y, rd.z, b0);
+        p[3] = make_float4(b1, 0.0f, 0.0f, 0.0f);
     }
-    /* candidates: a root child that misses at the entry depth misses at every
-     * later (smaller) depth too; root leaves are always taken */
-    const bool rootLeaf = lane < nI && f2u(Tt.inst[Tt.order[lane]].r1.w) != 0u;
-    unsigned long long cand = __ballot(lane < nI && (rootLeaf || slabHit(a0, a1, depth) != kFarAway ||
-                                                     slabHit(b0, b1, depth) != kFarAway));
+    unsigned long long cand = __ballot(keep);
     while (cand) {
         const uint32_t k = (uint32_t)(__ffsll((long long)cand) - 1);
         cand &= cand - 1ull;
@@ -799,17 +822,19 @@ __device__ __forceinline__ bool traceWave(const DevScene& S, const TraceTables& 
         const uint32_t nodeOff = I.meta.x;
         const float4* tri = S.tris + 3u * I.meta.y;
         const uint32_t rlf = f2u(I.r0.w), rcnt = f2u(I.r1.w);
+        const float4* pk = pro + 4u * k;                    /* one address for the wave: an LDS broadcast */
+        const float4 q0 = pk[0], q1 = pk[1], q2 = pk[2], q3 = pk[3];
         float dn = 0.0f, df = 0.0f;
         uint32_t cn = nodeOff + rlf, cf = cn + 1u;
         if (rcnt == 0u) {
             /* root: never box-tested (bvh.cpp:131); its children's boxes are in its record */
-            dn = slabHit(bcast(a0, k), bcast(a1, k), depth);
-            df = slabHit(bcast(b0, k), bcast(b1, k), depth);
+            dn = slabHit(q0.w, q1.w, depth);
+            df = slabHit(q2.w, q3.x, depth);
             if (dn > df) { const float t = dn; dn = df; df = t; const uint32_t c = cn; cn = cf; cf = c; }
             if (dn == kFarAway) continue;
         }
-        const V3 ok = mk3(bcast(oo.x, k), bcast(oo.y, k), bcast(oo.z, k));
-        const V3 dk = mk3(bcast(dd.x, k), bcast(dd.y, k), bcast(dd.z, k));
+        const V3 ok = xyz(q0);
+        const V3 dk = xyz(q1);
 #if SURF_SEG_TIMING
         if (ss) { const unsigned long long t1 = __builtin_readcyclecounter(); ss->cycInst += t1 - t0; t0 = t1; }
 #endif
@@ -817,7 +842,7 @@ __device__ __forceinline__ bool traceWave(const DevScene& S, const TraceTables& 
         if (rcnt != 0u) {
             h = leafWave<ANY>(tri, rlf, rcnt, ok, dk, depth, hu, hv, hprim);
         } else {
-            const V3 rk = mk3(bcast(rd.x, k), bcast(rd.y, k), bcast(rd.z, k));
+            const V3 rk = xyz(q2);
             h = (S.finiteBoxes && finite3(ok) && finite3(rk))
                     ? blasWalk<ANY, true>(S, nodeOff, tri, ok, dk, rk, dn, df, cn, cf, depth, hu, hv, hprim, rs, ss)
                     : blasWalk<ANY, false>(S, nodeOff, tri, ok, dk, rk, dn, df, cn, cf, depth, hu, hv, hprim, rs, ss);
@@ -885,10 +910,7 @@ __device__ __forceinline__ void blockCount(Counters* C, const int (&idx)[N], con
  * k_shade through order[]; hit records stay in order i, so the paths, their
  * results and the append order of the next pool are unchanged in content --
  * only the interleaving of lanes changes. */
-#ifndef SURF_POOL_DIR
-#define SURF_POOL_DIR 0            /* direction-sign bits in the pool key (0, 1: d.x, 2: d.x and d.z) */
-#endif
-constexpr uint32_t kBins = 64u << SURF_POOL_DIR;
+constexpr uint32_t kBins = 64;
 constexpr uint32_t kSortBlocks = 256;
 static_assert(kBins <= 256u, "pool/shadow keys are one byte");
 
@@ -899,11 +921,8 @@ static_assert(kBins <= 256u, "pool/shadow keys are one byte");
 __device__ __forceinline__ uint8_t poolKey(const DevScene& S, uint32_t inst, float4 o, float4 d) {
     const uint32_t cx = (o.x - S.cellLo[0]) * S.cellScale[0] >= 1.0f ? 1u : 0u;
     const uint32_t cz = (o.z - S.cellLo[2]) * S.cellScale[2] >= 1.0f ? 1u : 0u;
-    uint32_t k = (inst < 14u ? inst : 14u) * 4u + cx + 2u * cz;
-    if (SURF_POOL_DIR >= 1) k = k * 2u + (d.x < 0.0f ? 1u : 0u);
-    if (SURF_POOL_DIR >= 2) k = k * 2u + (d.z < 0.0f ? 1u : 0u);
     (void)d;
-    return (uint8_t)k;
+    return (uint8_t)((inst < 14u ? inst : 14u) * 4u + cx + 2u * cz);
 }
 
 /* Shadow-ray order key: light slot (mod 2) x the octant cell of the scene box
@@ -1495,12 +1514,13 @@ __global__ __launch_bounds__(64, SURF_COOP_WAVES) void k_tail_coop(DevScene S, P
                                                   uint32_t* __restrict__ frameDone, uint32_t npx, uint32_t window, Counters* C,
                                                   uint32_t stackWords, uint32_t firstCounted) {
     extern __shared__ uint32_t lds[];
-    const TraceTables Tt = stageTrace(S, lds, stackWords);
+    const TraceTables Tt = stageTrace(S, lds, stackWords + kProWords);
     const ShadeTables Tb{S.inst, S.mats, S.lights};
     const uint32_t i = blockIdx.x;
     if (i >= n) return;
     const bool lead = threadIdx.x == 0;
     float* rstk = reinterpret_cast<float*>(lds);     /* the record stack (16 words per entry) */
+    float4* pro = reinterpret_cast<float4*>(lds + stackWords);
     const uint32_t maxSeg = C->maxSeg, zeroCutoff = C->zeroCutoff;
     float4 o4 = cur.o[i], d4 = cur.d[i], T4 = cur.T[i];
     const uint32_t slot = f2u(o4.w) / npx;
@@ -1522,7 +1542,7 @@ __global__ __launch_bounds__(64, SURF_COOP_WAVES) void k_tail_coop(DevScene S, P
 #if SURF_SEG_TIMING
         const unsigned long long c0 = __builtin_readcyclecounter();
 #endif
-        const bool hit = traceWave<false>(S, Tt, xyz(o4), xyz(d4), depth, u, v, inst, prim, rstk, ssp);
+        const bool hit = traceWave<false>(S, Tt, xyz(o4), xyz(d4), depth, u, v, inst, prim, rstk, pro, ssp);
         (void)ssp;
         ++nExt;
         ShadeOut r;
@@ -1541,7 +1561,7 @@ __global__ __launch_bounds__(64, SURF_COOP_WAVES) void k_tail_coop(DevScene S, P
             ++nSh;
             float sdep = r.so.w, su = 0.0f, sv = 0.0f;
             uint32_t si = kUnset, sp = kUnset;
-            const bool occ = traceWave<true>(S, Tt, xyz(r.so), xyz(r.sd), sdep, su, sv, si, sp, rstk);
+            const bool occ = traceWave<true>(S, Tt, xyz(r.so), xyz(r.sd), sdep, su, sv, si, sp, rstk, pro);
             if (!occ) {
                 if (lead) addRadiance(rad, f2u(r.sd.w), xyz(r.sc));
                 ++nUn; ++nAcc;
@@ -1683,13 +1703,14 @@ __global__ __launch_bounds__(64) void k_trace_closest_coop(DevScene S, const flo
                                                            uint32_t n, float4* __restrict__ tuv, uint2* __restrict__ ip,
                                                            uint32_t stackWords) {
     extern __shared__ uint32_t lds[];
-    const TraceTables Tt = stageTrace(S, lds, stackWords);
+    const TraceTables Tt = stageTrace(S, lds, stackWords + kProWords);
     const uint32_t i = blockIdx.x;
     if (i >= n) return;
     float depth = kFarAway, u = 0.0f, v = 0.0f;
     uint32_t inst = kUnset, prim = kUnset;
     const V3 ro = mk3(o[3 * i], o[3 * i + 1], o[3 * i + 2]), rdir = mk3(d[3 * i], d[3 * i + 1], d[3 * i + 2]);
-    const bool hit = traceWave<false>(S, Tt, ro, rdir, depth, u, v, inst, prim, reinterpret_cast<float*>(lds));
+    const bool hit = traceWave<false>(S, Tt, ro, rdir, depth, u, v, inst, prim, reinterpret_cast<float*>(lds),
+                                      reinterpret_cast<float4*>(lds + stackWords));
     if (threadIdx.x == 0) {
         tuv[i] = make_float4(depth, hit ? u : 0.0f, hit ? v : 0.0f, 0.0f);
         ip[i] = make_uint2(hit ? inst : kUnset, hit ? prim : kUnset);
@@ -1699,13 +1720,14 @@ __global__ __launch_bounds__(64) void k_trace_any_coop(DevScene S, const float* 
                                                        const float* __restrict__ tmaxv, uint32_t n, uint8_t* __restrict__ occ,
                                                        uint32_t stackWords) {
     extern __shared__ uint32_t lds[];
-    const TraceTables Tt = stageTrace(S, lds, stackWords);
+    const TraceTables Tt = stageTrace(S, lds, stackWords + kProWords);
     const uint32_t i = blockIdx.x;
     if (i >= n) return;
     const V3 ro = mk3(o[3 * i], o[3 * i + 1], o[3 * i + 2]), rdir = mk3(d[3 * i], d[3 * i + 1], d[3 * i + 2]);
     float depth = tmaxv[i], u = 0.0f, v = 0.0f;
     uint32_t inst = kUnset, prim = kUnset;
-    const bool oc = traceWave<true>(S, Tt, ro, rdir, depth, u, v, inst, prim, reinterpret_cast<float*>(lds));
+    const bool oc = traceWave<true>(S, Tt, ro, rdir, depth, u, v, inst, prim, reinterpret_cast<float*>(lds),
+                                    reinterpret_cast<float4*>(lds + stackWords));
     if (threadIdx.x == 0) occ[i] = oc ? 1 : 0;
 }
 

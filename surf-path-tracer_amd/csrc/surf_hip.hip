@@ -186,7 +186,7 @@ size_t rowsLds(const surf_ctx* c) {
 }
 /* Dynamic LDS of the one-ray-per-wave kernels: the record stack, then the trace tables. */
 size_t coopLds(const surf_ctx* c) {
-    return (size_t)recStackWords(c) * sizeof(float) + (size_t)c->nInstances * (sizeof(TraceInst) + sizeof(uint32_t));
+    return ((size_t)recStackWords(c) + kProWords) * sizeof(float) + (size_t)c->nInstances * (sizeof(TraceInst) + sizeof(uint32_t));
 }
 size_t traversalLds(const surf_ctx* c, uint32_t block) {
     size_t b = (size_t)stackWords(c, block) * sizeof(uint32_t);
