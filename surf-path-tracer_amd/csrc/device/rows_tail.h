@@ -271,7 +271,7 @@ __global__ __launch_bounds__(64, SURF_ROWS_WAVES) void k_tail_rows(DevScene S, P
     const uint32_t st = blockIdx.x % kStripes;
     uint32_t idx = takePath(C);
     float4 o4 = make_float4(0, 0, 0, 0), d4 = o4, T4 = o4;
-    if (idx < n) { o4 = cur.o[idx]; d4 = cur.d[idx]; T4 = cur.T[idx]; }
+    if (idx < n) { o4 = cur.od[2u * (idx)]; d4 = cur.od[2u * (idx) + 1u]; T4 = cur.T[idx]; }
     uint32_t nExt = 0, nHit = 0, nCont = 0, nSh = 0, nAcc = 0, nUn = 0, nPaths = 0;
 #if SURF_DRAIN_TRACE
     unsigned long long tStart = wall_clock64();
@@ -319,7 +319,7 @@ __global__ __launch_bounds__(64, SURF_ROWS_WAVES) void k_tail_rows(DevScene S, P
         }
         ++nPaths;
         idx = takePath(C);
-        if (idx < n) { o4 = cur.o[idx]; d4 = cur.d[idx]; T4 = cur.T[idx]; }
+        if (idx < n) { o4 = cur.od[2u * (idx)]; d4 = cur.od[2u * (idx) + 1u]; T4 = cur.T[idx]; }
 #if SURF_DRAIN_TRACE
         tStart = wall_clock64();
         extStart = nExt;

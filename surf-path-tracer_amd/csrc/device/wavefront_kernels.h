@@ -106,7 +106,11 @@ struct DevCamera {
     uint32_t defocus;
 };
 
-struct Pool { float4* o; float4* d; float4* T; uint8_t* key; };   /* key: ray-order bin (start instance) */
+/* Path pool: od[2i] = (origin, sample id), od[2i + 1] = (direction, flags) --
+ * the ray a traversal reads is one 32-B piece of one cache line, also when it
+ * is gathered through the ray order -- T[i] = (throughput, rng state),
+ * key[i] = ray-order bin (start instance). */
+struct Pool { float4* od; float4* T; uint8_t* key; };
 /* Where a path that used up its segment budget goes. */
 struct Sink { Pool q; uint32_t* n; uint32_t cap; };
 struct ShadowQ { float4* o; float4* d; float4* c; uint8_t* key; };   /* key: ray-order bin (light instance) */
@@ -1012,7 +1016,7 @@ __global__ __launch_bounds__(kBlock, SURF_TRACE_WAVES) void k_extend(DevScene S,
     uint32_t* stk = lds + threadIdx.x;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const uint32_t j = order ? order[i] : i;       /* ray order: hit records stay in order i */
-        const float4 o = ldS(&cur.o[j]), d = ldS(&cur.d[j]);
+        const float4 o = ldS(&cur.od[2u * (j)]), d = ldS(&cur.od[2u * (j) + 1u]);
         float depth = kFarAway, u = 0.0f, v = 0.0f;
         uint32_t inst = kUnset, prim = kUnset;
         const bool hit = traceScene<false>(S, Tt, xyz(o), xyz(d), depth, u, v, inst, prim, stk, stride);
@@ -1273,11 +1277,11 @@ __global__ __launch_bounds__(kBlock, SURF_SHADE_WAVES) void k_shade(DevScene S, 
         const bool active = i < n;
         if (active) {
             const uint32_t j = order ? order[i] : i;   /* the path k_extend traced as ray i */
-            const float4 o4 = ldS(&cur.o[j]);
+            const float4 o4 = ldS(&cur.od[2u * (j)]);
             sid = f2u(o4.w);
             slot = sid / npx;
             hinst = ldSu(&hitInst[i]);
-            shadePath(S, Tb, o4, ldS(&cur.d[j]), ldS(&cur.T[j]), ldS(&hitTUV[i]), hinst, maxSeg, zeroCutoff, r);
+            shadePath(S, Tb, o4, ldS(&cur.od[2u * (j) + 1u]), ldS(&cur.T[j]), ldS(&hitTUV[i]), hinst, maxSeg, zeroCutoff, r);
             if (r.addRad) addRadiance(rad, sid, r.radd);
         }
         const unsigned long long mCont = __ballot(r.cont), mSh = __ballot(r.shadow);
@@ -1295,7 +1299,7 @@ __global__ __launch_bounds__(kBlock, SURF_SHADE_WAVES) void k_shade(DevScene S, 
         jc += rankBelow(mCont);
         js += rankBelow(mSh);
         if (r.cont) {
-            stS(&nxt.o[jc], r.o); stS(&nxt.d[jc], r.d); stS(&nxt.T[jc], r.T);
+            stS(&nxt.od[2u * (jc)], r.o); stS(&nxt.od[2u * (jc) + 1u], r.d); stS(&nxt.T[jc], r.T);
             nxt.key[jc] = poolKey(S, hinst, r.o, r.d);   /* starts on the instance it hit, from this quadrant */
         }
         if (r.shadow) {
@@ -1392,8 +1396,8 @@ __global__ __launch_bounds__(kBlock) void k_regen(DevCamera cam, Pool nxt, float
         const V3 plane = add(add(ld3(cam.firstPixel), lscl(u, ld3(cam.uVec))), lscl(v, ld3(cam.vVec)));
         const V3 dir = normalize(sub(plane, origin));
         const uint32_t slotIdx = cont + k;
-        stS(&nxt.o[slotIdx], make_float4(origin.x, origin.y, origin.z, u2f(sid)));
-        stS(&nxt.d[slotIdx], make_float4(dir.x, dir.y, dir.z, u2f(kFlagSpecular | (1u << 2))));
+        stS(&nxt.od[2u * (slotIdx)], make_float4(origin.x, origin.y, origin.z, u2f(sid)));
+        stS(&nxt.od[2u * (slotIdx) + 1u], make_float4(dir.x, dir.y, dir.z, u2f(kFlagSpecular | (1u << 2))));
         stS(&nxt.T[slotIdx], make_float4(1.0f, 1.0f, 1.0f, u2f(seed)));
         nxt.key[slotIdx] = (uint8_t)(kBins - 1u);                      /* camera rays */
         rad[sid] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -1454,7 +1458,7 @@ __device__ __forceinline__ bool runPath(const DevScene& S, const TraceTables& Tt
         if (budget != 0u && nExt >= budget) {
             const uint32_t k = atomicAdd(sink.n, 1u);
             if (k < sink.cap) {
-                sink.q.o[k] = r.o; sink.q.d[k] = r.d; sink.q.T[k] = r.T;
+                sink.q.od[2u * (k)] = r.o; sink.q.od[2u * (k) + 1u] = r.d; sink.q.T[k] = r.T;
                 done = false;
                 break;
             }
@@ -1497,7 +1501,7 @@ __global__ __launch_bounds__(64, SURF_TAIL_WAVES) void k_tail(DevScene S, Pool c
     const uint32_t lane = threadIdx.x;
     const uint32_t i = blockIdx.x * lpw + lane;
     if (lane >= lpw || i >= n) return;
-    runPath(S, Tt, Tb, cur.o[i], cur.d[i], cur.T[i], budget, Sink{surv, &C->survN, C->survCap}, rad, frameDone, npx, window, C,
+    runPath(S, Tt, Tb, cur.od[2u * (i)], cur.od[2u * (i) + 1u], cur.T[i], budget, Sink{surv, &C->survN, C->survCap}, rad, frameDone, npx, window, C,
             lds + threadIdx.x, blockDim.x, firstCounted);
 }
 
@@ -1522,7 +1526,7 @@ __global__ __launch_bounds__(64, SURF_COOP_WAVES) void k_tail_coop(DevScene S, P
     float* rstk = reinterpret_cast<float*>(lds);     /* the record stack (16 words per entry) */
     float4* pro = reinterpret_cast<float4*>(lds + stackWords);
     const uint32_t maxSeg = C->maxSeg, zeroCutoff = C->zeroCutoff;
-    float4 o4 = cur.o[i], d4 = cur.d[i], T4 = cur.T[i];
+    float4 o4 = cur.od[2u * (i)], d4 = cur.od[2u * (i) + 1u], T4 = cur.T[i];
     const uint32_t slot = f2u(o4.w) / npx;
     unsigned long long nExt = 0, nHit = 0, nCont = 0, nSh = 0, nAcc = 0, nUn = 0;
 #if SURF_DRAIN_TRACE

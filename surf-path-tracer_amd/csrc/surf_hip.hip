@@ -272,8 +272,7 @@ int allocWavefront(surf_ctx* c) {
     const size_t cap = c->capacity;
     int rc;
     for (int p = 0; p < 2; ++p) {
-        if ((rc = devAlloc(c, c->wfAllocs, &c->pool[p].o, cap))) return rc;
-        if ((rc = devAlloc(c, c->wfAllocs, &c->pool[p].d, cap))) return rc;
+        if ((rc = devAlloc(c, c->wfAllocs, &c->pool[p].od, 2 * cap))) return rc;
         if ((rc = devAlloc(c, c->wfAllocs, &c->pool[p].T, cap))) return rc;
         if ((rc = devAlloc(c, c->wfAllocs, &c->pool[p].key, cap))) return rc;
     }
@@ -286,8 +285,7 @@ int allocWavefront(surf_ctx* c) {
     /* drain stages: survivors of a tail stage, ping-pong */
     c->survCap = (uint32_t)std::min<size_t>(std::max<size_t>(cap / 16, 4096), 1u << 18);
     for (int q = 0; q < 2; ++q) {
-        if ((rc = devAlloc(c, c->wfAllocs, &c->surv[q].o, c->survCap))) return rc;
-        if ((rc = devAlloc(c, c->wfAllocs, &c->surv[q].d, c->survCap))) return rc;
+        if ((rc = devAlloc(c, c->wfAllocs, &c->surv[q].od, 2 * (size_t)c->survCap))) return rc;
         if ((rc = devAlloc(c, c->wfAllocs, &c->surv[q].T, c->survCap))) return rc;
     }
     if ((rc = devAlloc(c, c->wfAllocs, &c->hitTUV, cap))) return rc;
