@@ -47,10 +47,17 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 # Algorithmic HBM bytes per extension ray of k_extend:
 # read ray o, d (32 B: origin, direction, tmax, id), write hit t, u, v, inst, prim (20 B).
 EXTEND_BYTES_PER_RAY = 52
-# rocprofv3 summary of this bench command (tools/profile_round.sh + tools/summarize_profile.py):
+# C5: the BVH is HBM-resident, so scene bytes join B_alg: 32 B per node fetched + 36 B
+# per triangle tested, per extension ray, from the oracle's instrumented traversal
+# (profiles/r2_c5/oracle_visits.txt: 108.8 nodes, 51.4 triangles per ray).
+C5_SCENE_BYTES_PER_RAY = 32 * 108.8 + 36 * 51.4
+# Pipeline bytes per camera sample (SURVEY.md 8d B_alg): path generate, extension ray, shaded hit,
+# continuing path, shadow ray, accumulator contribution.
+B_EVENT = {"n_ext": 52, "n_hit": 68, "n_cont": 48, "n_shadow": 88, "n_acc": 24}
+# rocprofv3 summary of this bench command per workload (tools/profile_round.sh + tools/summarize_profile.py):
 # k_extend's average duration (--kernel-trace --stats) and HBM bytes per launch (FETCH_SIZE x2 +
 # WRITE_SIZE, separate PMC passes, MI355X_MICROARCH.md HBM/rocprofv3 section).
-PMC_SUMMARY = os.path.join(REPO, "profiles", "r2_c3", "summary.json")
+PMC_SUMMARY = os.path.join(REPO, "profiles", "r2_{}", "summary.json")
 
 WORKLOADS = {
     "C3": dict(scene="indoor", width=1280, height=720, spp=256, max_segments=0, cpu_row_step=5),
@@ -145,14 +152,15 @@ def cpu_baseline(args, wl, first_frame, gpu_acc):
 
 def rocprof_summary(workload):
     """k_extend's rocprofv3 average and PMC traffic from the committed summary of this command."""
-    if not os.path.exists(PMC_SUMMARY):
+    path = PMC_SUMMARY.format(workload.lower())
+    if not os.path.exists(path):
         return None
-    s = json.load(open(PMC_SUMMARY))
+    s = json.load(open(path))
     if s.get("workload", "C3") != workload:
         return None
     k = next((v for n, v in s.get("kernels", {}).items() if n.startswith("k_extend")), None)
     pmc = s.get("k_extend_pmc", {})
-    return {"source": os.path.relpath(PMC_SUMMARY, REPO), "avg_launch_ms": k["avg_us"] / 1e3 if k else None,
+    return {"source": os.path.relpath(path, REPO), "avg_launch_ms": k["avg_us"] / 1e3 if k else None,
             "traffic": pmc.get("hbm_bytes_per_launch_corrected")}
 
 
@@ -245,13 +253,14 @@ def main():
         r.set_profiling(False)
         launches = max(pe["launches_extend"], 1)
         rays_per_launch = pe["n_ext_wavefront"] / launches
-        bytes_per_launch = EXTEND_BYTES_PER_RAY * rays_per_launch
+        bytes_per_ray = EXTEND_BYTES_PER_RAY + (C5_SCENE_BYTES_PER_RAY if wl["scene"] == "c5" else 0.0)
+        bytes_per_launch = bytes_per_ray * rays_per_launch
         avg_ms = pe["ms_extend"] / launches
         achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
         roof = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
                 "kernel": "k_extend", "avg_launch_ms": round(avg_ms, 5), "launches": int(pe["launches_extend"]),
-                "rays_per_launch": round(rays_per_launch, 1), "bytes_per_ray": EXTEND_BYTES_PER_RAY,
+                "rays_per_launch": round(rays_per_launch, 1), "bytes_per_ray": round(bytes_per_ray, 1),
                 "algorithmic_bytes_per_launch": round(bytes_per_launch, 1)}
         rp = rocprof_summary(args.workload)
         if rp:
@@ -272,6 +281,12 @@ def main():
 
     if rank == 0:
         per_sample = {k: round(ev[k] / samples_per_render, 4) for k in ("n_ext", "n_hit", "n_cont", "n_shadow", "n_acc", "n_unocc")}
+        # SURVEY.md 8d whole-pipeline roofline: B_alg bytes per camera sample x samples/s against 8 TB/s
+        b_alg = 48 + sum(B_EVENT[k] * ev[k] / samples_per_render for k in B_EVENT) + 20.0 / SPP
+        if wl["scene"] == "c5":
+            b_alg += C5_SCENE_BYTES_PER_RAY * ev["n_ext"] / samples_per_render
+        pipeline = {"b_alg_per_sample": round(b_alg, 1), "achieved_gbs": round(value * 1e6 * b_alg / 1e9, 2),
+                    "frac": round(value * 1e6 * b_alg / 1e9 / HBM_PEAK_GBS, 6)}
         out = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -295,6 +310,7 @@ def main():
                        "parallelism": (f"row shards x{world} (rows interleaved in blocks of {args.row_block}) + one RCCL gather per render"
                                        if world > 1 else "single GPU")},
             "roofline": roof,
+            "pipeline_roofline": pipeline,
             "cpu_baseline": cpu,
             "parity": parity,
             "gpu_vs_cpu": round(value / cpu["value"], 2) if cpu and cpu.get("value") else None,
