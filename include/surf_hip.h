@@ -192,8 +192,9 @@ int surf_set_tail_policy(surf_ctx* ctx, uint32_t threshold_paths, uint32_t lanes
  * Identical results. */
 int surf_set_tail_coop(surf_ctx* ctx, uint32_t max_paths);
 /* Diagnostics: how many paths the segment cap ended in the current sample
- * stream, and the sample ids (frame slot * shard pixels + pixel) of the first
- * min(count, 64, max). */
+ * stream, and the sample ids (frame slot * shard pixels + pixel) of up to
+ * min(count, 64, max) of them (one per workgroup 0..63 that capped a path;
+ * unused entries are 0xffffffff). */
 int surf_debug_capped(surf_ctx* ctx, uint32_t* sample_ids, uint32_t max, uint64_t* count);
 /* When enabled, per-kernel device times are measured with HIP events on the
  * render stream (slower: disables the graph replay). */

@@ -301,8 +301,7 @@ __global__ __launch_bounds__(64, SURF_ROWS_WAVES) void k_tail_rows(DevScene S, P
             }
         }
         if (lead && r.capped) {
-            const unsigned long long k = atomicAdd(&C->ev[7], 1ull);
-            if (k < 64) C->capped[k] = f2u(o4.w);
+            noteCapped(C, f2u(o4.w));
         }
         if (r.cont) {
             ++nCont;

@@ -132,7 +132,7 @@ struct Counters {
     unsigned long long limit;        /* host-written issue limit (frame window) */
     unsigned long long baseFrame;    /* absolute frame index of stream frame 0 */
     unsigned long long ev[16];       /* ext, hit, cont, shadow, acc, unocc, tail paths, capped paths, wavefront ext */
-    uint32_t capped[64];             /* sample ids of the first paths ended by the segment cap (diagnostics) */
+    uint32_t capped[64];             /* sample ids of paths ended by the segment cap, one per workgroup 0..63 (diagnostics, ~0 = none) */
     /* event counts striped over kStripes cache lines (block b adds to stripe
      * b % kStripes): a counter shared by every block of a launch serializes its
      * atomics (~12 ns each, measured); totals = ev + sum over stripes */
@@ -141,6 +141,18 @@ struct Counters {
 };
 constexpr uint32_t kStripes = 32;    /* frameDone and event-count stripes */
 constexpr int kEvents = 9;           /* event kinds counted (ev / evS index) */
+
+/* A path ended by the segment cap: counted in the event stripes; workgroups
+ * 0..63 also keep the sample id of one such path each (diagnostics).  No
+ * shared address is touched per path: a same-address atomic or load per
+ * capped path serialized k_shade under C2's 8-segment cap (33 -> 88 ms). */
+__device__ __forceinline__ void noteCappedSid(bool capped, Counters* C, uint32_t sid) {
+    if (capped && blockIdx.x < 64u) C->capped[blockIdx.x] = sid;
+}
+__device__ __forceinline__ void noteCapped(Counters* C, uint32_t sid) {
+    atomicAdd(&C->evS[blockIdx.x % kStripes][7], 1ull);
+    noteCappedSid(true, C, sid);
+}
 
 /* Where a stream sample lives: radiance slot sid = (frame % window) * npx + pixel. */
 struct StreamGeom {
@@ -1267,7 +1279,7 @@ __global__ __launch_bounds__(kBlock, SURF_SHADE_WAVES) void k_shade(DevScene S, 
     const uint32_t maxSeg = C->maxSeg, zeroCutoff = C->zeroCutoff;
     const uint32_t wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
     uint32_t it = 0;
-    unsigned long long cHit = 0, cCont = 0, cSh = 0, cAcc = 0;
+    unsigned long long cHit = 0, cCont = 0, cSh = 0, cAcc = 0, cCap = 0;
     for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x, it ^= 1u) {
         const uint32_t i = base + threadIdx.x;
         ShadeOut r;
@@ -1310,16 +1322,14 @@ __global__ __launch_bounds__(kBlock, SURF_SHADE_WAVES) void k_shade(DevScene S, 
          * connect runs before the host reads frameDone (end of the phase). */
         frameDoneAdd(frameDone + (blockIdx.x % kStripes) * window, active && !r.cont, slot);
         if (active && !r.cont && r.seg > 32u) atomicMax(&C->segMax, r.seg);   /* rare: RR ends most paths early */
-        if (r.capped) {
-            const unsigned long long k = atomicAdd(&C->ev[7], 1ull);
-            if (k < 64) C->capped[k] = sid;
-        }
+        noteCappedSid(r.capped, C, sid);
+        cCap += (unsigned long long)__popcll(__ballot(r.capped));
         cHit += (unsigned long long)__popcll(__ballot(r.hitGeom));
         cCont += (unsigned long long)__popcll(__ballot(r.cont));
         cSh += (unsigned long long)__popcll(__ballot(r.shadow));
         cAcc += (unsigned long long)__popcll(__ballot(r.accd));
     }
-    blockCount<4>(C, {1, 2, 3, 4}, {cHit, cCont, cSh, cAcc});
+    blockCount<5>(C, {1, 2, 3, 4, 7}, {cHit, cCont, cSh, cAcc, cCap});
 }
 
 template <bool LDS>
@@ -1450,8 +1460,7 @@ __device__ __forceinline__ bool runPath(const DevScene& S, const TraceTables& Tt
             }
         }
         if (r.capped) {
-            const unsigned long long k = atomicAdd(&C->ev[7], 1ull);
-            if (k < 64) C->capped[k] = f2u(o4.w);
+            noteCapped(C, f2u(o4.w));
         }
         if (!r.cont) { atomicMax(&C->segMax, r.seg); break; }
         ++nCont;
@@ -1577,8 +1586,7 @@ __global__ __launch_bounds__(64, SURF_COOP_WAVES) void k_tail_coop(DevScene S, P
         cyc[0] += c1 - c0; cyc[1] += c2 - c1; cyc[2] += c3 - c2;
 #endif
         if (lead && r.capped) {
-            const unsigned long long k = atomicAdd(&C->ev[7], 1ull);
-            if (k < 64) C->capped[k] = f2u(o4.w);
+            noteCapped(C, f2u(o4.w));
         }
         if (!r.cont) {
             if (lead) atomicMax(&C->segMax, r.seg);

@@ -394,6 +394,7 @@ int buildGraph(surf_ctx* c) {
 /* ---- sample stream ------------------------------------------------------ */
 int startStream(surf_ctx* c, uint64_t baseFrame, uint32_t maxSeg) {
     Counters h{};
+    for (uint32_t& v : h.capped) v = kUnset;
     h.maxSeg = maxSeg;
     h.zeroCutoff = c->zeroCutoff ? 1u : 0u;
     h.baseFrame = baseFrame;
@@ -827,15 +828,25 @@ int surf_set_frame_batch(surf_ctx* c, uint32_t frames) {
     return SURF_OK;
 }
 
-/* Diagnostics: sample ids (slot * npx + shard pixel) of the first paths the
- * segment cap ended in the current stream, and how many were capped. */
+/* Diagnostics: how many paths the segment cap ended in the current stream, and
+ * sample ids (slot * npx + shard pixel) of up to 64 of them (unused entries ~0). */
 int surf_debug_capped(surf_ctx* c, uint32_t* sids, uint32_t max, uint64_t* count) {
     if (!c || !count) return SURF_ERR_INVALID;
     int rc = ensureDrained(c);
     if (rc) return rc;
-    *count = c->hctr ? c->hctr->ev[7] : 0;
-    const uint32_t n = (uint32_t)std::min<uint64_t>(std::min<uint64_t>(*count, 64), max);
-    if (sids && c->hctr) std::memcpy(sids, c->hctr->capped, n * sizeof(uint32_t));
+    *count = 0;
+    if (c->hctr) {
+        unsigned long long e[kEvents];
+        streamEvents(*c->hctr, e);
+        *count = e[7];
+    }
+    /* the recorded ids: one per workgroup 0..63 that capped a path */
+    uint32_t n = 0;
+    if (c->hctr)
+        for (uint32_t k = 0; k < 64 && n < max && n < *count; ++k)
+            if (c->hctr->capped[k] != kUnset) { if (sids) sids[n] = c->hctr->capped[k]; ++n; }
+    if (sids)
+        for (uint32_t k = n; k < std::min<uint32_t>(max, 64u); ++k) sids[k] = kUnset;
     return SURF_OK;
 }
 

@@ -306,7 +306,7 @@ class Renderer:
         ids = np.zeros(64, np.uint32)
         n = C.c_uint64()
         _check(load().surf_debug_capped(self._h, _ptr(ids), 64, C.byref(n)), "surf_debug_capped", self._h)
-        return int(n.value), ids[: min(int(n.value), 64)]
+        return int(n.value), ids[ids != 0xFFFFFFFF]
 
     def set_zero_cutoff(self, on: bool):
         _check(load().surf_set_zero_cutoff(self._h, 1 if on else 0), "surf_set_zero_cutoff", self._h)
