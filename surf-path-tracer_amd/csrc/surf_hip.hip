@@ -31,6 +31,11 @@ using namespace surfdev;
 namespace {
 
 constexpr int kPhasesPerGraph = 8;          /* even: parity returns to 0 after a replay */
+/* The short graph: a render call with at most one frame left to issue (the
+ * drop-in loop's 1-spp render(), main.cpp:381-446) replays 2 phases per host
+ * poll instead of 8, so a per-frame call does not keep the pool a quarter full
+ * for 8 phases per frame. */
+constexpr int kPhasesShort = 2;
 constexpr int kPhaseEvents = 6;             /* profiling events per phase: sort, extend, shade, sort, connect, regen */
 constexpr uint32_t kMaxStack = 120;          /* LDS stack entries per ray (block 256 -> 120 KiB max) */
 constexpr uint64_t kMaxIterations = 1ull << 22;  /* safety net: a path longer than this is a bug */
@@ -122,8 +127,8 @@ struct surf_ctx {
     uint64_t tailFirstRays = 0;    /* first extension rays of drained paths: counted by regen, traced by the tail */
 
     /* graph */
-    hipGraphExec_t graphExec = nullptr;
-    hipGraph_t graph = nullptr;
+    hipGraphExec_t graphExec = nullptr, graphExecShort = nullptr;
+    hipGraph_t graph = nullptr, graphShort = nullptr;
     uint32_t gridWork = 0, gridRegen = 0, gridExtend = 0, gridConnect = 0;
 
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -171,8 +176,10 @@ void freeList(std::vector<void*>& list) {
 void destroyGraph(surf_ctx* c) {
     if (c->graphExec) (void)hipGraphExecDestroy(c->graphExec);
     if (c->graph) (void)hipGraphDestroy(c->graph);
-    c->graphExec = nullptr;
-    c->graph = nullptr;
+    if (c->graphExecShort) (void)hipGraphExecDestroy(c->graphExecShort);
+    if (c->graphShort) (void)hipGraphDestroy(c->graphShort);
+    c->graphExec = c->graphExecShort = nullptr;
+    c->graph = c->graphShort = nullptr;
 }
 
 /* Dynamic LDS of a traversal kernel with `block` threads: the per-lane stack,
@@ -383,11 +390,14 @@ void launchPhase(surf_ctx* c, int ph, hipEvent_t* ev) {
 
 int buildGraph(surf_ctx* c) {
     if (c->graphExec) return SURF_OK;
-    SURF_CHECK(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-    for (int ph = 0; ph < kPhasesPerGraph; ++ph) launchPhase(c, ph, nullptr);
-    hipError_t e = hipStreamEndCapture(c->stream, &c->graph);
-    if (e != hipSuccess) return fail(c, SURF_ERR_HIP, std::string("graph capture: ") + hipGetErrorString(e));
-    SURF_CHECK(c, hipGraphInstantiate(&c->graphExec, c->graph, nullptr, nullptr, 0));
+    for (int shortG = 0; shortG < 2; ++shortG) {
+        SURF_CHECK(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+        for (int ph = 0; ph < (shortG ? kPhasesShort : kPhasesPerGraph); ++ph) launchPhase(c, ph, nullptr);
+        hipGraph_t& g = shortG ? c->graphShort : c->graph;
+        hipError_t e = hipStreamEndCapture(c->stream, &g);
+        if (e != hipSuccess) return fail(c, SURF_ERR_HIP, std::string("graph capture: ") + hipGetErrorString(e));
+        SURF_CHECK(c, hipGraphInstantiate(shortG ? &c->graphExecShort : &c->graphExec, g, nullptr, nullptr, 0));
+    }
     return SURF_OK;
 }
 
@@ -474,13 +484,14 @@ int syncAndAccumulate(surf_ctx* c) {
 
 /* One unit of forward progress: kPhasesPerGraph phases (graph replay, or
  * direct launches with per-kernel events when profiling). */
-int advance(surf_ctx* c) {
+int advance(surf_ctx* c, bool shortRun = false) {
+    const int phases = shortRun ? kPhasesShort : kPhasesPerGraph;
     if (c->profiling) {
-        for (int ph = 0; ph < kPhasesPerGraph; ++ph) launchPhase(c, ph, &c->pev[kPhaseEvents * ph]);
-        SURF_CHECK(c, hipEventRecord(c->pev[kPhaseEvents * kPhasesPerGraph], c->stream));
+        for (int ph = 0; ph < phases; ++ph) launchPhase(c, ph, &c->pev[kPhaseEvents * ph]);
+        SURF_CHECK(c, hipEventRecord(c->pev[kPhaseEvents * phases], c->stream));
         SURF_CHECK(c, hipGetLastError());
-        SURF_CHECK(c, hipEventSynchronize(c->pev[kPhaseEvents * kPhasesPerGraph]));
-        for (int ph = 0; ph < kPhasesPerGraph; ++ph) {
+        SURF_CHECK(c, hipEventSynchronize(c->pev[kPhaseEvents * phases]));
+        for (int ph = 0; ph < phases; ++ph) {
             float t[kPhaseEvents];
             for (int k = 0; k < kPhaseEvents; ++k)
                 (void)hipEventElapsedTime(&t[k], c->pev[kPhaseEvents * ph + k], c->pev[kPhaseEvents * ph + k + 1]);
@@ -489,9 +500,9 @@ int advance(surf_ctx* c) {
             c->stats.launches_extend++;
         }
     } else {
-        SURF_CHECK(c, hipGraphLaunch(c->graphExec, c->stream));
+        SURF_CHECK(c, hipGraphLaunch(shortRun ? c->graphExecShort : c->graphExec, c->stream));
     }
-    c->stats.iterations += kPhasesPerGraph;
+    c->stats.iterations += phases;
     if (c->stats.iterations > kMaxIterations)
         return fail(c, SURF_ERR_LIMIT, "wavefront did not drain after " + std::to_string(c->stats.iterations) + " iterations");
     return SURF_OK;
@@ -658,8 +669,10 @@ int pump(surf_ctx* c, bool drain) {
             /* draining (nothing left to issue): several replays per host poll --
              * the per-replay poll, not the kernels, is what a small pool pays */
             const int reps = starved ? c->drainReplays : 1;
+            /* at most one frame left to issue (a per-frame render call): short replays */
+            const bool shortRun = !drain && target - issued <= c->npx;
             for (int k = 0; k < reps; ++k)
-                if ((rc = advance(c))) return rc;
+                if ((rc = advance(c, shortRun))) return rc;
         }
         if ((rc = syncAndAccumulate(c))) return rc;
         if (starved && inflight == 0 && c->accFrames == accBefore)

@@ -226,6 +226,11 @@ def test_pool_and_batch_invariance(product_scene):
     again.render(2)
     again.render(3, first_frame=2)
     assert np.array_equal(a.view(np.uint32), again.accumulator().view(np.uint32))
+    # the drop-in loop: one frame per render() call (main.cpp:381-446, short replays)
+    loop = surf_amd.Renderer(product_scene, W, H)
+    for f in range(F):
+        loop.render(1, first_frame=f)
+    assert np.array_equal(a.view(np.uint32), loop.accumulator().view(np.uint32))
 
 
 @pytest.mark.parametrize("shards,block", [(2, 0), (3, 16), (4, 8)])
