@@ -663,13 +663,6 @@ __device__ __forceinline__ float loadEarly(const float* p) {
     return v;
 }
 __device__ __forceinline__ void waitLoads(float& v) { asm volatile("s_waitcnt vmcnt(0)" : "+v"(v)); }
-/* loadEarly with a wave-uniform base in SGPRs and a per-lane byte offset (the
- * saddr form: no per-visit 64-bit address arithmetic in the vector unit). */
-__device__ __forceinline__ float loadEarlyS(const float* base, uint32_t offBytes) {
-    float v;
-    asm volatile("global_load_dword %0, %1, %2" : "=v"(v) : "v"(offBytes), "s"(base));
-    return v;
-}
 /* ... and not before a and b are computed (the scheduler would hoist it). */
 __device__ __forceinline__ void waitLoadsAfter(float& v, float a, float b) {
     asm volatile("s_waitcnt vmcnt(0)" : "+v"(v) : "s"(a), "s"(b));
@@ -690,7 +683,6 @@ __device__ __forceinline__ bool blasWalk(const DevScene& S, uint32_t nodeOff, co
     const uint32_t half = (lane >> 4) & 1u;
     const float oA = pick3(o, ax), rdA = pick3(rd, ax);
     const float* nodesF = reinterpret_cast<const float*>(S.nodes);
-    const uint32_t laneOff = 4u * (16u * half + dw);     /* byte offset of this lane's word in a record pair */
     /* the root's children: both records (rows 0/1), the far one to the stack */
     const uint32_t cmin = cn < cf ? cn : cf;
     float cur = nodesF[16u * (cmin + half) + dw];
@@ -727,7 +719,7 @@ __device__ __forceinline__ bool blasWalk(const DevScene& S, uint32_t nodeOff, co
             continue;
         }
         const uint32_t c0 = nodeOff + lf;
-        float nxt = loadEarlyS(nodesF + 16u * c0, laneOff);
+        float nxt = loadEarly(nodesF + 16u * (c0 + half) + dw);
         const uint32_t bits = slabDecide<FIN>(cur, oA, rdA, depth, row);
         const uint32_t nearRow = bits & 1u;
 #if SURF_SEG_TIMING
