@@ -668,12 +668,127 @@ __device__ __forceinline__ void waitLoadsAfter(float& v, float a, float b) {
     asm volatile("s_waitcnt vmcnt(0)" : "+v"(v) : "s"(a), "s"(b));
 }
 
+/* blasWalk's interior visits (FIN: o, 1/d and every box finite) as one
+ * instruction sequence: the compiler's structurized control flow spent ~70
+ * instructions per visit on flag registers and loop-carried copies, while the
+ * drain's throughput is set by instructions issued per segment (+24 per visit
+ * of either kind: +15 % drain time, profiles/r2_experiments).  Same operations
+ * as slabDecide<true> and the C++ loop, in the same order: the record's plane
+ * distances, the DPP min/max fold, the hit / order masks, the near child
+ * (row of the prefetched pair) or a pop, the far child's record to the LDS
+ * stack.  Leaves the walk at a leaf (cnt != 0; lf, cnt of it) or with the
+ * stack empty (cnt == 0).  Stack pointer in bytes (64 per entry); the
+ * records are read through a raw buffer resource at byte offset
+ * 64 (nodeOff + lf) + laneOff. */
+typedef int surfI4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void walkInteriorFin(float& cur, uint32_t& row16, uint32_t& spb, uint32_t& lf, uint32_t& cnt,
+                                                float oA, float rdA, float depth, uint32_t nodeOff, surfI4 rsrc,
+                                                uint32_t laneOff, uint32_t stkLane) {
+    float nxt, t, t0a, t1a, m0, m1, mp;
+    uint32_t addr, idx, off;
+    unsigned long long h, tt, g, a, save;
+    const unsigned long long mask0 = 0x000000000000FFFFull, mask1 = 0x00000000FFFF0000ull;
+    asm volatile(
+        "L_top_%=:\n\t"
+        "s_or_b32 %[idx], %[row], 13\n\t"
+        "v_readlane_b32 %[cnt], %[cur], %[idx]\n\t"
+        "s_or_b32 %[idx], %[row], 12\n\t"
+        "v_readlane_b32 %[lf], %[cur], %[idx]\n\t"
+        "s_cmp_lg_u32 %[cnt], 0\n\t"
+        "s_cbranch_scc1 L_exit_%=\n\t"
+        "s_add_u32 %[off], %[lf], %[noff]\n\t"
+        "s_lshl_b32 %[off], %[off], 6\n\t"
+        "buffer_load_dword %[nxt], %[loff], %[rsrc], %[off] offen\n\t"
+        "v_sub_f32 %[t], %[cur], %[oA]\n\t"
+        "v_mul_f32 %[t], %[t], %[rdA]\n\t"
+        "s_nop 1\n\t"
+        "v_min_f32_dpp %[t0a], %[t], %[t] quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_max_f32_dpp %[t1a], %[t], %[t] quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_max_f32_dpp %[m0], %[t0a], %[t0a] row_shr:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_min_f32_dpp %[m1], %[t1a], %[t1a] row_shr:4 row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_max_f32_dpp %[m0], %[t0a], %[m0] row_shr:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_min_f32_dpp %[m1], %[t1a], %[m1] row_shr:2 row_mask:0xf bank_mask:0xf\n\t"
+        /* lanes 4 / 10 of the row: box 0 / box 1 hit (m1 >= m0, m0 < depth, m1 > 0) */
+        "v_cmp_ge_f32_e64 %[h], %[m1], %[m0]\n\t"
+        "v_cmp_gt_f32_e64 %[tt], %[depth], %[m0]\n\t"
+        "s_and_b64 %[h], %[h], %[tt]\n\t"
+        "v_cmp_lt_f32_e64 %[tt], 0, %[m1]\n\t"
+        "s_and_b64 %[h], %[h], %[tt]\n\t"
+        /* lane 10: m0 of box 0 > m0 of box 1 */
+        "v_mov_b32_dpp %[mp], %[m0] row_shr:6 row_mask:0xf bank_mask:0xf\n\t"
+        "v_cmp_gt_f32_e64 %[g], %[mp], %[m0]\n\t"
+        "s_lshr_b64 %[h], %[h], %[row]\n\t"
+        "s_lshr_b64 %[g], %[g], %[row]\n\t"
+        /* bit 10 of a: swap = hit1 && (gt || !hit0) */
+        "s_lshl_b64 %[a], %[h], 6\n\t"
+        "s_not_b64 %[a], %[a]\n\t"
+        "s_or_b64 %[a], %[a], %[g]\n\t"
+        "s_and_b64 %[a], %[a], %[h]\n\t"
+        "s_bitcmp1_b64 %[a], 10\n\t"
+        "s_cbranch_scc1 L_sw_%=\n\t"
+        /* near = box 0 (row 0 of nxt): taken if hit0; box 1 pushed if hit1 */
+        "s_bitcmp1_b64 %[h], 4\n\t"
+        "s_cbranch_scc0 L_pop_%=\n\t"
+        "s_mov_b32 %[row], 0\n\t"
+        "s_bitcmp1_b64 %[h], 10\n\t"
+        "s_cbranch_scc0 L_desc_%=\n\t"
+        "v_add_u32 %[addr], %[sp], %[stk]\n\t"
+        "s_mov_b64 %[save], exec\n\t"
+        "s_mov_b64 exec, %[mask1]\n\t"
+        "s_waitcnt vmcnt(0)\n\t"
+        "ds_write_b32 %[addr], %[nxt]\n\t"
+        "s_mov_b64 exec, %[save]\n\t"
+        "s_add_u32 %[sp], %[sp], 64\n\t"
+        "s_branch L_desc_%=\n"
+        /* near = box 1 (row 1, hit); box 0 pushed if hit0 */
+        "L_sw_%=:\n\t"
+        "s_mov_b32 %[row], 16\n\t"
+        "s_bitcmp1_b64 %[h], 4\n\t"
+        "s_cbranch_scc0 L_desc_%=\n\t"
+        "v_add_u32 %[addr], %[sp], %[stk]\n\t"
+        "s_mov_b64 %[save], exec\n\t"
+        "s_mov_b64 exec, %[mask0]\n\t"
+        "s_waitcnt vmcnt(0)\n\t"
+        "ds_write_b32 %[addr], %[nxt]\n\t"
+        "s_mov_b64 exec, %[save]\n\t"
+        "s_add_u32 %[sp], %[sp], 64\n"
+        "L_desc_%=:\n\t"
+        "s_waitcnt vmcnt(0)\n\t"
+        "v_mov_b32 %[cur], %[nxt]\n\t"
+        "s_branch L_top_%=\n"
+        /* both children missed: pop (every row reads the entry) or done */
+        "L_pop_%=:\n\t"
+        "s_waitcnt vmcnt(0)\n\t"
+        "s_cmp_eq_u32 %[sp], 0\n\t"
+        "s_cbranch_scc1 L_done_%=\n\t"
+        "s_sub_u32 %[sp], %[sp], 64\n\t"
+        "v_add_u32 %[addr], %[sp], %[stk]\n\t"
+        "ds_read_b32 %[cur], %[addr]\n\t"
+        "s_mov_b32 %[row], 0\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "s_branch L_top_%=\n"
+        "L_done_%=:\n\t"
+        "s_mov_b32 %[cnt], 0\n"
+        "L_exit_%=:"
+        : [cur] "+v"(cur), [row] "+s"(row16), [sp] "+s"(spb), [lf] "=&s"(lf), [cnt] "=&s"(cnt), [nxt] "=&v"(nxt),
+          [t] "=&v"(t), [t0a] "=&v"(t0a), [t1a] "=&v"(t1a), [m0] "=&v"(m0), [m1] "=&v"(m1), [mp] "=&v"(mp),
+          [addr] "=&v"(addr), [idx] "=&s"(idx), [off] "=&s"(off), [h] "=&s"(h), [tt] "=&s"(tt), [g] "=&s"(g),
+          [a] "=&s"(a), [save] "=&s"(save)
+        : [oA] "v"(oA), [rdA] "v"(rdA), [depth] "s"(depth), [noff] "s"(nodeOff), [rsrc] "s"(rsrc), [loff] "v"(laneOff),
+          [stk] "v"(stkLane), [mask0] "s"(mask0), [mask1] "s"(mask1)
+        : "memory", "scc");
+}
+
 /* The DFS below one BLAS root (blasTrace's loop), from the root's children:
  * near child cn at distance dn (!= kFarAway), far child cf at df.  Latency:
  * a visit issues the load of BOTH children's records (row 0 of the VGPR:
  * left child, row 1: right; rows 2/3 repeat them) before its own slab test,
  * so the near child's record is in registers when the decision is made; a
  * pop loads the popped node's record into every row. */
+#define SURF_STR(x) #x
+#define SURF_XSTR(x) SURF_STR(x)
 template <bool ANY, bool FIN>
 __device__ __forceinline__ bool blasWalk(const DevScene& S, uint32_t nodeOff, const float4* tri, V3 o, V3 d, V3 rd,
                                          float dn, float df, uint32_t cn, uint32_t cf, float& depth, float& hu, float& hv,
@@ -695,53 +810,78 @@ __device__ __forceinline__ bool blasWalk(const DevScene& S, uint32_t nodeOff, co
 #if SURF_SEG_TIMING
     if (ss) ++ss->entered;
 #endif
+    /* walkInteriorFin's operands: node records as a raw buffer (gfx9 dword 3),
+     * this lane's byte offset in a record pair, its LDS stack column */
+    const uintptr_t nb = reinterpret_cast<uintptr_t>(S.nodes);
+    const surfI4 rsrc = {(int)(uint32_t)nb, (int)(uint32_t)(nb >> 32), -1, 0x00020000};
+    const uint32_t laneOff = 64u * half + 4u * dw;
+    const uint32_t stkLane = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) float*)rs) + 4u * l16;
+    (void)rsrc; (void)laneOff; (void)stkLane;
     for (;;) {
-        const uint32_t lf = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(cur), (int)(12u + 16u * row));
-        const uint32_t cnt = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(cur), (int)(13u + 16u * row));
-#if SURF_SEG_TIMING
-        if (ss) { if (cnt) { ++ss->leaves; ss->tris += cnt; } else ++ss->visits; }
+        /* interior nodes: an inner loop that leaves depth and the hit untouched
+         * (no loop-carried copies of them per visit) */
+        uint32_t lf, cnt;
+#if !SURF_SEG_TIMING && !SURF_PAD_VALU && !SURF_PAD_SALU
+        if (FIN) {
+            uint32_t row16 = 16u * row, spb = 64u * sp;
+            walkInteriorFin(cur, row16, spb, lf, cnt, oA, rdA, depth, nodeOff, rsrc, laneOff, stkLane);
+            row = row16 >> 4;
+            sp = spb >> 6;
+            if (cnt == 0u) return any;
+        } else
 #endif
-        if (cnt != 0u) {
+        for (;;) {
+            lf = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(cur), (int)(12u + 16u * row));
+            cnt = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(cur), (int)(13u + 16u * row));
 #if SURF_SEG_TIMING
-            const unsigned long long tl0 = __builtin_readcyclecounter();
+            if (ss) { if (cnt) { ++ss->leaves; ss->tris += cnt; } else ++ss->visits; }
 #endif
-            const bool lh = leafWave<ANY>(tri, lf, cnt, o, d, depth, hu, hv, hprim);
+            if (cnt != 0u) break;
+#if SURF_PAD_VALU   /* diagnostics: extra VALU / SALU issue per interior visit */
+            asm volatile(".rept " SURF_XSTR(SURF_PAD_VALU) "\n\tv_nop\n\t.endr");
+#endif
+#if SURF_PAD_SALU
+            { uint32_t z = lf; asm volatile(".rept " SURF_XSTR(SURF_PAD_SALU) "\n\ts_add_u32 %0, %0, 1\n\t.endr" : "+s"(z)); }
+#endif
+            const uint32_t c0 = nodeOff + lf;
+            float nxt = loadEarly(nodesF + 16u * (c0 + half) + dw);
+            const uint32_t bits = slabDecide<FIN>(cur, oA, rdA, depth, row);
+            const uint32_t nearRow = bits & 1u;
 #if SURF_SEG_TIMING
-            if (ss) ss->cycLeaf += __builtin_readcyclecounter() - tl0;
+            const unsigned long long tw0 = __builtin_readcyclecounter();
 #endif
-            if (lh) {
-                if (ANY) return true;
-                any = true;
+            waitLoadsAfterBits(nxt, bits);   /* on every path: the register must not be reused while the load is in flight */
+#if SURF_SEG_TIMING
+            if (ss) { asm volatile("" : "+v"(nxt)); ss->cycWait += __builtin_readcyclecounter() - tw0; }
+#endif
+            if (!(bits & 2u)) {
+                if (sp == 0u) return any;
+                cur = rs[16u * --sp + l16];
+                row = 0;
+            } else {
+                cur = nxt;
+                row = nearRow;
+                /* the far child's record (already fetched, the other row) to the LDS stack */
+                if (bits & 4u) {
+                    if (half != nearRow && lane < 32u) rs[16u * sp + l16] = nxt;
+                    ++sp;
+                }
             }
-            if (sp == 0u) break;
-            cur = rs[16u * --sp + l16];
-            row = 0;
-            continue;
         }
-        const uint32_t c0 = nodeOff + lf;
-        float nxt = loadEarly(nodesF + 16u * (c0 + half) + dw);
-        const uint32_t bits = slabDecide<FIN>(cur, oA, rdA, depth, row);
-        const uint32_t nearRow = bits & 1u;
 #if SURF_SEG_TIMING
-        const unsigned long long tw0 = __builtin_readcyclecounter();
+        const unsigned long long tl0 = __builtin_readcyclecounter();
 #endif
-        waitLoadsAfterBits(nxt, bits);   /* on every path: the register must not be reused while the load is in flight */
+        const bool lh = leafWave<ANY>(tri, lf, cnt, o, d, depth, hu, hv, hprim);
 #if SURF_SEG_TIMING
-        if (ss) { asm volatile("" : "+v"(nxt)); ss->cycWait += __builtin_readcyclecounter() - tw0; }
+        if (ss) ss->cycLeaf += __builtin_readcyclecounter() - tl0;
 #endif
-        if (!(bits & 2u)) {
-            if (sp == 0u) break;
-            cur = rs[16u * --sp + l16];
-            row = 0;
-        } else {
-            cur = nxt;
-            row = nearRow;
-            /* the far child's record (already fetched, the other row) to the LDS stack */
-            if (bits & 4u) {
-                if (half != nearRow && lane < 32u) rs[16u * sp + l16] = nxt;
-                ++sp;
-            }
+        if (lh) {
+            if (ANY) return true;
+            any = true;
         }
+        if (sp == 0u) break;
+        cur = rs[16u * --sp + l16];
+        row = 0;
     }
     return any;
 }
