@@ -107,7 +107,7 @@ __device__ __forceinline__ bool leafRows(const float4* tri, uint32_t lf, uint32_
             const float4* tp = tri + 3u * (lf + k);
             const float4 a = tp[0], e1 = tp[1], e2 = tp[2];
             prim = f2u(a.w);
-            h = triHit(xyz(a), xyz(e1), xyz(e2), o, d, t, u, v);
+            h = triHitFlat(xyz(a), xyz(e1), xyz(e2), o, d, depth, t, u, v);
         }
         const uint32_t m16 = rowBits(__ballot(h));
         if (ANY) {

@@ -237,6 +237,29 @@ SURF_HD bool triHit(V3 v0, V3 e1, V3 e2, V3 o, V3 d, float& depth, float& hu, fl
     return true;
 }
 
+/* triHit without early exits, for lanes that each test a different triangle
+ * (the leaf of a wave walk): the same operations and the same four rejection
+ * tests (each negated as written, so NaN operands reject exactly where
+ * triHit's branches do), combined with bitwise ands so no lane mask is saved
+ * and restored per test.  t, u, v are meaningful only when it returns true;
+ * depth is not updated (the caller accepts hits in triangle order). */
+SURF_HD bool triHitFlat(V3 v0, V3 e1, V3 e2, V3 o, V3 d, float depth, float& t, float& hu, float& hv) {
+    const V3 h = cross(d, e2);
+    const float a = dot(e1, h);
+    const float f = 1.0f / a;
+    const V3 s = sub(o, v0);
+    const float u = f * dot(s, h);
+    const V3 q = cross(s, e1);
+    const float v = f * dot(d, q);
+    t = f * dot(e2, q);
+    hu = u; hv = v;
+    const bool k0 = !(fabsf(a) < kEps);
+    const bool k1 = !((0.0f > u) | (u > 1.0f));
+    const bool k2 = !((0.0f > v) | ((u + v) > 1.0f));
+    const bool k3 = (kEps <= t) & (t < depth);
+    return k0 & k1 & k2 & k3;
+}
+
 /* ---- glm mat4 * vec4, pairwise column sums (type_mat4x4.inl) ---- */
 SURF_HD float mrow(const float* m, int i, float x, float y, float z, float w) {
     float a = m[0 + i] * x + m[4 + i] * y;
