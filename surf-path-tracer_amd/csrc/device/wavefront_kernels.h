@@ -699,6 +699,9 @@ __device__ __forceinline__ void walkInteriorFin(float& cur, uint32_t& row16, uin
         "s_add_u32 %[off], %[lf], %[noff]\n\t"
         "s_lshl_b32 %[off], %[off], 6\n\t"
         "buffer_load_dword %[nxt], %[loff], %[rsrc], %[off] offen\n\t"
+#if SURF_EXPOSE_LOAD   /* diagnostics: the record load's whole latency on the visit's path */
+        "s_waitcnt vmcnt(0)\n\t"
+#endif
         "v_sub_f32 %[t], %[cur], %[oA]\n\t"
         "v_mul_f32 %[t], %[t], %[rdA]\n\t"
         "s_nop 1\n\t"
@@ -821,7 +824,7 @@ __device__ __forceinline__ bool blasWalk(const DevScene& S, uint32_t nodeOff, co
         /* interior nodes: an inner loop that leaves depth and the hit untouched
          * (no loop-carried copies of them per visit) */
         uint32_t lf, cnt;
-#if !SURF_SEG_TIMING && !SURF_PAD_VALU && !SURF_PAD_SALU
+#if !SURF_PAD_VALU && !SURF_PAD_SALU   /* (timing builds count no interior visits on this path) */
         if (FIN) {
             uint32_t row16 = 16u * row, spb = 64u * sp;
             walkInteriorFin(cur, row16, spb, lf, cnt, oA, rdA, depth, nodeOff, rsrc, laneOff, stkLane);
