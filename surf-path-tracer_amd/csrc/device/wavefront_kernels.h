@@ -522,8 +522,15 @@ __device__ __forceinline__ bool leafWave(const float4* tri, uint32_t lf, uint32_
     return any;
 }
 
-/* SURF_SEG_TIMING builds: per-segment breakdown of traceWave (diagnostics). */
+/* SURF_SEG_TIMING builds: per-segment breakdown of traceWave (diagnostics).
+ * segClock waits for every outstanding memory operation, then reads the
+ * shader clock, so a section's time includes its loads. */
 #if SURF_SEG_TIMING
+__device__ __forceinline__ unsigned long long segClock() {
+    unsigned long long t;
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : : "memory");
+    return t;
+}
 __device__ unsigned long long g_segStats[8];
 #endif
 struct SegStats { unsigned long long cycInst, cycLoop, visits, leaves, tris, entered, cycWait, cycLeaf; };
@@ -831,6 +838,9 @@ __device__ __forceinline__ bool blasWalk(const DevScene& S, uint32_t nodeOff, co
             row = row16 >> 4;
             sp = spb >> 6;
             if (cnt == 0u) return any;
+#if SURF_SEG_TIMING
+            if (ss) { ++ss->leaves; ss->tris += cnt; }
+#endif
         } else
 #endif
         for (;;) {
@@ -851,11 +861,11 @@ __device__ __forceinline__ bool blasWalk(const DevScene& S, uint32_t nodeOff, co
             const uint32_t bits = slabDecide<FIN>(cur, oA, rdA, depth, row);
             const uint32_t nearRow = bits & 1u;
 #if SURF_SEG_TIMING
-            const unsigned long long tw0 = __builtin_readcyclecounter();
+            const unsigned long long tw0 = segClock();
 #endif
             waitLoadsAfterBits(nxt, bits);   /* on every path: the register must not be reused while the load is in flight */
 #if SURF_SEG_TIMING
-            if (ss) { asm volatile("" : "+v"(nxt)); ss->cycWait += __builtin_readcyclecounter() - tw0; }
+            if (ss) { asm volatile("" : "+v"(nxt)); ss->cycWait += segClock() - tw0; }
 #endif
             if (!(bits & 2u)) {
                 if (sp == 0u) return any;
@@ -872,11 +882,11 @@ __device__ __forceinline__ bool blasWalk(const DevScene& S, uint32_t nodeOff, co
             }
         }
 #if SURF_SEG_TIMING
-        const unsigned long long tl0 = __builtin_readcyclecounter();
+        const unsigned long long tl0 = segClock();
 #endif
         const bool lh = leafWave<ANY>(tri, lf, cnt, o, d, depth, hu, hv, hprim);
 #if SURF_SEG_TIMING
-        if (ss) ss->cycLeaf += __builtin_readcyclecounter() - tl0;
+        if (ss) ss->cycLeaf += segClock() - tl0;
 #endif
         if (lh) {
             if (ANY) return true;
@@ -940,7 +950,7 @@ __device__ __forceinline__ bool traceWave(const DevScene& S, const TraceTables& 
         return any;
     }
 #if SURF_SEG_TIMING
-    unsigned long long t0 = __builtin_readcyclecounter();
+    unsigned long long t0 = segClock();
 #endif
     const uint32_t lane = __lane_id();
     /* lane k: instance k's object-space ray, 1/d and root-children ranges, kept
@@ -987,7 +997,7 @@ __device__ __forceinline__ bool traceWave(const DevScene& S, const TraceTables& 
         const V3 ok = xyz(q0);
         const V3 dk = xyz(q1);
 #if SURF_SEG_TIMING
-        if (ss) { const unsigned long long t1 = __builtin_readcyclecounter(); ss->cycInst += t1 - t0; t0 = t1; }
+        if (ss) { const unsigned long long t1 = segClock(); ss->cycInst += t1 - t0; t0 = t1; }
 #endif
         bool h;
         if (rcnt != 0u) {
@@ -999,7 +1009,7 @@ __device__ __forceinline__ bool traceWave(const DevScene& S, const TraceTables& 
                     : blasWalk<ANY, false>(S, nodeOff, tri, ok, dk, rk, dn, df, cn, cf, depth, hu, hv, hprim, rs, ss);
         }
 #if SURF_SEG_TIMING
-        if (ss) { const unsigned long long t1 = __builtin_readcyclecounter(); ss->cycLoop += t1 - t0; t0 = t1; }
+        if (ss) { const unsigned long long t1 = segClock(); ss->cycLoop += t1 - t0; t0 = t1; }
 #endif
         if (h) {
             if (ANY) return true;
@@ -1008,7 +1018,7 @@ __device__ __forceinline__ bool traceWave(const DevScene& S, const TraceTables& 
         }
     }
 #if SURF_SEG_TIMING
-    if (ss) ss->cycInst += __builtin_readcyclecounter() - t0;
+    if (ss) ss->cycInst += segClock() - t0;
 #endif
     return any;
 }
@@ -1688,7 +1698,7 @@ __global__ __launch_bounds__(64, SURF_COOP_WAVES) void k_tail_coop(DevScene S, P
         float depth = kFarAway, u = 0.0f, v = 0.0f;
         uint32_t inst = kUnset, prim = kUnset;
 #if SURF_SEG_TIMING
-        const unsigned long long c0 = __builtin_readcyclecounter();
+        const unsigned long long c0 = segClock();
 #endif
         const bool hit = traceWave<false>(S, Tt, xyz(o4), xyz(d4), depth, u, v, inst, prim, rstk, pro, ssp);
         (void)ssp;
@@ -1696,13 +1706,13 @@ __global__ __launch_bounds__(64, SURF_COOP_WAVES) void k_tail_coop(DevScene S, P
         ShadeOut r;
 #if SURF_SEG_TIMING
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        const unsigned long long c1 = __builtin_readcyclecounter();
+        const unsigned long long c1 = segClock();
 #endif
         shadePath(S, Tb, o4, d4, T4, make_float4(depth, u, v, u2f(prim)), hit ? inst : kUnset, maxSeg, zeroCutoff, r);
         if (lead && r.addRad) addRadiance(rad, f2u(o4.w), r.radd);
 #if SURF_SEG_TIMING
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        const unsigned long long c2 = __builtin_readcyclecounter();
+        const unsigned long long c2 = segClock();
 #endif
         nHit += r.hitGeom; nAcc += r.accd;
         if (r.shadow) {
@@ -1717,7 +1727,7 @@ __global__ __launch_bounds__(64, SURF_COOP_WAVES) void k_tail_coop(DevScene S, P
         }
 #if SURF_SEG_TIMING
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        const unsigned long long c3 = __builtin_readcyclecounter();
+        const unsigned long long c3 = segClock();
         cyc[0] += c1 - c0; cyc[1] += c2 - c1; cyc[2] += c3 - c2;
 #endif
         if (lead && r.capped) {

@@ -628,6 +628,8 @@ int runTail(surf_ctx* c) {
         std::fprintf(stderr, "[surf tail] extend per segment: instance prologues %.0f cycles, BLAS loops %.0f cycles, %.1f interior visits, "
                      "%.1f leaves, %.1f triangles, %.2f instances entered; %.0f cycles waiting for prefetched records, %.0f in leaves\n",
                      h[0] / ns, h[1] / ns, h[2] / ns, h[3] / ns, h[4] / ns, h[5] / ns, h[6] / ns, h[7] / ns);
+        const unsigned long long zero[8] = {};
+        SURF_CHECK(c, hipMemcpyToSymbol(HIP_SYMBOL(g_segStats), zero, sizeof(zero)));   /* per drain, like the counters */
     }
 #endif
     /* pool 0 is now empty: the next phase starts from regen's refill */
