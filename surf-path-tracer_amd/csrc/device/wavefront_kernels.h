@@ -928,7 +928,8 @@ __device__ __forceinline__ bool blasWave(const DevScene& S, const TraceInst& I, 
  * order, each applying the depth test to its ranges at its turn (with the
  * depth the earlier instances left), so a missed instance costs a few
  * readlanes instead of a serial transform, three divisions and a slab test. */
-constexpr uint32_t kProWords = 64u * 16u;   /* LDS prologue table of the wave traversal: 16 floats per lane */
+/* LDS prologue table of the wave traversal: 16 floats per instance (lane) */
+__device__ __forceinline__ uint32_t proWords(const DevScene& S) { return 16u * S.nInst; }
 template <bool ANY>
 __device__ __forceinline__ bool traceWave(const DevScene& S, const TraceTables& Tt, V3 o, V3 d, float& depth, float& hu,
                                           float& hv, uint32_t& hinst, uint32_t& hprim, float* rs, float4* pro, SegStats* ss = nullptr) {
@@ -1672,8 +1673,15 @@ __global__ __launch_bounds__(64, SURF_COOP_WAVES) void k_tail_coop(DevScene S, P
                                                   uint32_t* __restrict__ frameDone, uint32_t npx, uint32_t window, Counters* C,
                                                   uint32_t stackWords, uint32_t firstCounted) {
     extern __shared__ uint32_t lds[];
-    const TraceTables Tt = stageTrace(S, lds, stackWords + kProWords);
-    const ShadeTables Tb{S.inst, S.mats, S.lights};
+    const TraceTables Tt = stageTrace(S, lds, stackWords + proWords(S));
+    /* shading's instance / material / light tables in LDS too: a path's
+     * segments read them on its dependent chain (the drain's latency floor) */
+    uint32_t* const shw = lds + ((stackWords + proWords(S) + S.nInst * (uint32_t)((sizeof(TraceInst) + 4u) / 4u) + 3u) & ~3u);
+    DevInstance* const sInst = reinterpret_cast<DevInstance*>(shw);
+    DevMaterial* const sMat = reinterpret_cast<DevMaterial*>(sInst + S.nInst);
+    uint2* const sLights = reinterpret_cast<uint2*>(sMat + S.nMats);
+    stageTables(S, sInst, sMat, sLights);
+    const ShadeTables Tb{sInst, sMat, sLights};
     const uint32_t i = blockIdx.x;
     if (i >= n) return;
     const bool lead = threadIdx.x == 0;
@@ -1860,7 +1868,7 @@ __global__ __launch_bounds__(64) void k_trace_closest_coop(DevScene S, const flo
                                                            uint32_t n, float4* __restrict__ tuv, uint2* __restrict__ ip,
                                                            uint32_t stackWords) {
     extern __shared__ uint32_t lds[];
-    const TraceTables Tt = stageTrace(S, lds, stackWords + kProWords);
+    const TraceTables Tt = stageTrace(S, lds, stackWords + proWords(S));
     const uint32_t i = blockIdx.x;
     if (i >= n) return;
     float depth = kFarAway, u = 0.0f, v = 0.0f;
@@ -1877,7 +1885,7 @@ __global__ __launch_bounds__(64) void k_trace_any_coop(DevScene S, const float* 
                                                        const float* __restrict__ tmaxv, uint32_t n, uint8_t* __restrict__ occ,
                                                        uint32_t stackWords) {
     extern __shared__ uint32_t lds[];
-    const TraceTables Tt = stageTrace(S, lds, stackWords + kProWords);
+    const TraceTables Tt = stageTrace(S, lds, stackWords + proWords(S));
     const uint32_t i = blockIdx.x;
     if (i >= n) return;
     const V3 ro = mk3(o[3 * i], o[3 * i + 1], o[3 * i + 2]), rdir = mk3(d[3 * i], d[3 * i + 1], d[3 * i + 2]);

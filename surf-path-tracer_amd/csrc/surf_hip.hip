@@ -191,9 +191,15 @@ uint32_t recStackWords(const surf_ctx* c) { return c->stackDepth * 16u; }
 size_t rowsLds(const surf_ctx* c) {
     return ((size_t)4 * recStackWords(c) + kRowProWords) * sizeof(float) + (size_t)c->nInstances * (sizeof(TraceInst) + sizeof(uint32_t));
 }
-/* Dynamic LDS of the one-ray-per-wave kernels: the record stack, then the trace tables. */
+/* Dynamic LDS of the one-ray-per-wave kernels: the record stack, the prologue
+ * table (16 words per instance), then the trace tables; k_tail_coop adds the
+ * shading tables (coopTailLds). */
 size_t coopLds(const surf_ctx* c) {
-    return ((size_t)recStackWords(c) + kProWords) * sizeof(float) + (size_t)c->nInstances * (sizeof(TraceInst) + sizeof(uint32_t));
+    return ((size_t)recStackWords(c) + 16u * c->nInstances) * sizeof(float) + (size_t)c->nInstances * (sizeof(TraceInst) + sizeof(uint32_t));
+}
+size_t coopTailLds(const surf_ctx* c) {
+    return ((coopLds(c) + 15) & ~(size_t)15) + (size_t)c->nInstances * sizeof(DevInstance) + (size_t)c->nMaterials * sizeof(DevMaterial) +
+           (size_t)c->nLightsUp * sizeof(uint2);
 }
 size_t traversalLds(const surf_ctx* c, uint32_t block) {
     size_t b = (size_t)stackWords(c, block) * sizeof(uint32_t);
@@ -567,7 +573,7 @@ int runTail(surf_ctx* c) {
             break;
         }
         if (waveEligible(c) && cnt <= c->coopAll) {
-            hipLaunchKernelGGL(k_tail_coop, dim3(cnt), dim3(64), coopLds(c), c->stream, c->S, in, cnt, c->rad, c->frameDone,
+            hipLaunchKernelGGL(k_tail_coop, dim3(cnt), dim3(64), coopTailLds(c), c->stream, c->S, in, cnt, c->rad, c->frameDone,
                                c->npx, c->window, c->ctr, recStackWords(c), firstCounted);
             SURF_CHECK(c, hipGetLastError());
             c->stats.tail_survivors += cnt;
