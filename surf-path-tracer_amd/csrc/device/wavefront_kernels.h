@@ -957,8 +957,23 @@ __device__ __forceinline__ bool traceWave(const DevScene& S, const TraceTables& 
     /* lane k: instance k's object-space ray, 1/d and root-children ranges, kept
      * in the LDS prologue table (not in registers through the walk) */
     bool keep = false;
+    /* the lane traversal's instance cull (traceScene): an instance whose
+     * conservative world box the ray misses within [0, depth) holds no
+     * triangle that can yield an accepted hit -- here also for root-leaf
+     * instances (the room's walls), which otherwise cost a triangle test and
+     * its loads every segment */
+    const V3 rdw = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    const bool cullOk = finite3(o) && finite3(rdw);
     if (lane < nI) {
         const TraceInst& I = Tt.inst[Tt.order[lane]];
+        float w0 = -kFarAway, w1 = kFarAway;          /* world-box range; the full line when unusable */
+        if (cullOk && I.wlo.w != 0.0f) {
+            const float tx0 = (I.wlo.x - o.x) * rdw.x, tx1 = (I.whi.x - o.x) * rdw.x;
+            const float ty0 = (I.wlo.y - o.y) * rdw.y, ty1 = (I.whi.y - o.y) * rdw.y;
+            const float tz0 = (I.wlo.z - o.z) * rdw.z, tz1 = (I.whi.z - o.z) * rdw.z;
+            w0 = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fminf(tz0, tz1));
+            w1 = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
+        }
         V3 oo = mk3(rowDot(I.m0, o.x, o.y, o.z, 1.0f), rowDot(I.m1, o.x, o.y, o.z, 1.0f), rowDot(I.m2, o.x, o.y, o.z, 1.0f));
         if (!I.meta.z) oo = divs(oo, rowDot(I.m3, o.x, o.y, o.z, 1.0f));
         const V3 dd = mk3(rowDot(I.m0, d.x, d.y, d.z, 0.0f), rowDot(I.m1, d.x, d.y, d.z, 0.0f), rowDot(I.m2, d.x, d.y, d.z, 0.0f));
@@ -968,12 +983,13 @@ __device__ __forceinline__ bool traceWave(const DevScene& S, const TraceTables& 
         slabRange(I.r2, I.r3, oo, rd, b0, b1);
         /* candidates: a root child that misses at the entry depth misses at
          * every later (smaller) depth too; root leaves are always taken */
-        keep = f2u(I.r1.w) != 0u || slabHit(a0, a1, depth) != kFarAway || slabHit(b0, b1, depth) != kFarAway;
+        const bool wMiss = w1 < w0 || w1 < 0.0f || w0 >= depth;
+        keep = !wMiss && (f2u(I.r1.w) != 0u || slabHit(a0, a1, depth) != kFarAway || slabHit(b0, b1, depth) != kFarAway);
         float4* p = pro + 4u * lane;
         p[0] = make_float4(oo.x, oo.y, oo.z, a0);
         p[1] = make_float4(dd.x, dd.y, dd.z, a1);
         p[2] = make_float4(rd.x, rd.y, rd.z, b0);
-        p[3] = make_float4(b1, 0.0f, 0.0f, 0.0f);
+        p[3] = make_float4(b1, w0, w1, 0.0f);
     }
     unsigned long long cand = __ballot(keep);
     while (cand) {
@@ -986,6 +1002,7 @@ __device__ __forceinline__ bool traceWave(const DevScene& S, const TraceTables& 
         const uint32_t rlf = f2u(I.r0.w), rcnt = f2u(I.r1.w);
         const float4* pk = pro + 4u * k;                    /* one address for the wave: an LDS broadcast */
         const float4 q0 = pk[0], q1 = pk[1], q2 = pk[2], q3 = pk[3];
+        if (q3.z < q3.y || q3.z < 0.0f || q3.y >= depth) continue;   /* world-box cull at the current depth */
         float dn = 0.0f, df = 0.0f;
         uint32_t cn = nodeOff + rlf, cf = cn + 1u;
         if (rcnt == 0u) {
