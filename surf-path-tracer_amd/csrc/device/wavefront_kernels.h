@@ -283,10 +283,18 @@ __device__ __forceinline__ bool blasTrace(const DevScene& S, const TraceInst& I,
         float dn = boxDist<FIN>(r0, r1, o, rd, depth);
         float df = boxDist<FIN>(r2, r3, o, rd, depth);
         uint32_t cn = nodeOff + rlf, cf = cn + 1u;
-        if (dn > df) { const float t = dn; dn = df; df = t; const uint32_t c = cn; cn = cf; cf = c; }
-        if (dn == kFarAway) return false;
-        node = cn;
-        if (df != kFarAway) { *sp = cf; sp += stride; }
+        if (ANY) {
+            /* any-hit: the answer is an OR over every leaf the fixed-depth box
+             * tests admit, whatever the order -- left child first, no ordering */
+            if (dn == kFarAway && df == kFarAway) return false;
+            node = dn != kFarAway ? cn : cf;
+            if (dn != kFarAway && df != kFarAway) { *sp = cf; sp += stride; }
+        } else {
+            if (dn > df) { const float t = dn; dn = df; df = t; const uint32_t c = cn; cn = cf; cf = c; }
+            if (dn == kFarAway) return false;
+            node = cn;
+            if (df != kFarAway) { *sp = cf; sp += stride; }
+        }
     }
     for (;;) {
         const float4* nd = S.nodes + 4u * node;
@@ -306,6 +314,17 @@ __device__ __forceinline__ bool blasTrace(const DevScene& S, const TraceInst& I,
         float dn = boxDist<FIN>(q0, q1, o, rd, depth);
         float df = boxDist<FIN>(q2, q3, o, rd, depth);
         uint32_t cn = nodeOff + lf, cf = cn + 1u;
+        if (ANY) {
+            if (dn == kFarAway && df == kFarAway) {
+                if (sp == bottom) break;
+                sp -= stride;
+                node = *sp;
+            } else {
+                node = dn != kFarAway ? cn : cf;
+                if (dn != kFarAway && df != kFarAway) { *sp = cf; sp += stride; }
+            }
+            continue;
+        }
         if (dn > df) { const float t = dn; dn = df; df = t; const uint32_t c = cn; cn = cf; cf = c; }
         if (dn == kFarAway) {
             if (sp == bottom) break;
