@@ -707,6 +707,7 @@ __device__ __forceinline__ void waitLoadsAfter(float& v, float a, float b) {
  * records are read through a raw buffer resource at byte offset
  * 64 (nodeOff + lf) + laneOff. */
 typedef int surfI4 __attribute__((ext_vector_type(4)));
+template <bool ANY>
 __device__ __forceinline__ void walkInteriorFin(float& cur, uint32_t& row16, uint32_t& spb, uint32_t& lf, uint32_t& cnt,
                                                 float oA, float rdA, float depth, uint32_t nodeOff, surfI4 rsrc,
                                                 uint32_t laneOff, uint32_t stkLane) {
@@ -714,7 +715,85 @@ __device__ __forceinline__ void walkInteriorFin(float& cur, uint32_t& row16, uin
     uint32_t addr, idx, off;
     unsigned long long h, tt, g, a, save;
     const unsigned long long mask0 = 0x000000000000FFFFull, mask1 = 0x00000000FFFF0000ull;
-    asm volatile(
+    if (ANY) {
+        asm volatile(
+        "L_top_%=:\n\t"
+        "s_or_b32 %[idx], %[row], 13\n\t"
+        "v_readlane_b32 %[cnt], %[cur], %[idx]\n\t"
+        "s_or_b32 %[idx], %[row], 12\n\t"
+        "v_readlane_b32 %[lf], %[cur], %[idx]\n\t"
+        "s_cmp_lg_u32 %[cnt], 0\n\t"
+        "s_cbranch_scc1 L_exit_%=\n\t"
+        "s_add_u32 %[off], %[lf], %[noff]\n\t"
+        "s_lshl_b32 %[off], %[off], 6\n\t"
+        "buffer_load_dword %[nxt], %[loff], %[rsrc], %[off] offen\n\t"
+#if SURF_EXPOSE_LOAD   /* diagnostics: the record load's whole latency on the visit's path */
+        "s_waitcnt vmcnt(0)\n\t"
+#endif
+        "v_sub_f32 %[t], %[cur], %[oA]\n\t"
+        "v_mul_f32 %[t], %[t], %[rdA]\n\t"
+        "s_nop 1\n\t"
+        "v_min_f32_dpp %[t0a], %[t], %[t] quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_max_f32_dpp %[t1a], %[t], %[t] quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_max_f32_dpp %[m0], %[t0a], %[t0a] row_shr:4 row_mask:0xf bank_mask:0xf\n\t"
+        "v_min_f32_dpp %[m1], %[t1a], %[t1a] row_shr:4 row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_max_f32_dpp %[m0], %[t0a], %[m0] row_shr:2 row_mask:0xf bank_mask:0xf\n\t"
+        "v_min_f32_dpp %[m1], %[t1a], %[m1] row_shr:2 row_mask:0xf bank_mask:0xf\n\t"
+        /* lanes 4 / 10 of the row: box 0 / box 1 hit (m1 >= m0, m0 < depth, m1 > 0) */
+        "v_cmp_ge_f32_e64 %[h], %[m1], %[m0]\n\t"
+        "v_cmp_gt_f32_e64 %[tt], %[depth], %[m0]\n\t"
+        "s_and_b64 %[h], %[h], %[tt]\n\t"
+        "v_cmp_lt_f32_e64 %[tt], 0, %[m1]\n\t"
+        "s_and_b64 %[h], %[h], %[tt]\n\t"
+        /* any-hit: no near/far order (the answer is an OR over the admitted
+         * leaves): box 0 first when hit, box 1 pushed when both hit */
+        "s_lshr_b64 %[h], %[h], %[row]\n\t"
+        "s_bitcmp1_b64 %[h], 4\n\t"
+        "s_cbranch_scc1 L_h0_%=\n\t"
+        "s_bitcmp1_b64 %[h], 10\n\t"
+        "s_cbranch_scc0 L_pop_%=\n\t"
+        "s_mov_b32 %[row], 16\n\t"
+        "s_branch L_desc_%=\n"
+        "L_h0_%=:\n\t"
+        "s_mov_b32 %[row], 0\n\t"
+        "s_bitcmp1_b64 %[h], 10\n\t"
+        "s_cbranch_scc0 L_desc_%=\n\t"
+        "v_add_u32 %[addr], %[sp], %[stk]\n\t"
+        "s_mov_b64 %[save], exec\n\t"
+        "s_mov_b64 exec, %[mask1]\n\t"
+        "s_waitcnt vmcnt(0)\n\t"
+        "ds_write_b32 %[addr], %[nxt]\n\t"
+        "s_mov_b64 exec, %[save]\n\t"
+        "s_add_u32 %[sp], %[sp], 64\n"
+        "L_desc_%=:\n\t"
+        "s_waitcnt vmcnt(0)\n\t"
+        "v_mov_b32 %[cur], %[nxt]\n\t"
+        "s_branch L_top_%=\n"
+        /* both children missed: pop (every row reads the entry) or done */
+        "L_pop_%=:\n\t"
+        "s_waitcnt vmcnt(0)\n\t"
+        "s_cmp_eq_u32 %[sp], 0\n\t"
+        "s_cbranch_scc1 L_done_%=\n\t"
+        "s_sub_u32 %[sp], %[sp], 64\n\t"
+        "v_add_u32 %[addr], %[sp], %[stk]\n\t"
+        "ds_read_b32 %[cur], %[addr]\n\t"
+        "s_mov_b32 %[row], 0\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "s_branch L_top_%=\n"
+        "L_done_%=:\n\t"
+        "s_mov_b32 %[cnt], 0\n"
+        "L_exit_%=:"
+        : [cur] "+v"(cur), [row] "+s"(row16), [sp] "+s"(spb), [lf] "=&s"(lf), [cnt] "=&s"(cnt), [nxt] "=&v"(nxt),
+          [t] "=&v"(t), [t0a] "=&v"(t0a), [t1a] "=&v"(t1a), [m0] "=&v"(m0), [m1] "=&v"(m1), [mp] "=&v"(mp),
+          [addr] "=&v"(addr), [idx] "=&s"(idx), [off] "=&s"(off), [h] "=&s"(h), [tt] "=&s"(tt), [g] "=&s"(g),
+          [a] "=&s"(a), [save] "=&s"(save)
+        : [oA] "v"(oA), [rdA] "v"(rdA), [depth] "s"(depth), [noff] "s"(nodeOff), [rsrc] "s"(rsrc), [loff] "v"(laneOff),
+          [stk] "v"(stkLane), [mask0] "s"(mask0), [mask1] "s"(mask1)
+        : "memory", "scc");
+    } else {
+        asm volatile(
         "L_top_%=:\n\t"
         "s_or_b32 %[idx], %[row], 13\n\t"
         "v_readlane_b32 %[cnt], %[cur], %[idx]\n\t"
@@ -808,6 +887,7 @@ __device__ __forceinline__ void walkInteriorFin(float& cur, uint32_t& row16, uin
         : [oA] "v"(oA), [rdA] "v"(rdA), [depth] "s"(depth), [noff] "s"(nodeOff), [rsrc] "s"(rsrc), [loff] "v"(laneOff),
           [stk] "v"(stkLane), [mask0] "s"(mask0), [mask1] "s"(mask1)
         : "memory", "scc");
+    }
 }
 
 /* The DFS below one BLAS root (blasTrace's loop), from the root's children:
@@ -853,7 +933,7 @@ __device__ __forceinline__ bool blasWalk(const DevScene& S, uint32_t nodeOff, co
 #if !SURF_PAD_VALU && !SURF_PAD_SALU   /* (timing builds count no interior visits on this path) */
         if (FIN) {
             uint32_t row16 = 16u * row, spb = 64u * sp;
-            walkInteriorFin(cur, row16, spb, lf, cnt, oA, rdA, depth, nodeOff, rsrc, laneOff, stkLane);
+            walkInteriorFin<ANY>(cur, row16, spb, lf, cnt, oA, rdA, depth, nodeOff, rsrc, laneOff, stkLane);
             row = row16 >> 4;
             sp = spb >> 6;
             if (cnt == 0u) return any;
