@@ -717,15 +717,15 @@ __device__ __forceinline__ void walkInteriorFin(float& cur, uint32_t& row16, uin
     const unsigned long long mask0 = 0x000000000000FFFFull, mask1 = 0x00000000FFFF0000ull;
     if (ANY) {
         asm volatile(
-        "L_top_%=:\n\t"
+        /* lf / cnt of the current node are read where cur is set (entry, descend, pop) */
         "s_or_b32 %[idx], %[row], 13\n\t"
         "v_readlane_b32 %[cnt], %[cur], %[idx]\n\t"
         "s_or_b32 %[idx], %[row], 12\n\t"
-        "v_readlane_b32 %[lf], %[cur], %[idx]\n\t"
+        "v_readlane_b32 %[lf], %[cur], %[idx]\n"
+        "L_top_%=:\n\t"
         "s_cmp_lg_u32 %[cnt], 0\n\t"
         "s_cbranch_scc1 L_exit_%=\n\t"
-        "s_add_u32 %[off], %[lf], %[noff]\n\t"
-        "s_lshl_b32 %[off], %[off], 6\n\t"
+        "s_lshl_b32 %[off], %[lf], 6\n\t"
         "buffer_load_dword %[nxt], %[loff], %[rsrc], %[off] offen\n\t"
 #if SURF_EXPOSE_LOAD   /* diagnostics: the record load's whole latency on the visit's path */
         "s_waitcnt vmcnt(0)\n\t"
@@ -768,7 +768,11 @@ __device__ __forceinline__ void walkInteriorFin(float& cur, uint32_t& row16, uin
         "s_mov_b64 exec, %[save]\n\t"
         "s_add_u32 %[sp], %[sp], 64\n"
         "L_desc_%=:\n\t"
+        "s_or_b32 %[idx], %[row], 13\n\t"
         "s_waitcnt vmcnt(0)\n\t"
+        "v_readlane_b32 %[cnt], %[nxt], %[idx]\n\t"
+        "s_or_b32 %[idx], %[row], 12\n\t"
+        "v_readlane_b32 %[lf], %[nxt], %[idx]\n\t"
         "v_mov_b32 %[cur], %[nxt]\n\t"
         "s_branch L_top_%=\n"
         /* both children missed: pop (every row reads the entry) or done */
@@ -781,6 +785,8 @@ __device__ __forceinline__ void walkInteriorFin(float& cur, uint32_t& row16, uin
         "ds_read_b32 %[cur], %[addr]\n\t"
         "s_mov_b32 %[row], 0\n\t"
         "s_waitcnt lgkmcnt(0)\n\t"
+        "v_readlane_b32 %[cnt], %[cur], 13\n\t"
+        "v_readlane_b32 %[lf], %[cur], 12\n\t"
         "s_branch L_top_%=\n"
         "L_done_%=:\n\t"
         "s_mov_b32 %[cnt], 0\n"
@@ -794,15 +800,15 @@ __device__ __forceinline__ void walkInteriorFin(float& cur, uint32_t& row16, uin
         : "memory", "scc");
     } else {
         asm volatile(
-        "L_top_%=:\n\t"
+        /* lf / cnt of the current node are read where cur is set (entry, descend, pop) */
         "s_or_b32 %[idx], %[row], 13\n\t"
         "v_readlane_b32 %[cnt], %[cur], %[idx]\n\t"
         "s_or_b32 %[idx], %[row], 12\n\t"
-        "v_readlane_b32 %[lf], %[cur], %[idx]\n\t"
+        "v_readlane_b32 %[lf], %[cur], %[idx]\n"
+        "L_top_%=:\n\t"
         "s_cmp_lg_u32 %[cnt], 0\n\t"
         "s_cbranch_scc1 L_exit_%=\n\t"
-        "s_add_u32 %[off], %[lf], %[noff]\n\t"
-        "s_lshl_b32 %[off], %[off], 6\n\t"
+        "s_lshl_b32 %[off], %[lf], 6\n\t"
         "buffer_load_dword %[nxt], %[loff], %[rsrc], %[off] offen\n\t"
 #if SURF_EXPOSE_LOAD   /* diagnostics: the record load's whole latency on the visit's path */
         "s_waitcnt vmcnt(0)\n\t"
@@ -828,42 +834,34 @@ __device__ __forceinline__ void walkInteriorFin(float& cur, uint32_t& row16, uin
         "v_mov_b32_dpp %[mp], %[m0] row_shr:6 row_mask:0xf bank_mask:0xf\n\t"
         "v_cmp_gt_f32_e64 %[g], %[mp], %[m0]\n\t"
         "s_lshr_b64 %[h], %[h], %[row]\n\t"
-        "s_lshr_b64 %[g], %[g], %[row]\n\t"
-        /* bit 10 of a: swap = hit1 && (gt || !hit0) */
-        "s_lshl_b64 %[a], %[h], 6\n\t"
-        "s_not_b64 %[a], %[a]\n\t"
-        "s_or_b64 %[a], %[a], %[g]\n\t"
-        "s_and_b64 %[a], %[a], %[h]\n\t"
-        "s_bitcmp1_b64 %[a], 10\n\t"
-        "s_cbranch_scc1 L_sw_%=\n\t"
-        /* near = box 0 (row 0 of nxt): taken if hit0; box 1 pushed if hit1 */
-        "s_bitcmp1_b64 %[h], 4\n\t"
+        /* bits 4 / 10 of a: box 0 / box 1 hit.  One hit: that child, nothing
+         * pushed.  Both: the nearer (swap when m0 of box 0 > m0 of box 1, as
+         * blasTrace's dn > df), the other pushed.  None: pop. */
+        "s_and_b64 %[a], %[h], 0x410\n\t"
         "s_cbranch_scc0 L_pop_%=\n\t"
-        "s_mov_b32 %[row], 0\n\t"
-        "s_bitcmp1_b64 %[h], 10\n\t"
-        "s_cbranch_scc0 L_desc_%=\n\t"
-        "v_add_u32 %[addr], %[sp], %[stk]\n\t"
-        "s_mov_b64 %[save], exec\n\t"
-        "s_mov_b64 exec, %[mask1]\n\t"
-        "s_waitcnt vmcnt(0)\n\t"
-        "ds_write_b32 %[addr], %[nxt]\n\t"
-        "s_mov_b64 exec, %[save]\n\t"
-        "s_add_u32 %[sp], %[sp], 64\n\t"
+        "s_cmp_eq_u64 %[a], 0x410\n\t"
+        "s_cbranch_scc1 L_both_%=\n\t"
+        "s_cmp_eq_u64 %[a], 0x400\n\t"
+        "s_cselect_b32 %[row], 16, 0\n\t"
         "s_branch L_desc_%=\n"
-        /* near = box 1 (row 1, hit); box 0 pushed if hit0 */
-        "L_sw_%=:\n\t"
-        "s_mov_b32 %[row], 16\n\t"
-        "s_bitcmp1_b64 %[h], 4\n\t"
-        "s_cbranch_scc0 L_desc_%=\n\t"
+        "L_both_%=:\n\t"
+        "s_lshr_b64 %[g], %[g], %[row]\n\t"
         "v_add_u32 %[addr], %[sp], %[stk]\n\t"
+        "s_bitcmp1_b64 %[g], 10\n\t"
+        "s_cselect_b32 %[row], 16, 0\n\t"
+        "s_cselect_b64 %[a], %[mask0], %[mask1]\n\t"
         "s_mov_b64 %[save], exec\n\t"
-        "s_mov_b64 exec, %[mask0]\n\t"
+        "s_mov_b64 exec, %[a]\n\t"
         "s_waitcnt vmcnt(0)\n\t"
         "ds_write_b32 %[addr], %[nxt]\n\t"
         "s_mov_b64 exec, %[save]\n\t"
         "s_add_u32 %[sp], %[sp], 64\n"
         "L_desc_%=:\n\t"
+        "s_or_b32 %[idx], %[row], 13\n\t"
         "s_waitcnt vmcnt(0)\n\t"
+        "v_readlane_b32 %[cnt], %[nxt], %[idx]\n\t"
+        "s_or_b32 %[idx], %[row], 12\n\t"
+        "v_readlane_b32 %[lf], %[nxt], %[idx]\n\t"
         "v_mov_b32 %[cur], %[nxt]\n\t"
         "s_branch L_top_%=\n"
         /* both children missed: pop (every row reads the entry) or done */
@@ -876,6 +874,8 @@ __device__ __forceinline__ void walkInteriorFin(float& cur, uint32_t& row16, uin
         "ds_read_b32 %[cur], %[addr]\n\t"
         "s_mov_b32 %[row], 0\n\t"
         "s_waitcnt lgkmcnt(0)\n\t"
+        "v_readlane_b32 %[cnt], %[cur], 13\n\t"
+        "v_readlane_b32 %[lf], %[cur], 12\n\t"
         "s_branch L_top_%=\n"
         "L_done_%=:\n\t"
         "s_mov_b32 %[cnt], 0\n"
@@ -921,7 +921,7 @@ __device__ __forceinline__ bool blasWalk(const DevScene& S, uint32_t nodeOff, co
 #endif
     /* walkInteriorFin's operands: node records as a raw buffer (gfx9 dword 3),
      * this lane's byte offset in a record pair, its LDS stack column */
-    const uintptr_t nb = reinterpret_cast<uintptr_t>(S.nodes);
+    const uintptr_t nb = reinterpret_cast<uintptr_t>(S.nodes + 4u * (size_t)nodeOff);   /* this BLAS's records */
     const surfI4 rsrc = {(int)(uint32_t)nb, (int)(uint32_t)(nb >> 32), -1, 0x00020000};
     const uint32_t laneOff = 64u * half + 4u * dw;
     const uint32_t stkLane = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) float*)rs) + 4u * l16;
