@@ -1300,21 +1300,25 @@ __global__ __launch_bounds__(kBlock, SURF_TRACE_WAVES) void k_extend(DevScene S,
 }
 
 /* randomOnHemisphereCosineWeighted, surf_math.cpp:116-134 (retry loop for R.N == 0) */
+/* One try of the loop body (two draws); false when R.N == 0 (retry). */
+__device__ __forceinline__ bool cosineTry(uint32_t& seed, V3 n, V3& out) {
+    const float r0 = rndF(seed), r1 = rndF(seed);
+    const float r = sqrtf(r0);
+    const float theta = k2Pi * r1;
+    float sn, cs;
+    gSinCosf(theta, sn, cs);
+    const V3 dir = mk3(r * cs, r * sn, sqrtf(1.0f - r0));
+    const float xMax = 1.0f - kEps;
+    const V3 tmp = (fabsf(n.x) > xMax) ? mk3(0.0f, 1.0f, 0.0f) : mk3(1.0f, 0.0f, 0.0f);
+    const V3 B = normalize(cross(n, tmp));
+    const V3 T = cross(B, n);
+    out = add(add(lscl(dir.x, T), lscl(dir.y, B)), lscl(dir.z, n));
+    return !(dot(out, n) == 0.0f);
+}
 __device__ __forceinline__ V3 cosineSample(uint32_t& seed, V3 n) {
-    for (;;) {
-        const float r0 = rndF(seed), r1 = rndF(seed);
-        const float r = sqrtf(r0);
-        const float theta = k2Pi * r1;
-        float sn, cs;
-        gSinCosf(theta, sn, cs);
-        const V3 dir = mk3(r * cs, r * sn, sqrtf(1.0f - r0));
-        const float xMax = 1.0f - kEps;
-        const V3 tmp = (fabsf(n.x) > xMax) ? mk3(0.0f, 1.0f, 0.0f) : mk3(1.0f, 0.0f, 0.0f);
-        const V3 B = normalize(cross(n, tmp));
-        const V3 T = cross(B, n);
-        const V3 out = add(add(lscl(dir.x, T), lscl(dir.y, B)), lscl(dir.z, n));
-        if (!(dot(out, n) == 0.0f)) return out;
-    }
+    V3 out;
+    while (!cosineTry(seed, n, out)) {}
+    return out;
 }
 
 __device__ __forceinline__ void addRadiance(float4* rad, uint32_t sid, V3 c) {
@@ -1354,6 +1358,52 @@ __device__ __forceinline__ void stageTables(const DevScene& S, DevInstance* sIns
     __syncthreads();
 }
 
+/* Next-event estimation of one diffuse bounce (Scene::sampleLights +
+ * Instance::samplePoint, scene.h:53, bvh.cpp:533-552; renderer.cpp:384-415):
+ * four draws from seed; sets r's shadow ray when the light faces P. */
+__device__ __forceinline__ void sampleNEE(const DevScene& S, const ShadeTables& Tb, uint32_t& seed, V3 P, V3 N, V3 T, V3 brdf,
+                                          uint32_t sid, ShadeOut& r) {
+    /* Scene::sampleLights + Instance::samplePoint (scene.h:53, bvh.cpp:533-552) */
+    const uint32_t li = rndRangeU(seed, 0u, S.nLights);
+    const uint2 L = Tb.lights[li];
+    const DevInstance& LI = Tb.inst[L.x];
+    const float lu = rndRange(seed, 0.0f, 1.0f);
+    const float lv = rndRange(seed, 0.0f, 1.0f - lu);
+    const uint32_t ti = rndRangeU(seed, 0u, L.y);
+    const float4* tv = S.verts + 4u * (LI.triOffset + ti);
+    const float4* tn = S.normals + 3u * (LI.triOffset + ti);
+    const float lw = (1.0f - lu) - lv;
+    const V3 lp = add(add(lscl(lu, xyz(tv[0])), lscl(lv, xyz(tv[2]))), lscl(lw, xyz(tv[1])));
+    const V3 ln = add(add(lscl(lu, xyz(tn[0])), lscl(lv, xyz(tn[2]))), lscl(lw, xyz(tn[1])));
+    const float* LM = LI.M;
+    V3 Pl = mk3(mrow(LM, 0, lp.x, lp.y, lp.z, 1.0f), mrow(LM, 1, lp.x, lp.y, lp.z, 1.0f), mrow(LM, 2, lp.x, lp.y, lp.z, 1.0f));
+    if (!LI.affine) Pl = divs(Pl, mrow(LM, 3, lp.x, lp.y, lp.z, 1.0f));   /* w == 1 exactly when affine */
+    const V3 LN = normalize(mk3(mrow(LM, 0, ln.x, ln.y, ln.z, 0.0f), mrow(LM, 1, ln.x, ln.y, ln.z, 0.0f),
+                                mrow(LM, 2, ln.x, ln.y, ln.z, 0.0f)));
+    const V3 IL = sub(Pl, P);
+    const V3 Ld = normalize(IL);
+    const V3 SO = add(P, lscl(kEps, Ld));
+    const float srDepth = sqrtf(dot(IL, IL)) - 2.0f * kEps;
+    const float falloff = 1.0f / dot(IL, IL);
+    const float cosO = dot(N, Ld);
+    const float cosL = dot(LN, lscl(-1.0f, Ld));
+    if (cosO > 0.0f && cosL > 0.0f) {
+        const float SA = (cosL * LI.area) * falloff;
+        const float lightPdf = 1.0f / SA;
+        const float invPdf = 1.0f / lightPdf;
+        const DevMaterial& lm = Tb.mats[LI.material];
+        const V3 le = lscl(lm.emit, ld3(lm.ec));
+        const V3 Lc = scl(scl(mul(scl(le, invPdf), brdf), cosO), (float)S.nLights);
+        const V3 contrib = mul(T, Lc);
+        r.shadow = true;
+        r.light = li;
+        r.so = make_float4(SO.x, SO.y, SO.z, srDepth);
+        r.sd = make_float4(Ld.x, Ld.y, Ld.z, u2f(sid));
+        r.sc = make_float4(contrib.x, contrib.y, contrib.z, 0.0f);
+    }
+}
+
+template <bool SPEC = false>
 __device__ __forceinline__ void shadePath(const DevScene& S, const ShadeTables& Tb, float4 o4, float4 d4, float4 T4, float4 h4,
                                           uint32_t inst, uint32_t maxSeg, uint32_t zeroCutoff, ShadeOut& r) {
     r.cont = r.shadow = r.hitGeom = r.accd = r.capped = r.addRad = false;
@@ -1435,50 +1485,32 @@ __device__ __forceinline__ void shadePath(const DevScene& S, const ShadeTables& 
         T = mul(T, mul(ld3(m.albedo), medium));
         nextMedium = mustRefract ? !inMedium : inMedium;
     } else {
-        R = cosineSample(seed, N);
+        const V3 brdf = scl(ld3(m.albedo), kInvPi);
+        if (SPEC) {
+            /* the light sample depends on the cosine sample only through the RNG
+             * state after its draws: formed from the state after the first try
+             * (almost always accepted) beside the cosine sample, so the two
+             * dependency chains interleave; formed again after a retry */
+            uint32_t sC = seed;
+            V3 R1;
+            const bool ok1 = cosineTry(sC, N, R1);
+            uint32_t sL = sC;
+            if (S.nLights > 0u) sampleNEE(S, Tb, sL, P, N, T, brdf, sid, r);
+            if (ok1) {
+                R = R1;
+            } else {
+                R = cosineSample(sC, N);
+                sL = sC;
+                r.shadow = false;
+                if (S.nLights > 0u) sampleNEE(S, Tb, sL, P, N, T, brdf, sid, r);
+            }
+            seed = sL;
+        } else {
+            R = cosineSample(seed, N);
+            if (S.nLights > 0u) sampleNEE(S, Tb, seed, P, N, T, brdf, sid, r);
+        }
         const float cosT = dot(N, R);
         const float pdf = cosT * kInvPi;
-        const V3 brdf = scl(ld3(m.albedo), kInvPi);
-        if (S.nLights > 0u) {
-            /* Scene::sampleLights + Instance::samplePoint (scene.h:53, bvh.cpp:533-552) */
-            const uint32_t li = rndRangeU(seed, 0u, S.nLights);
-            const uint2 L = Tb.lights[li];
-            const DevInstance& LI = Tb.inst[L.x];
-            const float lu = rndRange(seed, 0.0f, 1.0f);
-            const float lv = rndRange(seed, 0.0f, 1.0f - lu);
-            const uint32_t ti = rndRangeU(seed, 0u, L.y);
-            const float4* tv = S.verts + 4u * (LI.triOffset + ti);
-            const float4* tn = S.normals + 3u * (LI.triOffset + ti);
-            const float lw = (1.0f - lu) - lv;
-            const V3 lp = add(add(lscl(lu, xyz(tv[0])), lscl(lv, xyz(tv[2]))), lscl(lw, xyz(tv[1])));
-            const V3 ln = add(add(lscl(lu, xyz(tn[0])), lscl(lv, xyz(tn[2]))), lscl(lw, xyz(tn[1])));
-            const float* LM = LI.M;
-            V3 Pl = mk3(mrow(LM, 0, lp.x, lp.y, lp.z, 1.0f), mrow(LM, 1, lp.x, lp.y, lp.z, 1.0f), mrow(LM, 2, lp.x, lp.y, lp.z, 1.0f));
-            if (!LI.affine) Pl = divs(Pl, mrow(LM, 3, lp.x, lp.y, lp.z, 1.0f));   /* w == 1 exactly when affine */
-            const V3 LN = normalize(mk3(mrow(LM, 0, ln.x, ln.y, ln.z, 0.0f), mrow(LM, 1, ln.x, ln.y, ln.z, 0.0f),
-                                        mrow(LM, 2, ln.x, ln.y, ln.z, 0.0f)));
-            const V3 IL = sub(Pl, P);
-            const V3 Ld = normalize(IL);
-            const V3 SO = add(P, lscl(kEps, Ld));
-            const float srDepth = sqrtf(dot(IL, IL)) - 2.0f * kEps;
-            const float falloff = 1.0f / dot(IL, IL);
-            const float cosO = dot(N, Ld);
-            const float cosL = dot(LN, lscl(-1.0f, Ld));
-            if (cosO > 0.0f && cosL > 0.0f) {
-                const float SA = (cosL * LI.area) * falloff;
-                const float lightPdf = 1.0f / SA;
-                const float invPdf = 1.0f / lightPdf;
-                const DevMaterial& lm = Tb.mats[LI.material];
-                const V3 le = lscl(lm.emit, ld3(lm.ec));
-                const V3 Lc = scl(scl(mul(scl(le, invPdf), brdf), cosO), (float)S.nLights);
-                const V3 contrib = mul(T, Lc);
-                r.shadow = true;
-                r.light = li;
-                r.so = make_float4(SO.x, SO.y, SO.z, srDepth);
-                r.sd = make_float4(Ld.x, Ld.y, Ld.z, u2f(sid));
-                r.sc = make_float4(contrib.x, contrib.y, contrib.z, 0.0f);
-            }
-        }
         const float pm = tmax(T.x, tmax(T.y, T.z));
         const float pr = pm < 0.0f ? 0.0f : (pm > 1.0f ? 1.0f : pm);   /* clamp(max(T), 0, 1) */
         if (pr < rndF(seed)) alive = false;
@@ -1832,7 +1864,7 @@ __global__ __launch_bounds__(64, SURF_COOP_WAVES) void k_tail_coop(DevScene S, P
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         const unsigned long long c1 = segClock();
 #endif
-        shadePath(S, Tb, o4, d4, T4, make_float4(depth, u, v, u2f(prim)), hit ? inst : kUnset, maxSeg, zeroCutoff, r);
+        shadePath<true>(S, Tb, o4, d4, T4, make_float4(depth, u, v, u2f(prim)), hit ? inst : kUnset, maxSeg, zeroCutoff, r);
         if (lead && r.addRad) addRadiance(rad, f2u(o4.w), r.radd);
 #if SURF_SEG_TIMING
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
