@@ -182,10 +182,17 @@ def main():
     W, H, SPP, MAXSEG = wl["width"], wl["height"], wl["spp"], wl["max_segments"]
 
     dist_on = world > 1
+    # SURF_BENCH_BACKEND=gloo: rehearsal of the N > 1 path on fewer GPUs than
+    # ranks (rank -> device LOCAL_RANK % device count, gather through host
+    # memory); the measured configuration is always nccl (RCCL), one GPU per rank
+    backend = os.environ.get("SURF_BENCH_BACKEND", "nccl")
     if dist_on:
+        if backend == "gloo":
+            local = local % max(torch.cuda.device_count(), 1)
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", init_method="env://")
+        dist.init_process_group(backend, init_method="env://")
     dev = torch.device("cuda", local)
+    coll_dev = dev if backend == "nccl" else torch.device("cpu")
     torch.cuda.init()
 
     surf_amd.load()
@@ -203,7 +210,7 @@ def main():
     if dist_on:
         from surf_amd.dist import RowGather
         acc_dev = torch.empty((rows, W, 4), dtype=torch.float32, device=dev)
-        gather = RowGather(W, H, world, rank, args.row_block, dev)
+        gather = RowGather(W, H, world, rank, args.row_block, coll_dev)
 
     def step(i):
         """One complete render: frames [i*SPP, (i+1)*SPP), drained; N > 1: one RCCL gather."""
@@ -212,7 +219,7 @@ def main():
         r.synchronize()                   # every frame of the render accumulated
         if dist_on:
             r.copy_accumulator_to(acc_dev.data_ptr())
-            gather.gather(acc_dev)
+            gather.gather(acc_dev if coll_dev == dev else acc_dev.to(coll_dev))
 
     for w in range(args.warmup):
         step(w)
@@ -231,10 +238,10 @@ def main():
     st = r.stats()                        # the last render's counts (cleared per step)
     ev = {k: st[k] for k in ("n_ext", "n_hit", "n_cont", "n_shadow", "n_acc", "n_unocc", "iterations", "tail_paths")}
     if dist_on:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        t = torch.tensor([dt], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-        evt = torch.tensor([ev[k] for k in ev], dtype=torch.float64, device=dev)
+        evt = torch.tensor([ev[k] for k in ev], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(evt)
         ev = {k: int(v) for k, v in zip(ev, evt.tolist())}
     gpu_acc = r.accumulator() if (rank == 0 and world == 1 and not args.no_cpu) else None
