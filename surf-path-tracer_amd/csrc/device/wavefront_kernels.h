@@ -95,6 +95,7 @@ struct DevScene {
     uint32_t nInst, nMats;
     uint32_t tlasLeafCount;   /* TLAS root is a leaf with this many instances (0: general TLAS) */
     uint32_t finiteBoxes;     /* every BLAS node box is finite: slabFinite is exact */
+    uint32_t nodes4G;         /* every BLAS-local record offset (64 B each) fits 32 bits: the asm wave walk's buffer offsets */
     uint32_t bgType;
     float bgColor[3], bgA[3], bgB[3];
     float cellLo[3], cellScale[3];   /* ray-order cells: the TLAS root box split in 2 per axis (scale 0: one cell) */
@@ -931,7 +932,7 @@ __device__ __forceinline__ bool blasWalk(const DevScene& S, uint32_t nodeOff, co
          * (no loop-carried copies of them per visit) */
         uint32_t lf, cnt;
 #if !SURF_PAD_VALU && !SURF_PAD_SALU   /* (timing builds count no interior visits on this path) */
-        if (FIN) {
+        if (FIN && S.nodes4G) {
             uint32_t row16 = 16u * row, spb = 64u * sp;
             walkInteriorFin<ANY>(cur, row16, spb, lf, cnt, oA, rdA, depth, nodeOff, rsrc, laneOff, stkLane);
             row = row16 >> 4;

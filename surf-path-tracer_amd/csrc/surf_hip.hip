@@ -1035,6 +1035,10 @@ int surf_upload_scene(surf_ctx* c, const surf_scene_desc* d) {
         !d->background || d->material_count == 0 || d->blas_node_count == 0 || d->blas_index_count == 0 ||
         (d->light_count && !d->lights))
         return fail(c, SURF_ERR_INVALID, "incomplete scene descriptor");
+    /* the kernels index records with 32-bit element offsets (16 floats per node,
+     * 12 per BLAS index slot, 16 per triangle record) */
+    if (d->blas_node_count >= (1u << 28) || d->blas_index_count >= (1u << 28) || d->triangle_count >= (1u << 28))
+        return fail(c, SURF_ERR_LIMIT, "scene larger than 2^28 BVH nodes / index slots / triangles");
     SURF_CHECK(c, hipSetDevice(c->device));
     int rc0 = endStream(c);
     if (rc0) return rc0;
@@ -1144,6 +1148,7 @@ int surf_upload_scene(surf_ctx* c, const surf_scene_desc* d) {
     S.nLights = d->light_count;
     S.nInst = d->instance_count;
     S.nMats = d->material_count;
+    S.nodes4G = d->blas_node_count < (1u << 26) ? 1u : 0u;
     S.finiteBoxes = 1u;
     for (const float4& q : nodes)
         if (!(std::fabs(q.x) <= FLT_MAX && std::fabs(q.y) <= FLT_MAX && std::fabs(q.z) <= FLT_MAX)) { S.finiteBoxes = 0u; break; }
