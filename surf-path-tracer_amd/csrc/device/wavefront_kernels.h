@@ -356,6 +356,9 @@ __device__ __forceinline__ bool instanceTrace(const DevScene& S, const TraceInst
     V3 oo = mk3(rowDot(I.m0, o.x, o.y, o.z, 1.0f), rowDot(I.m1, o.x, o.y, o.z, 1.0f), rowDot(I.m2, o.x, o.y, o.z, 1.0f));
     if (!I.meta.z) oo = divs(oo, rowDot(I.m3, o.x, o.y, o.z, 1.0f));
     const V3 dd = mk3(rowDot(I.m0, d.x, d.y, d.z, 0.0f), rowDot(I.m1, d.x, d.y, d.z, 0.0f), rowDot(I.m2, d.x, d.y, d.z, 0.0f));
+    /* a root leaf (the room's walls) needs no 1/d: its triangles are tested directly */
+    if (f2u(I.r1.w) != 0u)
+        return leafTestUniform<ANY>(S.tris + 3u * I.meta.y, f2u(I.r0.w), f2u(I.r1.w), oo, dd, depth, hu, hv, hprim);
     const V3 rd = mk3(1.0f / dd.x, 1.0f / dd.y, 1.0f / dd.z);
     /* S.finiteBoxes: every BLAS box is finite (checked at upload) */
     if (S.finiteBoxes && finite3(oo) && finite3(rd))
