@@ -1921,6 +1921,169 @@ __global__ __launch_bounds__(64, SURF_COOP_WAVES) void k_tail_coop(DevScene S, P
     }
 }
 
+/* Cooperative drain with partner waves (k_tail_pair): workgroups of two waves,
+ * each wave running paths from the drain's queue (Counters::rowNext) one at a
+ * time with k_tail_coop's per-segment code.  When the queue is empty and a
+ * wave's path ends while its sibling still runs one, the idle wave becomes the
+ * sibling's shadow tracer: the sibling posts segment i's shadow ray to an LDS
+ * mailbox and extends segment i+1 while the partner runs the any-hit walk; the
+ * answer is collected after that extension, before segment i+1 is shaded, so
+ * the path's radiance is added in the reference's order (renderer.cpp:415-444:
+ * NEE contribution of bounce i, then whatever bounce i+1 adds).  The last
+ * paths of a drain -- its latency floor -- then pay max(extend, any-hit) +
+ * shade per segment instead of the sum.  Same device functions, same results. */
+struct PairBox {
+    uint32_t run[2];      /* wave w is in its path loop */
+    uint32_t help[2];     /* help[w]: the sibling traces wave w's shadow rays */
+    uint32_t post[2];     /* shadow rays wave w has posted */
+    uint32_t done[2];     /* ... of which the sibling has answered */
+    uint32_t occ[2];      /* the last answer */
+    float4 so[2], sd[2];  /* the posted ray: (origin, tmax), (dir, sid) */
+    float4 sc[2];         /* its contribution T*Ld if unoccluded (read back by the poster) */
+};
+
+__device__ __forceinline__ uint32_t ldsLoadAcq(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void ldsStoreRel(uint32_t* p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+/* Every wave counts its paths' events and adds them once at exit. */
+struct PairCounts { uint32_t ext, hit, cont, sh, acc, un, paths; };
+
+/* One path of the queue on the calling wave (w); its shadow rays go to the
+ * sibling while box.help[w] is set. */
+__device__ __forceinline__ void pairPath(const DevScene& S, const TraceTables& Tt, const ShadeTables& Tb, PairBox& box, uint32_t w,
+                                         float4 o4, float4 d4, float4 T4, float4* __restrict__ rad, uint32_t* __restrict__ frameDone,
+                                         uint32_t npx, uint32_t window, Counters* C, float* rstk, float4* pro, bool lead,
+                                         uint32_t& posted, PairCounts& pc) {
+    const uint32_t maxSeg = C->maxSeg, zeroCutoff = C->zeroCutoff;
+    const uint32_t slot = f2u(o4.w) / npx;
+    bool pend = false;                     /* a posted shadow ray awaits its answer */
+    for (;;) {
+        float depth = kFarAway, u = 0.0f, v = 0.0f;
+        uint32_t inst = kUnset, prim = kUnset;
+        const bool hit = traceWave<false>(S, Tt, xyz(o4), xyz(d4), depth, u, v, inst, prim, rstk, pro);
+        ++pc.ext;
+        if (pend) {
+            while (ldsLoadAcq(&box.done[w]) != posted) __builtin_amdgcn_s_sleep(1);
+            if (!box.occ[w]) {
+                if (lead) addRadiance(rad, f2u(box.sd[w].w), xyz(box.sc[w]));
+                ++pc.un; ++pc.acc;
+            }
+            pend = false;
+        }
+        ShadeOut r;
+        shadePath<true>(S, Tb, o4, d4, T4, make_float4(depth, u, v, u2f(prim)), hit ? inst : kUnset, maxSeg, zeroCutoff, r);
+        if (lead && r.addRad) addRadiance(rad, f2u(o4.w), r.radd);
+        pc.hit += r.hitGeom; pc.acc += r.accd;
+        if (r.shadow) {
+            ++pc.sh;
+            if (ldsLoadAcq(&box.help[w])) {
+                ++posted;
+                if (lead) {
+                    box.so[w] = r.so; box.sd[w] = r.sd; box.sc[w] = r.sc;
+                    ldsStoreRel(&box.post[w], posted);
+                }
+                pend = true;
+            } else {
+                float sdep = r.so.w, su = 0.0f, sv = 0.0f;
+                uint32_t si = kUnset, sp = kUnset;
+                if (!traceWave<true>(S, Tt, xyz(r.so), xyz(r.sd), sdep, su, sv, si, sp, rstk, pro)) {
+                    if (lead) addRadiance(rad, f2u(r.sd.w), xyz(r.sc));
+                    ++pc.un; ++pc.acc;
+                }
+            }
+        }
+        if (lead && r.capped) noteCapped(C, f2u(o4.w));
+        if (!r.cont) {
+            if (lead) atomicMax(&C->segMax, r.seg);
+            break;
+        }
+        ++pc.cont;
+        o4 = r.o; d4 = r.d; T4 = r.T;
+    }
+    if (pend) {                            /* the last segment's shadow ray */
+        while (ldsLoadAcq(&box.done[w]) != posted) __builtin_amdgcn_s_sleep(1);
+        if (!box.occ[w]) {
+            if (lead) addRadiance(rad, f2u(box.sd[w].w), xyz(box.sc[w]));
+            ++pc.un; ++pc.acc;
+        }
+    }
+    ++pc.paths;
+    if (lead) {
+        __threadfence();          /* radiance before completion */
+        atomicAdd(&frameDone[(blockIdx.x % kStripes) * window + slot], 1u);
+    }
+}
+
+__global__ __launch_bounds__(128, SURF_COOP_WAVES) void k_tail_pair(DevScene S, Pool cur, uint32_t n, float4* __restrict__ rad,
+                                                   uint32_t* __restrict__ frameDone, uint32_t npx, uint32_t window, Counters* C,
+                                                   uint32_t stackWords, uint32_t firstCounted) {
+    extern __shared__ uint32_t lds[];
+    __shared__ PairBox box;
+    /* LDS: [record stack | prologue table] per wave, then the trace tables and the shading tables */
+    const uint32_t per = stackWords + proWords(S);
+    const TraceTables Tt = stageTrace(S, lds, 2u * per);
+    uint32_t* const shw = lds + ((2u * per + S.nInst * (uint32_t)((sizeof(TraceInst) + 4u) / 4u) + 3u) & ~3u);
+    DevInstance* const sInst = reinterpret_cast<DevInstance*>(shw);
+    DevMaterial* const sMat = reinterpret_cast<DevMaterial*>(sInst + S.nInst);
+    uint2* const sLights = reinterpret_cast<uint2*>(sMat + S.nMats);
+    if (threadIdx.x < 2u) {
+        box.run[threadIdx.x] = 1u; box.help[threadIdx.x] = 0u;
+        box.post[threadIdx.x] = 0u; box.done[threadIdx.x] = 0u; box.occ[threadIdx.x] = 0u;
+    }
+    stageTables(S, sInst, sMat, sLights);            /* ends with a barrier */
+    const ShadeTables Tb{sInst, sMat, sLights};
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   /* wave-uniform: the walk's LDS bases are scalar */
+    const bool lead = (threadIdx.x & 63u) == 0u;
+    float* rstk = reinterpret_cast<float*>(lds + w * per);
+    float4* pro = reinterpret_cast<float4*>(lds + w * per + stackWords);
+    PairCounts pc{0, 0, 0, 0, 0, 0, 0};
+    uint32_t posted = 0u;                             /* == box.post[w] */
+    for (;;) {
+        uint32_t i = 0u;
+        if (lead) i = atomicAdd(&C->rowNext, 1u);
+        i = __builtin_amdgcn_readfirstlane(i);
+        if (i >= n) break;
+        pairPath(S, Tt, Tb, box, w, cur.od[2u * i], cur.od[2u * i + 1u], cur.T[i], rad, frameDone, npx, window, C, rstk, pro,
+                 lead, posted, pc);
+    }
+    /* queue empty: leave the path loop, then serve the sibling's shadow rays
+     * while it still runs a path (one of the two always sees the other's 0) */
+    const uint32_t m = w ^ 1u;
+    __hip_atomic_store(&box.run[w], 0u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (__hip_atomic_load(&box.run[m], __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+        ldsStoreRel(&box.help[m], 1u);
+        uint32_t served = ldsLoadAcq(&box.done[m]);
+        for (;;) {
+            const uint32_t p = ldsLoadAcq(&box.post[m]);
+            if (p != served) {
+                const float4 so = box.so[m], sd = box.sd[m];
+                float sdep = so.w, su = 0.0f, sv = 0.0f;
+                uint32_t si = kUnset, sp = kUnset;
+                const bool occ = traceWave<true>(S, Tt, xyz(so), xyz(sd), sdep, su, sv, si, sp, rstk, pro);
+                if (lead) {
+                    box.occ[m] = occ ? 1u : 0u;
+                    ldsStoreRel(&box.done[m], p);
+                }
+                served = p;
+                continue;
+            }
+            if (!ldsLoadAcq(&box.run[m])) break;
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    if (lead && pc.paths) {
+        unsigned long long* ev = C->evS[blockIdx.x % kStripes];
+        atomicAdd(&ev[0], (unsigned long long)(pc.ext - pc.paths * firstCounted)); atomicAdd(&ev[1], (unsigned long long)pc.hit);
+        atomicAdd(&ev[2], (unsigned long long)pc.cont); atomicAdd(&ev[3], (unsigned long long)pc.sh);
+        atomicAdd(&ev[4], (unsigned long long)pc.acc); atomicAdd(&ev[5], (unsigned long long)pc.un);
+        atomicAdd(&ev[6], (unsigned long long)pc.paths);
+    }
+}
+
 /* acc[p] += (radiance, 1) for frames [f0, f0+count) of the stream, in frame
  * order (renderer.cpp:180); frame f's radiance lives in slot f % window. */
 __global__ __launch_bounds__(kBlock) void k_accumulate(const float4* __restrict__ rad, float4* __restrict__ acc,

@@ -118,6 +118,8 @@ struct surf_ctx {
     bool coopEligible = false;     /* single-leaf TLAS of <= 64 instances, LDS tables */
     int traceMode = 0;             /* surf_trace_closest/_any: 0 one ray per lane, 1 one ray per wave, 2 one ray per 16-lane row */
     bool tailRows = false;         /* drain on k_tail_rows (four paths per wave; SURF_TAIL_ROWS=1) instead of k_tail_coop */
+    bool tailPair = true;          /* cooperative drain on k_tail_pair (partner waves trace the shadow rays; SURF_TAIL_PAIR=0: k_tail_coop) */
+    uint32_t cus = 256;            /* compute units of the device */
     bool sortRays = true;          /* order each phase's rays by start instance (SURF_SORT=0: off) */
     /* ray order (k_bincount / k_binscan / k_binscatter each phase) */
     uint32_t* order = nullptr;
@@ -200,6 +202,10 @@ size_t coopLds(const surf_ctx* c) {
 size_t coopTailLds(const surf_ctx* c) {
     return ((coopLds(c) + 15) & ~(size_t)15) + (size_t)c->nInstances * sizeof(DevInstance) + (size_t)c->nMaterials * sizeof(DevMaterial) +
            (size_t)c->nLightsUp * sizeof(uint2);
+}
+/* k_tail_pair: a record stack and a prologue table per wave (two waves), then the tables */
+size_t pairTailLds(const surf_ctx* c) {
+    return coopTailLds(c) + ((size_t)recStackWords(c) + 16u * c->nInstances) * sizeof(float);
 }
 size_t traversalLds(const surf_ctx* c, uint32_t block) {
     size_t b = (size_t)stackWords(c, block) * sizeof(uint32_t);
@@ -329,6 +335,7 @@ int allocWavefront(surf_ctx* c) {
     c->gridExtend = (uint32_t)std::min<uint64_t>((cap + c->extBlock - 1) / c->extBlock, (uint64_t)cus * extPerCu);
     c->gridConnect = (uint32_t)std::min<uint64_t>(maxBlocks, (uint64_t)cus * conPerCu);
     c->coopMax = (uint32_t)cus * 4 * SURF_TAIL_WAVES;
+    c->cus = (uint32_t)cus;
     if (const char* e = std::getenv("SURF_DRAIN_REPLAYS")) c->drainReplays = std::max(1, std::atoi(e));
     c->gridRegen = (uint32_t)std::min<uint64_t>(maxBlocks, (uint64_t)cus * 8);
     c->allocated = true;
@@ -572,6 +579,21 @@ int runTail(surf_ctx* c) {
             c->stats.tail_survivors += cnt;
             break;
         }
+        if (c->tailPair && waveEligible(c) && cnt <= c->coopAll) {
+            /* as many two-wave workgroups as are resident at once, each wave
+             * taking paths from the queue; idle waves trace their sibling's
+             * shadow rays once the queue is empty */
+            int per = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_tail_pair, 128, pairTailLds(c)) != hipSuccess || per < 1)
+                per = 2 * SURF_COOP_WAVES;
+            const uint32_t blocks = std::max<uint32_t>(1u, std::min<uint32_t>((cnt + 1u) / 2u, c->cus * (uint32_t)per));
+            SURF_CHECK(c, hipMemsetAsync(&c->ctr->rowNext, 0, sizeof(uint32_t), c->stream));
+            hipLaunchKernelGGL(k_tail_pair, dim3(blocks), dim3(128), pairTailLds(c), c->stream, c->S, in, cnt, c->rad, c->frameDone,
+                               c->npx, c->window, c->ctr, recStackWords(c), firstCounted);
+            SURF_CHECK(c, hipGetLastError());
+            c->stats.tail_survivors += cnt;
+            break;
+        }
         if (waveEligible(c) && cnt <= c->coopAll) {
             hipLaunchKernelGGL(k_tail_coop, dim3(cnt), dim3(64), coopTailLds(c), c->stream, c->S, in, cnt, c->rad, c->frameDone,
                                c->npx, c->window, c->ctr, recStackWords(c), firstCounted);
@@ -757,6 +779,7 @@ int createCtx(int dev, uint32_t w, uint32_t h, std::vector<uint32_t> rows, surf_
     if (const char* e = std::getenv("SURF_SORT")) c->sortRays = e[0] != '0';
     if (const char* e = std::getenv("SURF_CONNECT_GLOBAL")) c->connectGlobal = e[0] != '0';
     if (const char* e = std::getenv("SURF_TAIL_ROWS")) c->tailRows = e[0] == '1';
+    if (const char* e = std::getenv("SURF_TAIL_PAIR")) c->tailPair = e[0] != '0';
     c->width = w;
     c->height = h;
     c->rows = std::move(rows);

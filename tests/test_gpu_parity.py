@@ -133,15 +133,20 @@ def test_render_64x64x4_bitexact(oracle_scene, product_scene):
     _assert_counts(stats, cnt)
 
 
-@pytest.mark.parametrize("policy,coop,rows", [((0, 0, 16), 60000, "1"), ((0, 0, 16), 60000, "0"), ((0, 8, 4), 0, "1"),
-                                              ((1 << 30, 0, 8), 1 << 30, "1"), ((1 << 30, 0, 8), 1 << 30, "0"), ((1, 0, 0), 0, "1")],
-                         ids=["staged+rows", "staged+coop", "8-lanes-staged", "rows-from-start", "coop-from-start",
-                              "wavefront-to-end"])
-def test_drain_policies_bitexact(oracle_scene, product_scene, policy, coop, rows, monkeypatch):
+@pytest.mark.parametrize("policy,coop,engine", [((0, 0, 16), 60000, "rows"), ((0, 0, 16), 60000, "pair"),
+                                                ((0, 0, 16), 60000, "coop"), ((0, 8, 4), 0, "rows"),
+                                                ((1 << 30, 0, 8), 1 << 30, "rows"), ((1 << 30, 0, 8), 1 << 30, "pair"),
+                                                ((1 << 30, 0, 8), 1 << 30, "coop"), ((1, 0, 0), 0, "rows")],
+                         ids=["staged+rows", "staged+pair", "staged+coop", "8-lanes-staged", "rows-from-start",
+                              "pair-from-start", "coop-from-start", "wavefront-to-end"])
+def test_drain_policies_bitexact(oracle_scene, product_scene, policy, coop, engine, monkeypatch):
     """Every drain schedule (lane stages with survivor hand-off, the four-rows
-    tail with its path queue, the one-path-per-wave tail, tail from the first
-    phase, wavefront to the end) gives the same radiance and event counts."""
-    monkeypatch.setenv("SURF_TAIL_ROWS", rows)
+    tail with its path queue, the partner-wave tail (k_tail_pair: idle waves
+    trace their sibling's shadow rays), the one-path-per-wave tail, tail from
+    the first phase, wavefront to the end) gives the same radiance and event
+    counts."""
+    monkeypatch.setenv("SURF_TAIL_ROWS", "1" if engine == "rows" else "0")
+    monkeypatch.setenv("SURF_TAIL_PAIR", "1" if engine == "pair" else "0")
     r0 = surf_amd.Renderer(product_scene, 96, 64)
     r0.set_tail_policy(*policy)
     r0.set_tail_coop(coop)
