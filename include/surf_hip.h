@@ -185,9 +185,11 @@ int surf_set_zero_cutoff(surf_ctx* ctx, int enabled);
  * stage to the end; default 16).  Results do not depend on the policy.
  * Drains the context first. */
 int surf_set_tail_policy(surf_ctx* ctx, uint32_t threshold_paths, uint32_t lanes_per_wave, uint32_t stage_segments);
-/* Drain paths handed to the cooperative tail (default 60000, 0 = never): one
+/* Drain paths handed to the cooperative tail (default 150000, 0 = never): one
  * path per 64-lane wave with the lanes-as-planes traversal (single-leaf TLAS of
- * <= 64 instances); with SURF_TAIL_ROWS=1 in the environment at surf_create,
+ * <= 64 instances), in two-wave workgroups whose idle wave traces its
+ * sibling's shadow rays once the path queue is empty (SURF_TAIL_PAIR=0 in the
+ * environment: one-wave workgroups); with SURF_TAIL_ROWS=1 at surf_create,
  * four paths per wave (one per 16-lane row, a path queue; <= 16 instances).
  * Identical results. */
 int surf_set_tail_coop(surf_ctx* ctx, uint32_t max_paths);

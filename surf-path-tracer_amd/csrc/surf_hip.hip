@@ -113,7 +113,7 @@ struct surf_ctx {
     Pool surv[2]{};                /* drain survivors, ping-pong between stages */
     uint32_t survCap = 0;
     uint32_t coopMax = 0;          /* survivors handled by the cooperative tail (one path per wave) */
-    uint32_t coopAll = 60000;      /* drain paths left to the cooperative (one path per wave) tail (surf_set_tail_coop) */
+    uint32_t coopAll = 150000;     /* drain paths left to the cooperative tail (surf_set_tail_coop); C3 drain 176-184 ms at 60000, 172-178 at 150000 */
     int drainReplays = 1;          /* graph replays per host poll while draining (SURF_DRAIN_REPLAYS) */
     bool coopEligible = false;     /* single-leaf TLAS of <= 64 instances, LDS tables */
     int traceMode = 0;             /* surf_trace_closest/_any: 0 one ray per lane, 1 one ray per wave, 2 one ray per 16-lane row */
