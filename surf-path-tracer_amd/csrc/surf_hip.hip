@@ -121,6 +121,8 @@ struct surf_ctx {
     bool tailPair = true;          /* cooperative drain on k_tail_pair (partner waves trace the shadow rays; SURF_TAIL_PAIR=0: k_tail_coop) */
     uint32_t cus = 256;            /* compute units of the device */
     bool sortRays = true;          /* order each phase's rays by start instance (SURF_SORT=0: off) */
+    bool sortPool = true;
+    bool sortShadow = true;        /* ... and the shadow queue by light (SURF_SORT=2: pool only, 3: shadow queue only) */
     /* ray order (k_bincount / k_binscan / k_binscatter each phase) */
     uint32_t* order = nullptr;
     uint32_t* binHist = nullptr;
@@ -363,7 +365,7 @@ void launchPhase(surf_ctx* c, int ph, hipEvent_t* ev) {
     const uint32_t sw = stackWords(c, kBlock);
     if (ev) (void)hipEventRecord(ev[0], c->stream);
     const uint32_t* order = nullptr;
-    if (c->sortRays) {
+    if (c->sortRays && c->sortPool) {
         launchSort(c, c->pool[par].key, par, 0);
         order = c->order;
     }
@@ -385,7 +387,7 @@ void launchPhase(surf_ctx* c, int ph, hipEvent_t* ev) {
     if (ev) (void)hipEventRecord(ev[3], c->stream);
     /* shadow rays toward the same light together (the pool order no longer needed: reuse it) */
     const uint32_t* qorder = nullptr;
-    if (c->sortRays) {
+    if (c->sortRays && c->sortShadow) {
         launchSort(c, c->Q.key, par, 1);
         qorder = c->order;
     }
@@ -776,7 +778,11 @@ int createCtx(int dev, uint32_t w, uint32_t h, std::vector<uint32_t> rows, surf_
     auto* c = new surf_ctx();
     c->device = dev;
     c->extBlock = extBlock;
-    if (const char* e = std::getenv("SURF_SORT")) c->sortRays = e[0] != '0';
+    if (const char* e = std::getenv("SURF_SORT")) {
+        c->sortRays = e[0] != '0';
+        c->sortPool = e[0] != '3';
+        c->sortShadow = e[0] != '2';
+    }
     if (const char* e = std::getenv("SURF_CONNECT_GLOBAL")) c->connectGlobal = e[0] != '0';
     if (const char* e = std::getenv("SURF_TAIL_ROWS")) c->tailRows = e[0] == '1';
     if (const char* e = std::getenv("SURF_TAIL_PAIR")) c->tailPair = e[0] != '0';
