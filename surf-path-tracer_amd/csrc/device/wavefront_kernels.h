@@ -1194,6 +1194,7 @@ __device__ __forceinline__ void blockCount(Counters* C, const int (&idx)[N], con
  * only the interleaving of lanes changes. */
 constexpr uint32_t kBins = 64;
 constexpr uint32_t kSortBlocks = 256;
+constexpr uint32_t kSortUnroll = 16;   /* keys per thread in flight in k_bincount / k_binscatter */
 static_assert(kBins <= 256u, "pool/shadow keys are one byte");
 
 /* Pool order key: the instance the path starts on (<= 14; camera rays: kBins - 1)
@@ -1237,7 +1238,18 @@ __global__ __launch_bounds__(kBlock) void k_bincount(const uint8_t* __restrict__
     __syncthreads();
     uint32_t a, b;
     sortChunk(sortCount(C, par, which), a, b);
-    for (uint32_t i = a + threadIdx.x; i < b; i += blockDim.x) atomicAdd(&h[key[i]], 1u);
+    /* kSortUnroll key loads in flight per thread before their atomics (one
+     * wave per SIMD: a rolled loop waited on each load in turn); same atomic
+     * order as the rolled loop */
+    uint32_t i = a + threadIdx.x;
+    for (; i + (kSortUnroll - 1u) * blockDim.x < b; i += kSortUnroll * blockDim.x) {
+        uint32_t k[kSortUnroll];
+#pragma unroll
+        for (uint32_t u = 0; u < kSortUnroll; ++u) k[u] = key[i + u * blockDim.x];
+#pragma unroll
+        for (uint32_t u = 0; u < kSortUnroll; ++u) atomicAdd(&h[k[u]], 1u);
+    }
+    for (; i < b; i += blockDim.x) atomicAdd(&h[key[i]], 1u);
     __syncthreads();
     if (threadIdx.x < kBins) hist[threadIdx.x * gridDim.x + blockIdx.x] = h[threadIdx.x];
 }
@@ -1276,7 +1288,15 @@ __global__ __launch_bounds__(kBlock) void k_binscatter(const uint8_t* __restrict
     __syncthreads();
     uint32_t a, b;
     sortChunk(sortCount(C, par, which), a, b);
-    for (uint32_t i = a + threadIdx.x; i < b; i += blockDim.x) order[atomicAdd(&base[key[i]], 1u)] = i;
+    uint32_t i = a + threadIdx.x;
+    for (; i + (kSortUnroll - 1u) * blockDim.x < b; i += kSortUnroll * blockDim.x) {
+        uint32_t k[kSortUnroll];
+#pragma unroll
+        for (uint32_t u = 0; u < kSortUnroll; ++u) k[u] = key[i + u * blockDim.x];
+#pragma unroll
+        for (uint32_t u = 0; u < kSortUnroll; ++u) order[atomicAdd(&base[k[u]], 1u)] = i + u * blockDim.x;
+    }
+    for (; i < b; i += blockDim.x) order[atomicAdd(&base[key[i]], 1u)] = i;
 }
 
 /* ------------------------------------------------------------------ kernels */
