@@ -1195,6 +1195,10 @@ __device__ __forceinline__ void blockCount(Counters* C, const int (&idx)[N], con
 constexpr uint32_t kBins = 64;
 constexpr uint32_t kSortBlocks = 256;
 constexpr uint32_t kSortUnroll = 16;   /* keys per thread in flight in k_bincount / k_binscatter */
+constexpr uint32_t kSortThreads = 1024; /* threads per k_bincount / k_binscatter block (4 waves per SIMD) */
+#ifndef SURF_SORT_FUSED_SCAN
+#define SURF_SORT_FUSED_SCAN 1          /* k_binscatter scans the counts itself (no k_binscan launch) */
+#endif
 static_assert(kBins <= 256u, "pool/shadow keys are one byte");
 
 /* Pool order key: the instance the path starts on (<= 14; camera rays: kBins - 1)
@@ -1231,7 +1235,7 @@ __device__ __forceinline__ void sortChunk(uint32_t n, uint32_t& a, uint32_t& b) 
     b = min(n, a + c);
 }
 
-__global__ __launch_bounds__(kBlock) void k_bincount(const uint8_t* __restrict__ key, const Counters* C, int par, int which,
+__global__ __launch_bounds__(kSortThreads) void k_bincount(const uint8_t* __restrict__ key, const Counters* C, int par, int which,
                                                      uint32_t* __restrict__ hist) {
     __shared__ uint32_t h[kBins];
     if (threadIdx.x < kBins) h[threadIdx.x] = 0u;
@@ -1281,10 +1285,50 @@ __global__ __launch_bounds__(1024) void k_binscan(uint32_t* __restrict__ hist, u
     for (uint32_t k = 0; k < kPer; ++k) { hist[a + k] = run; run += c[k]; }
 }
 
-__global__ __launch_bounds__(kBlock) void k_binscatter(const uint8_t* __restrict__ key, const Counters* C, int par, int which,
+__global__ __launch_bounds__(kSortThreads) void k_binscatter(const uint8_t* __restrict__ key, const Counters* C, int par, int which,
                                                        const uint32_t* __restrict__ hist, uint32_t* __restrict__ order) {
     __shared__ uint32_t base[kBins];
+#if SURF_SORT_FUSED_SCAN
+    /* this block's start in every bin, from the raw bin-major [kBins][blocks]
+     * counts (no separate scan launch): kLanes consecutive lanes per bin sum
+     * the bin's count over all blocks and over the blocks before this one,
+     * then one wave scans the bin totals */
+    {
+        constexpr uint32_t kLanes = kSortThreads / kBins, kPer = kSortBlocks / kLanes;
+        static_assert(kSortThreads % kBins == 0u && kSortBlocks % kLanes == 0u && kLanes <= 64u, "scan layout");
+        __shared__ uint32_t tot[kBins];
+        const uint32_t bin = threadIdx.x / kLanes, sub = threadIdx.x % kLanes;
+        const uint32_t* row = hist + bin * kSortBlocks + sub * kPer;
+        uint32_t c[kPer];
+#pragma unroll
+        for (uint32_t u = 0; u < kPer; ++u) c[u] = row[u];
+        uint32_t all = 0, below = 0;
+#pragma unroll
+        for (uint32_t u = 0; u < kPer; ++u) {
+            all += c[u];
+            below += sub * kPer + u < blockIdx.x ? c[u] : 0u;
+        }
+#pragma unroll
+        for (uint32_t off = 1; off < kLanes; off <<= 1) {
+            all += __shfl_xor(all, off, kLanes);
+            below += __shfl_xor(below, off, kLanes);
+        }
+        if (sub == 0u) { tot[bin] = all; base[bin] = below; }
+        __syncthreads();
+        if (threadIdx.x < kBins) {
+            const uint32_t v = tot[threadIdx.x];
+            uint32_t inc = v;
+#pragma unroll
+            for (uint32_t off = 1; off < kBins; off <<= 1) {
+                const uint32_t t = __shfl_up(inc, off, kBins);
+                if (threadIdx.x >= off) inc += t;
+            }
+            base[threadIdx.x] += inc - v;
+        }
+    }
+#else
     if (threadIdx.x < kBins) base[threadIdx.x] = hist[threadIdx.x * gridDim.x + blockIdx.x];
+#endif
     __syncthreads();
     uint32_t a, b;
     sortChunk(sortCount(C, par, which), a, b);

@@ -349,10 +349,12 @@ StreamGeom geom(const surf_ctx* c) { return StreamGeom{c->dRows, c->width, c->np
 /* Counting sort of the pool (which 0) or shadow queue (which 1) of phase par
  * by its 4-bit key into c->order. */
 void launchSort(surf_ctx* c, const uint8_t* key, int par, int which) {
-    hipLaunchKernelGGL(k_bincount, dim3(kSortBlocks), dim3(kBlock), 0, c->stream, key, (const Counters*)c->ctr, par, which,
+    hipLaunchKernelGGL(k_bincount, dim3(kSortBlocks), dim3(kSortThreads), 0, c->stream, key, (const Counters*)c->ctr, par, which,
                        c->binHist);
+#if !SURF_SORT_FUSED_SCAN
     hipLaunchKernelGGL(k_binscan, dim3(1), dim3(1024), 0, c->stream, c->binHist, kBins * kSortBlocks);
-    hipLaunchKernelGGL(k_binscatter, dim3(kSortBlocks), dim3(kBlock), 0, c->stream, key, (const Counters*)c->ctr, par, which,
+#endif
+    hipLaunchKernelGGL(k_binscatter, dim3(kSortBlocks), dim3(kSortThreads), 0, c->stream, key, (const Counters*)c->ctr, par, which,
                        (const uint32_t*)c->binHist, c->order);
 }
 
