@@ -217,6 +217,21 @@ def test_full_resolution_rows(oracle_scene, product_scene):
     assert np.isfinite(g).all() and np.all(g[..., 3] == F)
 
 
+def test_c3_subset_1280x720x16_bitexact(oracle_scene, product_scene):
+    """SURVEY.md 8d's C3 parity subset: 1280x720 at 16 spp, unbounded + RR,
+    the GPU rendering the whole frame as one stream (its drain included), the
+    oracle three bands of rows (top, middle, bottom), compared bit for bit."""
+    W, H, F = 1280, 720, 16
+    r = surf_amd.Renderer(product_scene, W, H)
+    r.render(F, 0, 0)
+    g = r.accumulator()
+    assert np.all(g[..., 3] == F)
+    for a, b in ((0, 8), (356, 364), (712, 720)):
+        c, _, _ = oracle_scene.render(W, H, F, rows=(a, b))
+        _assert_bitexact(g[a:b], c, f"1280x720x16 rows {a}..{b - 1}")
+    r.close()
+
+
 def test_pool_and_batch_invariance(product_scene):
     """Compaction/regeneration/batching must not change any sample."""
     W, H, F = 80, 60, 5
