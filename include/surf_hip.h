@@ -156,20 +156,26 @@ int surf_shard_rows(const surf_ctx* ctx, uint32_t* rows, uint32_t* row_count);
 /* Paths in flight (default: sized from the shard, >= 1M when possible). Must be
  * called before the first render. */
 int surf_set_pool_capacity(surf_ctx* ctx, uint32_t paths);
-/* Frame window: frames whose samples may be in flight at once (default: as
- * many as 32 GiB of radiance slots hold, at most 4096 -- 2330 frames at
- * 1280x720, 1035 at 1920x1080, of the 288 GB HBM).  Sample radiance is held
- * per (frame slot, pixel) until a frame completes and is accumulated in frame
- * order; long Russian-roulette paths of old frames overlap the bulk of newer
- * ones.  A stream longer than the window issues frame f only once frame
- * f - window is accumulated, so the window is sized past the longest renders
- * (C4: 1024 frames). */
+/* Frame window: frames whose samples may be in flight at once.  Default: the
+ * frames the stream being started requests (one render call's frame count),
+ * at least 256 (a drop-in loop extends its stream one frame per call), at most
+ * 4096 and at most what min(32 GiB, a quarter of the free HBM) holds; a later
+ * stream that requests more frames grows the ring (C3 at 1280x720: 256 frames
+ * = 3.8 GB; C4 at 1920x1080: 1024 frames = 34 GB, within the 1035 that 32 GiB hold).
+ * Sample radiance is held per (frame slot, pixel) until a frame completes and
+ * is accumulated in frame order; long Russian-roulette paths of old frames
+ * overlap the bulk of newer ones.  A stream longer than the window issues
+ * frame f only once frame f - window is accumulated.  Setting it fixes it
+ * (must be called before the first render). */
 int surf_set_frame_batch(surf_ctx* ctx, uint32_t frames);
 /* Throughput cutoff (default on): a path whose throughput T is below FLT_MIN
  * (1.17549435e-38) in every channel -- zero or denormal -- ends early.  The
  * reference's Russian roulette ends such a path with certainty at its next
- * diffuse bounce (p = max(T) < 2^-32, the smallest positive randomF32), so at
- * most two contributions of < 1.2e-38 x (emission or light term) are dropped:
+ * diffuse bounce (p = max(T) < 2^-32, the smallest positive randomF32).  The
+ * terms dropped are those the path would still add before that bounce: the
+ * emitter hits along its chain of specular / dielectric bounces up to the next
+ * diffuse bounce (any number of them), plus that bounce's NEE term -- each
+ * below 1.2e-38 x (emission or light term):
  * radiance-neutral in f32 except for a pixel whose own energy is ~1e-38 (the
  * parity tests compare the GPU with the cutoff against the oracle without it,
  * bit for bit, on every tested image); n_ext/n_cont/... shrink.  It ends the

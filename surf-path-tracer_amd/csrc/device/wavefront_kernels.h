@@ -133,7 +133,7 @@ struct Counters {
     unsigned long long limit;        /* host-written issue limit (frame window) */
     unsigned long long baseFrame;    /* absolute frame index of stream frame 0 */
     unsigned long long ev[16];       /* ext, hit, cont, shadow, acc, unocc, tail paths, capped paths, wavefront ext */
-    uint32_t capped[64];             /* sample ids of paths ended by the segment cap, one per workgroup 0..63 (diagnostics, ~0 = none) */
+    uint32_t capped[64];             /* sample ids of paths ended by the segment cap, slot blockIdx % 64 (diagnostics, ~0 = none) */
     /* event counts striped over kStripes cache lines (block b adds to stripe
      * b % kStripes): a counter shared by every block of a launch serializes its
      * atomics (~12 ns each, measured); totals = ev + sum over stripes */
@@ -143,12 +143,13 @@ struct Counters {
 constexpr uint32_t kStripes = 32;    /* frameDone and event-count stripes */
 constexpr int kEvents = 9;           /* event kinds counted (ev / evS index) */
 
-/* A path ended by the segment cap: counted in the event stripes; workgroups
- * 0..63 also keep the sample id of one such path each (diagnostics).  No
- * shared address is touched per path: a same-address atomic or load per
- * capped path serialized k_shade under C2's 8-segment cap (33 -> 88 ms). */
+/* A path ended by the segment cap: counted in the event stripes; its sample
+ * id is also stored in slot blockIdx % 64 (diagnostics: a racy overwrite, so
+ * every workgroup that caps a path leaves some id behind).  No single shared
+ * address is touched per path: a same-address atomic or load per capped path
+ * serialized k_shade under C2's 8-segment cap (33 -> 88 ms). */
 __device__ __forceinline__ void noteCappedSid(bool capped, Counters* C, uint32_t sid) {
-    if (capped && blockIdx.x < 64u) C->capped[blockIdx.x] = sid;
+    if (capped) C->capped[blockIdx.x % 64u] = sid;
 }
 __device__ __forceinline__ void noteCapped(Counters* C, uint32_t sid) {
     atomicAdd(&C->evS[blockIdx.x % kStripes][7], 1ull);
@@ -1590,8 +1591,9 @@ __device__ __forceinline__ void shadePath(const DevScene& S, const ShadeTables& 
         }
     }
     /* throughput cutoff: every channel of T below FLT_MIN.  Russian roulette ends
-     * such a path with certainty at its next diffuse bounce (p < 2^-32 <= rand),
-     * so at most two contributions of < 1.2e-38 * L remain; it also ends the
+     * such a path with certainty at its next diffuse bounce (p < 2^-32 <= rand);
+     * what is dropped is the emitter hits along the specular / dielectric chain
+     * up to that bounce plus its NEE term, each < 1.2e-38 * L; it also ends the
      * TIR orbits in the glass lens that never terminate in the reference. */
     if (zeroCutoff && T.x < 1.17549435e-38f && T.y < 1.17549435e-38f && T.z < 1.17549435e-38f) alive = false;
     r.capped = alive && (maxSeg != 0u && seg >= maxSeg);

@@ -61,7 +61,8 @@ struct surf_ctx {
     std::vector<uint32_t> rows;
     uint32_t npx = 0;
     uint32_t capacity = 0;
-    uint32_t window = 0;           /* frames whose samples may be in flight (radiance slots); 0 = default */
+    uint32_t window = 0;           /* frames whose samples may be in flight (radiance slots; ensureWindow) */
+    bool windowFixed = false;      /* set by surf_set_frame_batch */
     bool profiling = false;
     std::string err;
 
@@ -280,16 +281,6 @@ int allocWavefront(surf_ctx* c) {
         const uint64_t want = (uint64_t)c->width * c->height * 4;
         c->capacity = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(want, 65536), 1u << 22);
     }
-    if (c->window == 0) {
-        /* default: the frames 32 GiB of radiance slots hold (of the 288 GB HBM;
-         * at most a quarter of the free memory), at most 4096 -- past the longest render (C4, 1024 frames), so a
-         * stream never waits for an old frame's long paths to free a slot */
-        uint64_t budget = 32ull << 30;
-        size_t freeB = 0, totalB = 0;
-        if (hipMemGetInfo(&freeB, &totalB) == hipSuccess && freeB > 0) budget = std::min<uint64_t>(budget, freeB / 4);
-        const uint64_t maxFrames = budget / ((uint64_t)c->npx * sizeof(float4));
-        c->window = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(4096, maxFrames));
-    }
     const size_t cap = c->capacity;
     int rc;
     for (int p = 0; p < 2; ++p) {
@@ -315,12 +306,9 @@ int allocWavefront(surf_ctx* c) {
     if ((rc = devAlloc(c, c->wfAllocs, &c->Q.d, cap))) return rc;
     if ((rc = devAlloc(c, c->wfAllocs, &c->Q.c, cap))) return rc;
     if ((rc = devAlloc(c, c->wfAllocs, &c->Q.key, cap))) return rc;
-    if ((rc = devAlloc(c, c->wfAllocs, &c->rad, (size_t)c->npx * c->window))) return rc;
     if ((rc = devAlloc(c, c->wfAllocs, &c->ctr, 1))) return rc;
-    if ((rc = devAlloc(c, c->wfAllocs, &c->frameDone, (size_t)kStripes * c->window))) return rc;
     if ((rc = devAlloc(c, c->wfAllocs, &c->dOutRGBA, c->npx))) return rc;
-    if (hipHostMalloc((void**)&c->hctr, sizeof(Counters), hipHostMallocDefault) != hipSuccess ||
-        hipHostMalloc((void**)&c->hFrameDone, (size_t)kStripes * c->window * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess)
+    if (hipHostMalloc((void**)&c->hctr, sizeof(Counters), hipHostMallocDefault) != hipSuccess)
         return fail(c, SURF_ERR_OOM, "hipHostMalloc of the counter block failed");
     for (auto& e : c->pev) SURF_CHECK(c, hipEventCreate(&e));
     const uint64_t maxBlocks = (cap + kBlock - 1) / kBlock;
@@ -341,6 +329,43 @@ int allocWavefront(surf_ctx* c) {
     if (const char* e = std::getenv("SURF_DRAIN_REPLAYS")) c->drainReplays = std::max(1, std::atoi(e));
     c->gridRegen = (uint32_t)std::min<uint64_t>(maxBlocks, (uint64_t)cus * 8);
     c->allocated = true;
+    return SURF_OK;
+}
+
+/* The radiance ring (float4 per frame slot x pixel) and the per-slot
+ * completion counters, sized for the stream about to start (no stream active):
+ * as many slots as the stream requests frames -- so no frame waits for an old
+ * frame's long Russian-roulette paths to free a slot -- at least kWindowFloor
+ * (a drop-in loop extends its stream one frame per call, so its first request
+ * says nothing about its length), at most 4096 and at most what
+ * min(32 GiB, a quarter of the free HBM) holds.  A later, longer stream grows
+ * the ring; a window set by surf_set_frame_batch is kept as given. */
+constexpr uint64_t kWindowFloor = 256;
+int ensureWindow(surf_ctx* c, uint64_t frames) {
+    uint64_t want = c->windowFixed ? c->window : std::min<uint64_t>(4096, std::max<uint64_t>(frames, kWindowFloor));
+    if (!c->windowFixed) {
+        uint64_t budget = 32ull << 30;
+        size_t freeB = 0, totalB = 0;
+        if (hipMemGetInfo(&freeB, &totalB) == hipSuccess && freeB > 0)
+            budget = std::min<uint64_t>(budget, (freeB + (c->rad ? (size_t)c->npx * c->window * sizeof(float4) : 0)) / 4);
+        want = std::max<uint64_t>(1, std::min<uint64_t>(want, budget / ((uint64_t)c->npx * sizeof(float4))));
+    }
+    if (c->rad && want <= c->window) return SURF_OK;
+    if (c->rad) {
+        SURF_CHECK(c, hipStreamSynchronize(c->stream));
+        (void)hipFree(c->rad); (void)hipFree(c->frameDone); (void)hipHostFree(c->hFrameDone);
+        c->rad = nullptr; c->frameDone = nullptr; c->hFrameDone = nullptr;
+        destroyGraph(c);                          /* the ring and the window are kernel arguments */
+    }
+    c->window = (uint32_t)want;
+    if (hipMalloc(&c->rad, (size_t)c->npx * c->window * sizeof(float4)) != hipSuccess ||
+        hipMalloc(&c->frameDone, (size_t)kStripes * c->window * sizeof(uint32_t)) != hipSuccess ||
+        hipHostMalloc((void**)&c->hFrameDone, (size_t)kStripes * c->window * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess) {
+        if (c->rad) (void)hipFree(c->rad);
+        if (c->frameDone) (void)hipFree(c->frameDone);
+        c->rad = nullptr; c->frameDone = nullptr; c->hFrameDone = nullptr;
+        return fail(c, SURF_ERR_OOM, "radiance ring of " + std::to_string(c->window) + " frames does not fit");
+    }
     return SURF_OK;
 }
 
@@ -572,10 +597,7 @@ int runTail(surf_ctx* c) {
             /* every remaining path through the row queue: as many four-row
              * waves as are resident at once, each row taking the next path
              * when its own ends */
-            int cus = 256;
-            hipDeviceProp_t prop;
-            if (hipGetDeviceProperties(&prop, c->device) == hipSuccess && prop.multiProcessorCount > 0) cus = prop.multiProcessorCount;
-            const uint32_t blocks = std::min<uint32_t>((cnt + 3u) / 4u, (uint32_t)cus * 4u * SURF_ROWS_WAVES);
+            const uint32_t blocks = std::min<uint32_t>((cnt + 3u) / 4u, c->cus * 4u * SURF_ROWS_WAVES);
             SURF_CHECK(c, hipMemsetAsync(&c->ctr->rowNext, 0, sizeof(uint32_t), c->stream));
             hipLaunchKernelGGL(k_tail_rows, dim3(blocks), dim3(64), rowsLds(c), c->stream, c->S, in, cnt, c->rad, c->frameDone,
                                c->npx, c->window, c->ctr, recStackWords(c), firstCounted);
@@ -842,6 +864,8 @@ void surf_destroy(surf_ctx* c) {
     freeList(c->wfAllocs);
     if (c->hctr) (void)hipHostFree(c->hctr);
     if (c->hFrameDone) (void)hipHostFree(c->hFrameDone);
+    if (c->rad) (void)hipFree(c->rad);
+    if (c->frameDone) (void)hipFree(c->frameDone);
     for (auto& e : c->pev) if (e) (void)hipEventDestroy(e);
     if (c->acc) (void)hipFree(c->acc);
     if (c->dRows) (void)hipFree(c->dRows);
@@ -877,6 +901,7 @@ int surf_set_frame_batch(surf_ctx* c, uint32_t frames) {
     if (!c || frames == 0 || (uint64_t)frames * c->npx >= (1ull << 32)) return SURF_ERR_INVALID;
     if (c->allocated) return fail(c, SURF_ERR_INVALID, "frame window is fixed after the first render");
     c->window = frames;
+    c->windowFixed = true;
     return SURF_OK;
 }
 
@@ -892,7 +917,7 @@ int surf_debug_capped(surf_ctx* c, uint32_t* sids, uint32_t max, uint64_t* count
         streamEvents(*c->hctr, e);
         *count = e[7];
     }
-    /* the recorded ids: one per workgroup 0..63 that capped a path */
+    /* the recorded ids: slot blockIdx % 64 of each workgroup that capped a path (racy, any one per slot) */
     uint32_t n = 0;
     if (c->hctr)
         for (uint32_t k = 0; k < 64 && n < max && n < *count; ++k)
@@ -1281,11 +1306,14 @@ int surf_render(surf_ctx* c, uint32_t frames, uint32_t firstFrame, uint32_t maxS
     SURF_CHECK(c, hipSetDevice(c->device));
     int rc = allocWavefront(c);
     if (rc) return rc;
-    if (!c->profiling && (rc = buildGraph(c))) return rc;
     /* continue the open stream only for the next consecutive frames of the same kind */
     if (c->streamActive && (firstFrame != c->baseFrame + c->targetFrames || maxSeg != c->streamMaxSeg))
         if ((rc = endStream(c))) return rc;
-    if (!c->streamActive && (rc = startStream(c, firstFrame, maxSeg))) return rc;
+    if (!c->streamActive) {
+        if ((rc = ensureWindow(c, frames))) return rc;
+        if ((rc = startStream(c, firstFrame, maxSeg))) return rc;
+    }
+    if (!c->profiling && (rc = buildGraph(c))) return rc;         /* (re)captured if the ring moved */
     SURF_CHECK(c, hipEventRecord(c->ev0, c->stream));
     c->targetFrames += frames;
     if ((rc = pump(c, false))) return rc;

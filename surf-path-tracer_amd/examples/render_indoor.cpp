@@ -80,11 +80,18 @@ int main(int argc, char** argv) {
             const auto t0 = std::chrono::steady_clock::now();
             renderer.render(0.0f);        /* returns once the frame's samples are issued (lumenOutput: frameInfo() drains) */
             const FrameInstrumentationData& info = renderer.frameInfo();
-            const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-            /* main.cpp:431-442 */
-            std::printf("%08.2fms (%05.1f fps) - %08.2fMrays/s - %05u samples (%u spp) - %010.2f Lumen\n", ms, 1000.0 / ms,
-                        (double)W * H * renderer.config().samplesPerFrame / ms / 1000.0, info.totalSamples,
-                        renderer.config().samplesPerFrame, info.energy);
+            const auto t1 = std::chrono::steady_clock::now();
+            const double ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+            /* main.cpp:431-442's line.  Without --lumen, render() returns once the
+             * frame is issued, so `ms` is the ISSUE latency of the call, not a
+             * frame time; the rate printed is samples ISSUED so far over the
+             * loop's wall time (frames still in flight included, so it reads
+             * high until the drain); the finished-sample rate of the loop is the
+             * final JSON line's mrays_per_s */
+            const double loopSoFar = std::chrono::duration<double, std::milli>(t1 - tLoop).count();
+            std::printf("%08.2fms issue (%05.1f calls/s) - %08.2fMrays/s issued avg - %05u samples (%u spp) - %010.2f Lumen\n", ms,
+                        1000.0 / ms, (double)W * H * renderer.config().samplesPerFrame * (f + 1) / loopSoFar / 1000.0,
+                        info.totalSamples, renderer.config().samplesPerFrame, info.energy);
         }
 
         renderer.synchronize();           /* every frame accumulated */

@@ -206,6 +206,47 @@ def test_segment_cap_c2_semantics(oracle_scene, product_scene):
     _assert_counts(stats, cnt)
 
 
+def test_c2_1280x720_cap8_rows(oracle_scene, product_scene):
+    """C2 at its full resolution (BASELINE.json configs[1]: 1280x720, at most 8
+    segments): the GPU renders the whole frame as one stream (the cap ends
+    paths in k_shade, the drain included), the oracle three bands of rows in
+    reference semantics; bit for bit, and the event counts of the bands'
+    paths are consistent (every capped path still adds its radiance)."""
+    W, H, F = 1280, 720, 4
+    r = surf_amd.Renderer(product_scene, W, H)
+    r.render(F, 0, 8)
+    g = r.accumulator()
+    st = r.stats()
+    r.close()
+    assert np.all(g[..., 3] == F)
+    assert st["max_segments"] <= 8
+    for a, b in ((0, 8), (356, 364), (712, 720)):
+        c, _, _ = oracle_scene.render(W, H, F, rows=(a, b), max_segments=8)
+        _assert_bitexact(g[a:b], c, f"C2 1280x720x{F} cap 8 rows {a}..{b - 1}")
+
+
+def test_window_grows_with_stream_bitexact(oracle_scene, product_scene):
+    """The radiance ring follows the requested stream: a first 1-frame stream
+    sizes it at the floor (256 frames), a later 300-frame stream grows it (the
+    graph is re-captured on the new ring); both renders equal the oracle's."""
+    W, H = 16, 12
+    r = surf_amd.Renderer(product_scene, W, H)
+    r.render(1, 0, 0)
+    g1 = r.accumulator()
+    r.clear_accumulator()
+    r.render(300, 0, 0)
+    g2 = r.accumulator()
+    r.close()
+    oracle.set_zero_cutoff(True)
+    try:
+        c1, _, _ = oracle_scene.render(W, H, 1)
+        c2, _, _ = oracle_scene.render(W, H, 300)
+    finally:
+        oracle.set_zero_cutoff(False)
+    _assert_bitexact(g1, c1, "1-frame stream")
+    _assert_bitexact(g2, c2, "300-frame stream after the ring grew")
+
+
 def test_full_resolution_rows(oracle_scene, product_scene):
     """1280x720 (C2/C3 resolution): GPU renders the whole frame, the oracle a band of rows."""
     W, H, F = 1280, 720, 2
@@ -346,8 +387,9 @@ def test_animation_update_render_bitexact():
 
 def test_c5_deep_bvh_bitexact():
     """C5: 10.2M-triangle lattice BLAS (HBM-resident, depth 36,
-    built by the parallel builder) -- hit records and a small render equal the
-    oracle's, whose BLAS comes from the reference's sequential build."""
+    built by the parallel builder) -- hit records, a small render and three row
+    bands of a full 1280x720 render equal the oracle's, whose BLAS comes from
+    the reference's sequential build."""
     W, H, F = 64, 48, 2
     o = oracle.OracleScene(variant=1)
     p = surf_amd.Scene.indoor(variant=1)
@@ -363,6 +405,17 @@ def test_c5_deep_bvh_bitexact():
         c, _, _ = o.render(W, H, F)
         _assert_bitexact(r.accumulator(), c, "C5 64x48x2")
         r.close()
+        # C5 at its full resolution (1280x720): the whole frame on the GPU (drain
+        # included), one band of rows per third of the image on the oracle
+        W, H = 1280, 720
+        r = surf_amd.Renderer(p, W, H)
+        r.render(F, 0, 0)
+        g = r.accumulator()
+        r.close()
+        assert np.all(g[..., 3] == F)
+        for a in (120, 360, 600):
+            c, _, _ = o.render(W, H, F, rows=(a, a + 4))
+            _assert_bitexact(g[a:a + 4], c, f"C5 1280x720x{F} rows {a}..{a + 3}")
     finally:
         o.close()
         p.close()
