@@ -96,6 +96,8 @@ struct DevScene {
     uint32_t tlasLeafCount;   /* TLAS root is a leaf with this many instances (0: general TLAS) */
     uint32_t finiteBoxes;     /* every BLAS node box is finite: slabFinite is exact */
     uint32_t nodes4G;         /* every BLAS-local record offset (64 B each) fits 32 bits: the asm wave walk's buffer offsets */
+    const float* wnodes;      /* two-level records (48 floats per BLAS node, see surf_upload_scene), or null */
+    uint32_t nWnodes;         /* nodes in wnodes (every 192-B offset fits 32 bits) */
     uint32_t bgType;
     float bgColor[3], bgA[3], bgB[3];
     float cellLo[3], cellScale[3];   /* ray-order cells: the TLAS root box split in 2 per axis (scale 0: one cell) */
@@ -1025,111 +1027,400 @@ __device__ __forceinline__ bool blasWave(const DevScene& S, const TraceInst& I, 
     return blasWalk<ANY, false>(S, nodeOff, tri, o, d, rd, dn, df, cn, cf, depth, hu, hv, hprim, rs, ss);
 }
 
-/* BvhTLAS::intersect / intersectAny over a single-leaf TLAS (bvh.cpp:654-778).
- * With <= 64 instances, lane k first computes instance k's object-space ray,
- * 1/d and the slab ranges of its root's two children (all instances at once,
- * the same operations as blasWave); the instances are then taken in TLAS
- * order, each applying the depth test to its ranges at its turn (with the
- * depth the earlier instances left), so a missed instance costs a few
- * readlanes instead of a serial transform, three divisions and a slab test. */
-/* LDS prologue table of the wave traversal: 16 floats per instance (lane) */
+/* ---------------------------------------------------------------------------
+ * Two BVH levels per wave visit (the drain's closest-hit and any-hit walks).
+ *
+ * The two-level record W(X) of node X (host-built, 48 floats = 192 B) holds
+ * three node records in the lanes-as-planes order (lane l of a row holds dword
+ * planeDword(l) of the 64-B record): row 0 = rec(X), row 1 = rec(X.left),
+ * row 2 = rec(X.right) -- the boxes of X's two children and of its four
+ * grandchildren, every child's and grandchild's leftFirst / count.  (A leaf's
+ * W holds its own record in row 0.)
+ *
+ * One visit of X with W(X) in a VGPR:
+ *   - issues the loads of W of X's four grandchildren (the candidates for the
+ *     next visit) and of X's two children (what a push of the far child
+ *     needs), all addresses read from W(X);
+ *   - one slab pass over the three rows: the hit / order masks of X's
+ *     children and of both children's children;
+ *   - the reference's decisions for both levels (bvh.cpp:129-191: near child
+ *     first, far child pushed when hit, pop when both miss), exact because no
+ *     leaf lies between the two levels, so the depth is the same: near child
+ *     C of X (a leaf: push the far child, leave for the leaf), then near
+ *     child G of C with the far grandchild pushed after the far child, or --
+ *     both of C's children missed -- the far child (pushed then popped at
+ *     once in the reference), or a pop;
+ *   - the next state W(G) is one of the four candidate loads, selected by
+ *     v_cndmask on scalar masks; pushes write whole W records to the LDS
+ *     stack (256 B per entry; ds_write2st64 writes both slots, the stack
+ *     pointer advances by how many were real).
+ * One memory round trip per two levels instead of one per level, and one
+ * slab pass + one decision sequence per two levels. */
+#define SURF_W2_HEAD                                                                                   \
+    /* the state may be a leaf (entry, pop, descent): leave for it */                                  \
+    "L_chk_%=:\n\t"                                                                                    \
+    "v_readlane_b32 %[cnt], %[st], 13\n\t"                                                             \
+    "v_readlane_b32 %[lf], %[st], 12\n\t"                                                              \
+    "s_cmp_lg_u32 %[cnt], 0\n\t"                                                                       \
+    "s_cbranch_scc1 L_exit_%=\n\t"                                                                     \
+    /* candidate loads: W of the grandchildren (n0..n3) and of the children (f0, f1) */                \
+    "v_readlane_b32 %[lfL], %[st], 28\n\t"                                                             \
+    "v_readlane_b32 %[lfR], %[st], 44\n\t"                                                             \
+    "s_mul_i32 %[o0], %[lfL], 192\n\t"                                                                 \
+    "s_mul_i32 %[o2], %[lfR], 192\n\t"                                                                 \
+    "s_mul_i32 %[of], %[lf], 192\n\t"                                                                  \
+    "buffer_load_dword %[n0], %[loff], %[rsrc], %[o0] offen\n\t"                                       \
+    "buffer_load_dword %[n1], %[loff], %[rsrc], %[o0] offen offset:192\n\t"                            \
+    "buffer_load_dword %[n2], %[loff], %[rsrc], %[o2] offen\n\t"                                       \
+    "buffer_load_dword %[n3], %[loff], %[rsrc], %[o2] offen offset:192\n\t"                            \
+    "buffer_load_dword %[f0], %[loff], %[rsrc], %[of] offen\n\t"                                       \
+    "buffer_load_dword %[f1], %[loff], %[rsrc], %[of] offen offset:192\n\t"                            \
+    /* the 36 planes of rows 0..2: distances, the DPP min/max fold */                                  \
+    "v_sub_f32 %[t], %[st], %[oA]\n\t"                                                                 \
+    "v_mul_f32 %[t], %[t], %[rdA]\n\t"                                                                 \
+    "s_nop 1\n\t"                                                                                      \
+    "v_min_f32_dpp %[t0a], %[t], %[t] quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"             \
+    "v_max_f32_dpp %[t1a], %[t], %[t] quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"             \
+    "s_nop 1\n\t"                                                                                      \
+    "v_max_f32_dpp %[m0], %[t0a], %[t0a] row_shr:4 row_mask:0xf bank_mask:0xf\n\t"                    \
+    "v_min_f32_dpp %[m1], %[t1a], %[t1a] row_shr:4 row_mask:0xf bank_mask:0xf\n\t"                    \
+    "s_nop 1\n\t"                                                                                      \
+    "v_max_f32_dpp %[m0], %[t0a], %[m0] row_shr:2 row_mask:0xf bank_mask:0xf\n\t"                     \
+    "v_min_f32_dpp %[m1], %[t1a], %[m1] row_shr:2 row_mask:0xf bank_mask:0xf\n\t"                     \
+    /* lanes 16r+4 / 16r+10: box 0 / box 1 of row r hit (m1 >= m0, m0 < depth, m1 > 0) */             \
+    "v_cmp_ge_f32_e64 %[h], %[m1], %[m0]\n\t"                                                          \
+    "v_cmp_gt_f32_e64 %[tt], %[depth], %[m0]\n\t"                                                      \
+    "s_and_b64 %[h], %[h], %[tt]\n\t"                                                                  \
+    "v_cmp_lt_f32_e64 %[tt], 0, %[m1]\n\t"                                                             \
+    "s_and_b64 %[h], %[h], %[tt]\n\t"
+
+/* closest hit: lanes 16r+10 of g: m0 of box 0 > m0 of box 1 (blasTrace's dn > df) */
+#define SURF_W2_ORDER                                                                                  \
+    "v_mov_b32_dpp %[mp], %[m0] row_shr:6 row_mask:0xf bank_mask:0xf\n\t"                              \
+    "v_cmp_gt_f32_e64 %[g], %[mp], %[m0]\n\t"
+
+/* level 1 (X's children, row 0): none hit -> pop; b0: both hit (far pushed); c: near child */
+#define SURF_W2_L1A                                                                                    \
+    "s_and_b64 %[a], %[h], %[m410]\n\t"                                                                \
+    "s_cbranch_scc0 L_pop_%=\n\t"                                                                      \
+    "s_cmp_eq_u64 %[a], %[m410]\n\t"                                                                   \
+    "s_cselect_b32 %[b0], 1, 0\n\t"                                                                    \
+    "s_cmp_eq_u64 %[a], 0x400\n\t"                                                                     \
+    "s_cselect_b32 %[c], 1, 0\n\t"
+/* closest hit, both hit: the nearer (swap when m0 of box 0 > m0 of box 1) */
+#define SURF_W2_L1ORDER                                                                                \
+    "s_bitcmp1_b64 %[g], 10\n\t"                                                                       \
+    "s_cselect_b32 %[idx], 1, 0\n\t"                                                                   \
+    "s_and_b32 %[idx], %[idx], %[b0]\n\t"                                                              \
+    "s_or_b32 %[c], %[c], %[idx]\n\t"
+/* near child C in row 1 + c; a leaf: push the far child, leave for C; else level 2 (row 1 + c) */
+#define SURF_W2_L2A                                                                                    \
+    "s_lshl_b32 %[k16], %[c], 4\n\t"                                                                   \
+    "s_add_u32 %[k16], %[k16], 16\n\t"                                                                 \
+    "s_add_u32 %[idx], %[k16], 13\n\t"                                                                 \
+    "v_readlane_b32 %[cnt], %[st], %[idx]\n\t"                                                         \
+    "s_cmp_lg_u32 %[c], 0\n\t"                                                                         \
+    "s_cselect_b64 %[sc], -1, 0\n\t"                                                                   \
+    "s_cmp_lg_u32 %[cnt], 0\n\t"                                                                       \
+    "s_cbranch_scc1 L_leafC_%=\n\t"                                                                    \
+    "s_lshr_b64 %[tt], %[h], %[k16]\n\t"                                                               \
+    "s_and_b64 %[a], %[tt], %[m410]\n\t"                                                               \
+    "s_cbranch_scc0 L_miss2_%=\n\t"                                                                    \
+    "s_cmp_eq_u64 %[a], %[m410]\n\t"                                                                   \
+    "s_cselect_b32 %[b1], 1, 0\n\t"                                                                    \
+    "s_cmp_eq_u64 %[a], 0x400\n\t"                                                                     \
+    "s_cselect_b32 %[cc], 1, 0\n\t"
+#define SURF_W2_L2ORDER                                                                                \
+    "s_lshr_b64 %[tt], %[g], %[k16]\n\t"                                                               \
+    "s_bitcmp1_b64 %[tt], 10\n\t"                                                                      \
+    "s_cselect_b32 %[idx], 1, 0\n\t"                                                                   \
+    "s_and_b32 %[idx], %[idx], %[b1]\n\t"                                                              \
+    "s_or_b32 %[cc], %[cc], %[idx]\n\t"
+/* descend to grandchild n[2c + cc]; push the far child f[1 - c] (b0) and the far
+ * grandchild n[2c + 1 - cc] (b1): slot 0 = b0 ? far child : far grandchild,
+ * slot 1 = far grandchild, the stack pointer advances by b0 + b1 entries */
+#define SURF_W2_TAIL                                                                                   \
+    "s_cmp_lg_u32 %[cc], 0\n\t"                                                                        \
+    "s_cselect_b64 %[scc], -1, 0\n\t"                                                                  \
+    "s_cmp_lg_u32 %[b0], 0\n\t"                                                                        \
+    "s_cselect_b64 %[sb0], -1, 0\n\t"                                                                  \
+    "s_add_u32 %[b1], %[b1], %[b0]\n\t"                                                                \
+    "s_lshl_b32 %[b1], %[b1], 8\n\t"                                                                   \
+    "v_add_u32 %[addr], %[sp], %[stk]\n\t"                                                             \
+    "s_waitcnt vmcnt(0)\n\t"                                                                           \
+    "v_cndmask_b32_e64 %[ta], %[n0], %[n1], %[scc]\n\t"                                                \
+    "v_cndmask_b32_e64 %[tb], %[n2], %[n3], %[scc]\n\t"                                                \
+    "v_cndmask_b32_e64 %[m0], %[n1], %[n0], %[scc]\n\t"                                                \
+    "v_cndmask_b32_e64 %[m1], %[n3], %[n2], %[scc]\n\t"                                                \
+    "v_cndmask_b32_e64 %[st], %[ta], %[tb], %[sc]\n\t"                                                 \
+    "v_cndmask_b32_e64 %[mp], %[m0], %[m1], %[sc]\n\t"                                                 \
+    "v_cndmask_b32_e64 %[t], %[f1], %[f0], %[sc]\n\t"                                                  \
+    "v_cndmask_b32_e64 %[sl0], %[mp], %[t], %[sb0]\n\t"                                                \
+    "ds_write2st64_b32 %[addr], %[sl0], %[mp] offset1:1\n\t"                                           \
+    "s_add_u32 %[sp], %[sp], %[b1]\n\t"                                                                \
+    "s_branch L_chk_%=\n"                                                                              \
+    /* C is a leaf: push the far child (when both were hit), leave for C */                            \
+    "L_leafC_%=:\n\t"                                                                                  \
+    "s_add_u32 %[idx], %[k16], 12\n\t"                                                                 \
+    "v_readlane_b32 %[lf], %[st], %[idx]\n\t"                                                          \
+    "v_add_u32 %[addr], %[sp], %[stk]\n\t"                                                             \
+    "s_waitcnt vmcnt(0)\n\t"                                                                           \
+    "s_cmp_eq_u32 %[b0], 0\n\t"                                                                        \
+    "s_cbranch_scc1 L_exit_%=\n\t"                                                                     \
+    "v_cndmask_b32_e64 %[t], %[f1], %[f0], %[sc]\n\t"                                                  \
+    "ds_write_b32 %[addr], %[t]\n\t"                                                                   \
+    "s_add_u32 %[sp], %[sp], 256\n\t"                                                                  \
+    "s_branch L_exit_%=\n"                                                                             \
+    /* both of C's children missed: the reference pushes the far child and pops   \
+     * it at once -- visit it (when hit), else pop */                                                  \
+    "L_miss2_%=:\n\t"                                                                                  \
+    "s_waitcnt vmcnt(0)\n\t"                                                                           \
+    "s_cmp_eq_u32 %[b0], 0\n\t"                                                                        \
+    "s_cbranch_scc1 L_pop_%=\n\t"                                                                      \
+    "v_cndmask_b32_e64 %[st], %[f1], %[f0], %[sc]\n\t"                                                 \
+    "s_nop 1\n\t"                                                                                      \
+    "s_branch L_chk_%=\n"                                                                              \
+    /* pop (every load of the visit has landed) */                                                     \
+    "L_pop_%=:\n\t"                                                                                    \
+    "s_waitcnt vmcnt(0)\n\t"                                                                           \
+    "s_cmp_eq_u32 %[sp], 0\n\t"                                                                        \
+    "s_cbranch_scc1 L_done_%=\n\t"                                                                     \
+    "s_sub_u32 %[sp], %[sp], 256\n\t"                                                                  \
+    "v_add_u32 %[addr], %[sp], %[stk]\n\t"                                                             \
+    "ds_read_b32 %[st], %[addr]\n\t"                                                                   \
+    "s_waitcnt lgkmcnt(0)\n\t"                                                                         \
+    "s_branch L_chk_%=\n"                                                                              \
+    "L_done_%=:\n\t"                                                                                   \
+    "s_mov_b32 %[cnt], 0\n"                                                                            \
+    "L_exit_%=:"
+
+#define SURF_W2_OPERANDS                                                                               \
+    : [st] "+v"(st), [sp] "+s"(spb), [lf] "=&s"(lf), [cnt] "=&s"(cnt), [n0] "=&v"(n0), [n1] "=&v"(n1),  \
+      [n2] "=&v"(n2), [n3] "=&v"(n3), [f0] "=&v"(f0), [f1] "=&v"(f1), [t] "=&v"(t), [t0a] "=&v"(t0a),    \
+      [t1a] "=&v"(t1a), [m0] "=&v"(m0), [m1] "=&v"(m1), [mp] "=&v"(mp), [ta] "=&v"(ta), [tb] "=&v"(tb),  \
+      [sl0] "=&v"(sl0), [addr] "=&v"(addr), [lfL] "=&s"(lfL), [lfR] "=&s"(lfR), [o0] "=&s"(o0),          \
+      [o2] "=&s"(o2), [of] "=&s"(of), [c] "=&s"(c), [cc] "=&s"(cc), [k16] "=&s"(k16), [idx] "=&s"(idx),   \
+      [b0] "=&s"(b0), [b1] "=&s"(b1), [h] "=&s"(h), [tt] "=&s"(tt), [g] "=&s"(g), [a] "=&s"(a),           \
+      [sc] "=&s"(sc), [scc] "=&s"(scc), [sb0] "=&s"(sb0)                                                 \
+    : [oA] "v"(oA), [rdA] "v"(rdA), [depth] "s"(depth), [rsrc] "s"(rsrc), [loff] "v"(laneOff),            \
+      [stk] "v"(stkLane), [m410] "s"(m410)                                                               \
+    : "memory", "scc"
+
+template <bool ANY>
+__device__ __forceinline__ void walk2Fin(float& st, uint32_t& spb, uint32_t& lf, uint32_t& cnt, float oA, float rdA, float depth,
+                                         surfI4 rsrc, uint32_t laneOff, uint32_t stkLane) {
+    float n0, n1, n2, n3, f0, f1, t, t0a, t1a, m0, m1, mp, ta, tb, sl0;
+    uint32_t addr, lfL, lfR, o0, o2, of, c, cc, k16, idx, b0, b1;
+    unsigned long long h, tt, g = 0, a, sc, scc, sb0;
+    const unsigned long long m410 = 0x410ull;
+    if (ANY) {
+        /* any-hit: no near/far order (the answer is an OR over the admitted
+         * leaves): box 0 first when hit, box 1 pushed when both hit */
+        asm volatile(SURF_W2_HEAD SURF_W2_L1A SURF_W2_L2A SURF_W2_TAIL SURF_W2_OPERANDS);
+    } else {
+        asm volatile(SURF_W2_HEAD SURF_W2_ORDER SURF_W2_L1A SURF_W2_L1ORDER SURF_W2_L2A SURF_W2_L2ORDER SURF_W2_TAIL
+                     SURF_W2_OPERANDS);
+    }
+}
+
+/* blasWalk with two-level visits (S.wnodes): the DFS below one BLAS root from
+ * W(root) -- its first visit re-tests the root's children at the current
+ * depth (the caller's entry test gave the same answer) and their children. */
+template <bool ANY>
+__device__ __forceinline__ bool blasWalk2(const DevScene& S, uint32_t nodeOff, const float4* tri, V3 o, V3 d, V3 rd, float& depth,
+                                          float& hu, float& hv, uint32_t& hprim, float* rs) {
+    const uint32_t lane = __lane_id(), l16 = lane & 15u;
+    const uint32_t ax = l16 < 12u ? (l16 % 6u) >> 1 : 0u;
+    const float oA = pick3(o, ax), rdA = pick3(rd, ax);
+    const float* wb = S.wnodes + 48u * (size_t)nodeOff;                 /* this BLAS's W records */
+    const uintptr_t nb = reinterpret_cast<uintptr_t>(wb);
+    const surfI4 rsrc = {(int)(uint32_t)nb, (int)(uint32_t)(nb >> 32), (int)((S.nWnodes - nodeOff) * 192u), 0x00020000};
+    const uint32_t laneOff = 4u * lane;
+    const uint32_t stkLane = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) float*)rs) + 4u * lane;
+    float st = loadEarly(wb + lane);                                     /* W(root) */
+    waitLoads(st);
+    uint32_t sp = 0u;
+    bool any = false;
+    for (;;) {
+        uint32_t lf, cnt;
+        const float dS = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(depth)));   /* wave-uniform */
+        walk2Fin<ANY>(st, sp, lf, cnt, oA, rdA, dS, rsrc, laneOff, stkLane);
+        if (cnt == 0u) return any;
+        if (leafWave<ANY>(tri, lf, cnt, o, d, depth, hu, hv, hprim)) {
+            if (ANY) return true;
+            any = true;
+        }
+        if (sp == 0u) return any;
+        sp -= 256u;
+        st = rs[sp / 4u + lane];
+    }
+}
+
+/* LDS prologue table of the wave traversal: 16 floats per instance */
 __device__ __forceinline__ uint32_t proWords(const DevScene& S) { return 16u * S.nInst; }
+
+/* Prologue entry of one instance (lane-parallel: one instance per lane): its
+ * object-space ray, 1/d, the slab ranges of its BLAS root's two children and
+ * the range of its conservative world box (the lane traversal's instance
+ * cull, traceScene; the full line when unusable), as blasWave forms them.
+ * None of it depends on depth: the depth tests are applied at the instance's
+ * turn.  Returns whether the instance can still yield a hit at `depth`. */
+__device__ __forceinline__ bool waveProEntry(const TraceInst& I, V3 o, V3 d, V3 rdw, bool cullOk, float depth, float4* p) {
+    float w0 = -kFarAway, w1 = kFarAway;
+    if (cullOk && I.wlo.w != 0.0f) {
+        const float tx0 = (I.wlo.x - o.x) * rdw.x, tx1 = (I.whi.x - o.x) * rdw.x;
+        const float ty0 = (I.wlo.y - o.y) * rdw.y, ty1 = (I.whi.y - o.y) * rdw.y;
+        const float tz0 = (I.wlo.z - o.z) * rdw.z, tz1 = (I.whi.z - o.z) * rdw.z;
+        w0 = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fminf(tz0, tz1));
+        w1 = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
+    }
+    V3 oo = mk3(rowDot(I.m0, o.x, o.y, o.z, 1.0f), rowDot(I.m1, o.x, o.y, o.z, 1.0f), rowDot(I.m2, o.x, o.y, o.z, 1.0f));
+    if (!I.meta.z) oo = divs(oo, rowDot(I.m3, o.x, o.y, o.z, 1.0f));
+    const V3 dd = mk3(rowDot(I.m0, d.x, d.y, d.z, 0.0f), rowDot(I.m1, d.x, d.y, d.z, 0.0f), rowDot(I.m2, d.x, d.y, d.z, 0.0f));
+    const V3 rd = mk3(1.0f / dd.x, 1.0f / dd.y, 1.0f / dd.z);
+    float a0, a1, b0, b1;
+    slabRange(I.r0, I.r1, oo, rd, a0, a1);
+    slabRange(I.r2, I.r3, oo, rd, b0, b1);
+    p[0] = make_float4(oo.x, oo.y, oo.z, a0);
+    p[1] = make_float4(dd.x, dd.y, dd.z, a1);
+    p[2] = make_float4(rd.x, rd.y, rd.z, b0);
+    p[3] = make_float4(b1, w0, w1, 0.0f);
+    /* a root child that misses at this depth misses at every later (smaller)
+     * depth too; root leaves are always taken */
+    const bool wMiss = w1 < w0 || w1 < 0.0f || w0 >= depth;
+    return !wMiss && (f2u(I.r1.w) != 0u || slabHit(a0, a1, depth) != kFarAway || slabHit(b0, b1, depth) != kFarAway);
+}
+
+/* The one-level walk (no two-level records, or a non-finite ray / box). */
+template <bool ANY>
+__device__ __forceinline__ bool blasWalkFallback(const DevScene& S, uint32_t nodeOff, const float4* tri, V3 o, V3 d, V3 rd, float dn, float df,
+                                              uint32_t cn, uint32_t cf, float& depth, float& hu, float& hv, uint32_t& hprim, float* rs,
+                                              SegStats* ss, bool fin) {
+    return fin ? blasWalk<ANY, true>(S, nodeOff, tri, o, d, rd, dn, df, cn, cf, depth, hu, hv, hprim, rs, ss)
+               : blasWalk<ANY, false>(S, nodeOff, tri, o, d, rd, dn, df, cn, cf, depth, hu, hv, hprim, rs, ss);
+}
+
+/* Instance::intersect(Any) (bvh.cpp:481-513) of one instance at its turn, from
+ * its prologue entry pk (LDS, one address for the wave: a broadcast): the
+ * world-box cull and the root children's depth tests at the current depth,
+ * then the BLAS walk (or the root leaf's triangles). */
+template <bool ANY>
+__device__ __forceinline__ bool waveInstance(const DevScene& S, const TraceInst& I, const float4* pk, float& depth, float& hu,
+                                             float& hv, uint32_t& hprim, float* rs, SegStats* ss) {
+    /* wave-uniform (the tables may be read through a generic pointer: LDS or global) */
+    const uint32_t nodeOff = (uint32_t)__builtin_amdgcn_readfirstlane((int)I.meta.x);
+    const float4* tri = S.tris + 3u * (uint32_t)__builtin_amdgcn_readfirstlane((int)I.meta.y);
+    const uint32_t rlf = (uint32_t)__builtin_amdgcn_readfirstlane((int)f2u(I.r0.w));
+    const uint32_t rcnt = (uint32_t)__builtin_amdgcn_readfirstlane((int)f2u(I.r1.w));
+    const float4 q0 = pk[0], q1 = pk[1], q2 = pk[2], q3 = pk[3];
+    if (q3.z < q3.y || q3.z < 0.0f || q3.y >= depth) return false;   /* world-box cull at the current depth */
+    const V3 ok = xyz(q0);
+    const V3 dk = xyz(q1);
+    if (rcnt != 0u) return leafWave<ANY>(tri, rlf, rcnt, ok, dk, depth, hu, hv, hprim);
+    /* root: never box-tested (bvh.cpp:131); its children's boxes are in its record */
+    float dn = slabHit(q0.w, q1.w, depth);
+    float df = slabHit(q2.w, q3.x, depth);
+    uint32_t cn = nodeOff + rlf, cf = cn + 1u;
+    if (dn > df) { const float t = dn; dn = df; df = t; const uint32_t c = cn; cn = cf; cf = c; }
+    if (dn == kFarAway) return false;
+    const V3 rk = xyz(q2);
+    const bool fin = S.finiteBoxes && finite3(ok) && finite3(rk);
+    if (fin && S.wnodes) return blasWalk2<ANY>(S, nodeOff, tri, ok, dk, rk, depth, hu, hv, hprim, rs);
+    return blasWalkFallback<ANY>(S, nodeOff, tri, ok, dk, rk, dn, df, cn, cf, depth, hu, hv, hprim, rs, ss, fin);
+}
+
+/* BvhTLAS::intersect / intersectAny (bvh.cpp:654-778) for any TLAS: the
+ * prologue entries of every instance first (64 lanes at a time, by instance
+ * id), then the reference's TLAS DFS on the wave -- the node record's 12
+ * planes in lanes (slabPair: the ternary min/max in its operand order), near
+ * child first, the far child pushed when hit (a stack of node indices, entry
+ * k in lane k of one VGPR), a leaf's instances in index order, each at its
+ * turn with the depth the earlier ones left (waveInstance). */
+template <bool ANY>
+__device__ __forceinline__ bool traceWaveTlas(const DevScene& S, const TraceTables& Tt, V3 o, V3 d, float& depth, float& hu,
+                                              float& hv, uint32_t& hinst, uint32_t& hprim, float* rs, float4* pro, SegStats* ss) {
+    const uint32_t lane = __lane_id();
+    const V3 rdw = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    const bool cullOk = finite3(o) && finite3(rdw);
+    for (uint32_t b = 0; b < S.nInst; b += 64u)
+        if (b + lane < S.nInst) (void)waveProEntry(Tt.inst[b + lane], o, d, rdw, cullOk, depth, pro + 4u * (b + lane));
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_s_waitcnt(0xc07f);              /* the entries are in LDS before any lane reads another's */
+    const float* nodesF = reinterpret_cast<const float*>(S.tlasNodes);
+    const uint32_t dw = planeDword(lane), ax = lane < 12u ? (lane % 6u) >> 1 : 0u;
+    const float oA = pick3(o, ax), rdA = pick3(rdw, ax);
+    bool any = false;
+    uint32_t node = 0u, tsp = 0u;
+    int tstk = 0;                                     /* TLAS stack: entry k in lane k */
+    for (;;) {
+        const float rec = nodesF[16u * node + dw];
+        const uint32_t lf = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(rec), 12);
+        const uint32_t cnt = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(rec), 13);
+        if (cnt != 0u) {
+            for (uint32_t k = 0; k < cnt; ++k) {
+                const uint32_t ii = Tt.order[lf + k];
+                if (waveInstance<ANY>(S, Tt.inst[ii], pro + 4u * ii, depth, hu, hv, hprim, rs, ss)) {
+                    if (ANY) return true;
+                    any = true;
+                    hinst = ii;
+                }
+            }
+            if (tsp == 0u) break;
+            node = (uint32_t)__builtin_amdgcn_readlane(tstk, (int)--tsp);
+            continue;
+        }
+        float dn, df;
+        slabPair(rec, oA, rdA, depth, dn, df);
+        uint32_t cn = lf, cf = lf + 1u;
+        if (dn > df) { const float t = dn; dn = df; df = t; const uint32_t c = cn; cn = cf; cf = c; }
+        if (dn == kFarAway) {
+            if (tsp == 0u) break;
+            node = (uint32_t)__builtin_amdgcn_readlane(tstk, (int)--tsp);
+        } else {
+            node = cn;
+            if (df != kFarAway) {
+                if (lane == tsp) tstk = (int)cf;
+                ++tsp;
+            }
+        }
+    }
+    return any;
+}
+
+/* BvhTLAS::intersect / intersectAny on the wave (bvh.cpp:654-778).  A
+ * single-leaf TLAS of <= 64 instances (the bundled scene) takes the fast
+ * path: lane k forms the prologue entry of the k-th instance in TLAS order,
+ * the instances whose entry can still hit are taken in that order, each
+ * applying the depth tests at its turn (a missed instance costs a few
+ * readlanes instead of a serial transform, three divisions and a slab test).
+ * Any other TLAS: traceWaveTlas. */
 template <bool ANY>
 __device__ __forceinline__ bool traceWave(const DevScene& S, const TraceTables& Tt, V3 o, V3 d, float& depth, float& hu,
                                           float& hv, uint32_t& hinst, uint32_t& hprim, float* rs, float4* pro, SegStats* ss = nullptr) {
     bool any = false;
     const uint32_t nI = S.tlasLeafCount;
-    if (nI > 64u) {
-        for (uint32_t k = 0; k < nI; ++k) {
-            const uint32_t ii = Tt.order[k];
-            const TraceInst& I = Tt.inst[ii];
-            V3 oo = mk3(rowDot(I.m0, o.x, o.y, o.z, 1.0f), rowDot(I.m1, o.x, o.y, o.z, 1.0f), rowDot(I.m2, o.x, o.y, o.z, 1.0f));
-            if (!I.meta.z) oo = divs(oo, rowDot(I.m3, o.x, o.y, o.z, 1.0f));
-            const V3 dd = mk3(rowDot(I.m0, d.x, d.y, d.z, 0.0f), rowDot(I.m1, d.x, d.y, d.z, 0.0f), rowDot(I.m2, d.x, d.y, d.z, 0.0f));
-            if (blasWave<ANY>(S, I, oo, dd, depth, hu, hv, hprim, rs, ss)) {
-                if (ANY) return true;
-                any = true;
-                hinst = ii;
-            }
-        }
-        return any;
-    }
+    if (nI == 0u || nI > 64u) return traceWaveTlas<ANY>(S, Tt, o, d, depth, hu, hv, hinst, hprim, rs, pro, ss);
 #if SURF_SEG_TIMING
     unsigned long long t0 = segClock();
 #endif
     const uint32_t lane = __lane_id();
-    /* lane k: instance k's object-space ray, 1/d and root-children ranges, kept
-     * in the LDS prologue table (not in registers through the walk) */
-    bool keep = false;
-    /* the lane traversal's instance cull (traceScene): an instance whose
-     * conservative world box the ray misses within [0, depth) holds no
-     * triangle that can yield an accepted hit -- here also for root-leaf
-     * instances (the room's walls), which otherwise cost a triangle test and
-     * its loads every segment */
+    /* lane k: the k-th instance's entry, kept in the LDS prologue table (not
+     * in registers through the walk); root-leaf instances (the room's walls)
+     * are culled by their world box too, which otherwise cost a triangle test
+     * and its loads every segment */
     const V3 rdw = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     const bool cullOk = finite3(o) && finite3(rdw);
-    if (lane < nI) {
-        const TraceInst& I = Tt.inst[Tt.order[lane]];
-        float w0 = -kFarAway, w1 = kFarAway;          /* world-box range; the full line when unusable */
-        if (cullOk && I.wlo.w != 0.0f) {
-            const float tx0 = (I.wlo.x - o.x) * rdw.x, tx1 = (I.whi.x - o.x) * rdw.x;
-            const float ty0 = (I.wlo.y - o.y) * rdw.y, ty1 = (I.whi.y - o.y) * rdw.y;
-            const float tz0 = (I.wlo.z - o.z) * rdw.z, tz1 = (I.whi.z - o.z) * rdw.z;
-            w0 = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fminf(tz0, tz1));
-            w1 = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
-        }
-        V3 oo = mk3(rowDot(I.m0, o.x, o.y, o.z, 1.0f), rowDot(I.m1, o.x, o.y, o.z, 1.0f), rowDot(I.m2, o.x, o.y, o.z, 1.0f));
-        if (!I.meta.z) oo = divs(oo, rowDot(I.m3, o.x, o.y, o.z, 1.0f));
-        const V3 dd = mk3(rowDot(I.m0, d.x, d.y, d.z, 0.0f), rowDot(I.m1, d.x, d.y, d.z, 0.0f), rowDot(I.m2, d.x, d.y, d.z, 0.0f));
-        const V3 rd = mk3(1.0f / dd.x, 1.0f / dd.y, 1.0f / dd.z);
-        float a0, a1, b0, b1;
-        slabRange(I.r0, I.r1, oo, rd, a0, a1);
-        slabRange(I.r2, I.r3, oo, rd, b0, b1);
-        /* candidates: a root child that misses at the entry depth misses at
-         * every later (smaller) depth too; root leaves are always taken */
-        const bool wMiss = w1 < w0 || w1 < 0.0f || w0 >= depth;
-        keep = !wMiss && (f2u(I.r1.w) != 0u || slabHit(a0, a1, depth) != kFarAway || slabHit(b0, b1, depth) != kFarAway);
-        float4* p = pro + 4u * lane;
-        p[0] = make_float4(oo.x, oo.y, oo.z, a0);
-        p[1] = make_float4(dd.x, dd.y, dd.z, a1);
-        p[2] = make_float4(rd.x, rd.y, rd.z, b0);
-        p[3] = make_float4(b1, w0, w1, 0.0f);
-    }
+    bool keep = false;
+    if (lane < nI) keep = waveProEntry(Tt.inst[Tt.order[lane]], o, d, rdw, cullOk, depth, pro + 4u * lane);
     unsigned long long cand = __ballot(keep);
     while (cand) {
         const uint32_t k = (uint32_t)(__ffsll((long long)cand) - 1);
         cand &= cand - 1ull;
         const uint32_t ii = Tt.order[k];
-        const TraceInst& I = Tt.inst[ii];
-        const uint32_t nodeOff = I.meta.x;
-        const float4* tri = S.tris + 3u * I.meta.y;
-        const uint32_t rlf = f2u(I.r0.w), rcnt = f2u(I.r1.w);
-        const float4* pk = pro + 4u * k;                    /* one address for the wave: an LDS broadcast */
-        const float4 q0 = pk[0], q1 = pk[1], q2 = pk[2], q3 = pk[3];
-        if (q3.z < q3.y || q3.z < 0.0f || q3.y >= depth) continue;   /* world-box cull at the current depth */
-        float dn = 0.0f, df = 0.0f;
-        uint32_t cn = nodeOff + rlf, cf = cn + 1u;
-        if (rcnt == 0u) {
-            /* root: never box-tested (bvh.cpp:131); its children's boxes are in its record */
-            dn = slabHit(q0.w, q1.w, depth);
-            df = slabHit(q2.w, q3.x, depth);
-            if (dn > df) { const float t = dn; dn = df; df = t; const uint32_t c = cn; cn = cf; cf = c; }
-            if (dn == kFarAway) continue;
-        }
-        const V3 ok = xyz(q0);
-        const V3 dk = xyz(q1);
 #if SURF_SEG_TIMING
         if (ss) { const unsigned long long t1 = segClock(); ss->cycInst += t1 - t0; t0 = t1; }
 #endif
-        bool h;
-        if (rcnt != 0u) {
-            h = leafWave<ANY>(tri, rlf, rcnt, ok, dk, depth, hu, hv, hprim);
-        } else {
-            const V3 rk = xyz(q2);
-            h = (S.finiteBoxes && finite3(ok) && finite3(rk))
-                    ? blasWalk<ANY, true>(S, nodeOff, tri, ok, dk, rk, dn, df, cn, cf, depth, hu, hv, hprim, rs, ss)
-                    : blasWalk<ANY, false>(S, nodeOff, tri, ok, dk, rk, dn, df, cn, cf, depth, hu, hv, hprim, rs, ss);
-        }
+        const bool h = waveInstance<ANY>(S, Tt.inst[ii], pro + 4u * k, depth, hu, hv, hprim, rs, ss);
 #if SURF_SEG_TIMING
         if (ss) { const unsigned long long t1 = segClock(); ss->cycLoop += t1 - t0; t0 = t1; }
 #endif
@@ -1425,6 +1716,29 @@ __device__ __forceinline__ void stageTables(const DevScene& S, DevInstance* sIns
     for (uint32_t k = threadIdx.x; k < nM; k += blockDim.x) reinterpret_cast<float4*>(sMat)[k] = reinterpret_cast<const float4*>(S.mats)[k];
     for (uint32_t k = threadIdx.x; k < S.nLights; k += blockDim.x) sLights[k] = S.lights[k];
     __syncthreads();
+}
+
+/* The cooperative (one path per wave) kernels stage the trace and shading
+ * tables in LDS when they fit; with more instances / materials / lights they
+ * read them from global memory (wave-uniform reads).  The host sizes the
+ * dynamic LDS the same way (surf_hip.hip coopLds / coopTailLds). */
+/* (a compile-time choice: through a pointer that may be LDS or global, a
+ * table load is a flat load the compiler cannot prove wave-uniform, and the
+ * walk's scalar operands derive from those loads) */
+template <bool LDS>
+__device__ __forceinline__ TraceTables coopTrace(const DevScene& S, uint32_t* lds, uint32_t words) {
+    if (LDS) return stageTrace(S, lds, words);
+    return TraceTables{S.tinst, S.tlasIdx};
+}
+/* shading tables at LDS word `at` (16-B aligned) when they fit */
+template <bool LDS>
+__device__ __forceinline__ ShadeTables coopShade(const DevScene& S, uint32_t* lds, uint32_t at) {
+    if (!LDS) return ShadeTables{S.inst, S.mats, S.lights};
+    DevInstance* const sInst = reinterpret_cast<DevInstance*>(lds + at);
+    DevMaterial* const sMat = reinterpret_cast<DevMaterial*>(sInst + S.nInst);
+    uint2* const sLights = reinterpret_cast<uint2*>(sMat + S.nMats);
+    stageTables(S, sInst, sMat, sLights);            /* ends with a barrier */
+    return ShadeTables{sInst, sMat, sLights};
 }
 
 /* Next-event estimation of one diffuse bounce (Scene::sampleLights +
@@ -1887,19 +2201,15 @@ __global__ __launch_bounds__(64, SURF_TAIL_WAVES) void k_tail(DevScene S, Pool c
  * (stackWords = 16 x depth words), then the trace tables; the shading tables
  * are read from global memory (wave-uniform reads): LDS copies would cap the
  * one-wave blocks at ~2 waves per SIMD. */
+template <bool LDS>
 __global__ __launch_bounds__(64, SURF_COOP_WAVES) void k_tail_coop(DevScene S, Pool cur, uint32_t n, float4* __restrict__ rad,
                                                   uint32_t* __restrict__ frameDone, uint32_t npx, uint32_t window, Counters* C,
                                                   uint32_t stackWords, uint32_t firstCounted) {
     extern __shared__ uint32_t lds[];
-    const TraceTables Tt = stageTrace(S, lds, stackWords + proWords(S));
+    const TraceTables Tt = coopTrace<LDS>(S, lds, stackWords + proWords(S));
     /* shading's instance / material / light tables in LDS too: a path's
      * segments read them on its dependent chain (the drain's latency floor) */
-    uint32_t* const shw = lds + ((stackWords + proWords(S) + S.nInst * (uint32_t)((sizeof(TraceInst) + 4u) / 4u) + 3u) & ~3u);
-    DevInstance* const sInst = reinterpret_cast<DevInstance*>(shw);
-    DevMaterial* const sMat = reinterpret_cast<DevMaterial*>(sInst + S.nInst);
-    uint2* const sLights = reinterpret_cast<uint2*>(sMat + S.nMats);
-    stageTables(S, sInst, sMat, sLights);
-    const ShadeTables Tb{sInst, sMat, sLights};
+    const ShadeTables Tb = coopShade<LDS>(S, lds, (stackWords + proWords(S) + S.nInst * (uint32_t)((sizeof(TraceInst) + 4u) / 4u) + 3u) & ~3u);
     const uint32_t i = blockIdx.x;
     if (i >= n) return;
     const bool lead = threadIdx.x == 0;
@@ -2084,6 +2394,7 @@ __device__ __forceinline__ void pairPath(const DevScene& S, const TraceTables& T
     }
 }
 
+template <bool LDS>
 __global__ __launch_bounds__(128, SURF_COOP_WAVES) void k_tail_pair(DevScene S, Pool cur, uint32_t n, float4* __restrict__ rad,
                                                    uint32_t* __restrict__ frameDone, uint32_t npx, uint32_t window, Counters* C,
                                                    uint32_t stackWords, uint32_t firstCounted) {
@@ -2091,17 +2402,13 @@ __global__ __launch_bounds__(128, SURF_COOP_WAVES) void k_tail_pair(DevScene S, 
     __shared__ PairBox box;
     /* LDS: [record stack | prologue table] per wave, then the trace tables and the shading tables */
     const uint32_t per = stackWords + proWords(S);
-    const TraceTables Tt = stageTrace(S, lds, 2u * per);
-    uint32_t* const shw = lds + ((2u * per + S.nInst * (uint32_t)((sizeof(TraceInst) + 4u) / 4u) + 3u) & ~3u);
-    DevInstance* const sInst = reinterpret_cast<DevInstance*>(shw);
-    DevMaterial* const sMat = reinterpret_cast<DevMaterial*>(sInst + S.nInst);
-    uint2* const sLights = reinterpret_cast<uint2*>(sMat + S.nMats);
     if (threadIdx.x < 2u) {
         box.run[threadIdx.x] = 1u; box.help[threadIdx.x] = 0u;
         box.post[threadIdx.x] = 0u; box.done[threadIdx.x] = 0u; box.occ[threadIdx.x] = 0u;
     }
-    stageTables(S, sInst, sMat, sLights);            /* ends with a barrier */
-    const ShadeTables Tb{sInst, sMat, sLights};
+    const TraceTables Tt = coopTrace<LDS>(S, lds, 2u * per);
+    const ShadeTables Tb = coopShade<LDS>(S, lds, (2u * per + S.nInst * (uint32_t)((sizeof(TraceInst) + 4u) / 4u) + 3u) & ~3u);
+    __syncthreads();                                  /* the mailboxes are initialised (global tables: no staging barrier) */
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   /* wave-uniform: the walk's LDS bases are scalar */
     const bool lead = (threadIdx.x & 63u) == 0u;
     float* rstk = reinterpret_cast<float*>(lds + w * per);
@@ -2245,11 +2552,12 @@ __global__ __launch_bounds__(kBlock) void k_trace_any(DevScene S, const float* _
 /* Cooperative traversal entry points (one ray per 64-lane block, the
  * lanes-as-planes traversal of the cooperative tail): the same results as
  * k_trace_closest / k_trace_any, for parity tests and latency measurements. */
+template <bool LDS>
 __global__ __launch_bounds__(64) void k_trace_closest_coop(DevScene S, const float* __restrict__ o, const float* __restrict__ d,
                                                            uint32_t n, float4* __restrict__ tuv, uint2* __restrict__ ip,
                                                            uint32_t stackWords) {
     extern __shared__ uint32_t lds[];
-    const TraceTables Tt = stageTrace(S, lds, stackWords + proWords(S));
+    const TraceTables Tt = coopTrace<LDS>(S, lds, stackWords + proWords(S));
     const uint32_t i = blockIdx.x;
     if (i >= n) return;
     float depth = kFarAway, u = 0.0f, v = 0.0f;
@@ -2262,11 +2570,12 @@ __global__ __launch_bounds__(64) void k_trace_closest_coop(DevScene S, const flo
         ip[i] = make_uint2(hit ? inst : kUnset, hit ? prim : kUnset);
     }
 }
+template <bool LDS>
 __global__ __launch_bounds__(64) void k_trace_any_coop(DevScene S, const float* __restrict__ o, const float* __restrict__ d,
                                                        const float* __restrict__ tmaxv, uint32_t n, uint8_t* __restrict__ occ,
                                                        uint32_t stackWords) {
     extern __shared__ uint32_t lds[];
-    const TraceTables Tt = stageTrace(S, lds, stackWords + proWords(S));
+    const TraceTables Tt = coopTrace<LDS>(S, lds, stackWords + proWords(S));
     const uint32_t i = blockIdx.x;
     if (i >= n) return;
     const V3 ro = mk3(o[3 * i], o[3 * i + 1], o[3 * i + 2]), rdir = mk3(d[3 * i], d[3 * i + 1], d[3 * i + 2]);

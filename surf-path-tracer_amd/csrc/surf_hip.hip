@@ -116,7 +116,7 @@ struct surf_ctx {
     uint32_t coopMax = 0;          /* survivors handled by the cooperative tail (one path per wave) */
     uint32_t coopAll = 150000;     /* drain paths left to the cooperative tail (surf_set_tail_coop); C3 drain 176-184 ms at 60000, 172-178 at 150000 */
     int drainReplays = 1;          /* graph replays per host poll while draining (SURF_DRAIN_REPLAYS) */
-    bool coopEligible = false;     /* single-leaf TLAS of <= 64 instances, LDS tables */
+    bool coopEligible = false;     /* single-leaf TLAS of <= 64 instances, LDS tables (the four-rows engine) */
     int traceMode = 0;             /* surf_trace_closest/_any: 0 one ray per lane, 1 one ray per wave, 2 one ray per 16-lane row */
     bool tailRows = false;         /* drain on k_tail_rows (four paths per wave; SURF_TAIL_ROWS=1) instead of k_tail_coop */
     bool tailPair = true;          /* cooperative drain on k_tail_pair (partner waves trace the shadow rays; SURF_TAIL_PAIR=0: k_tail_coop) */
@@ -190,8 +190,9 @@ void destroyGraph(surf_ctx* c) {
 /* Dynamic LDS of a traversal kernel with `block` threads: the per-lane stack,
  * then (LDS tables) the TraceInst table and the TLAS index array. */
 uint32_t stackWords(const surf_ctx* c, uint32_t block) { return c->stackDepth * block; }
-/* one-ray-per-wave traversal (traceWave): a stack of node records, 16 words per entry */
-uint32_t recStackWords(const surf_ctx* c) { return c->stackDepth * 16u; }
+/* one-ray-per-wave traversal (traceWave): a stack of node records, 16 words per
+ * entry -- 64 with two-level records (blasWalk2 pushes whole W records) */
+uint32_t recStackWords(const surf_ctx* c) { return c->stackDepth * (c->S.wnodes ? 64u : 16u); }
 /* Dynamic LDS of the four-rows kernels: four record stacks, then the trace tables. */
 size_t rowsLds(const surf_ctx* c) {
     return ((size_t)4 * recStackWords(c) + kRowProWords) * sizeof(float) + (size_t)c->nInstances * (sizeof(TraceInst) + sizeof(uint32_t));
@@ -199,10 +200,13 @@ size_t rowsLds(const surf_ctx* c) {
 /* Dynamic LDS of the one-ray-per-wave kernels: the record stack, the prologue
  * table (16 words per instance), then the trace tables; k_tail_coop adds the
  * shading tables (coopTailLds). */
+/* (tables staged only when they fit: coopLdsTables in the kernels) */
 size_t coopLds(const surf_ctx* c) {
-    return ((size_t)recStackWords(c) + 16u * c->nInstances) * sizeof(float) + (size_t)c->nInstances * (sizeof(TraceInst) + sizeof(uint32_t));
+    return ((size_t)recStackWords(c) + 16u * c->nInstances) * sizeof(float) +
+           (c->ldsTables ? (size_t)c->nInstances * (sizeof(TraceInst) + sizeof(uint32_t)) : 0);
 }
 size_t coopTailLds(const surf_ctx* c) {
+    if (!c->ldsTables) return coopLds(c);
     return ((coopLds(c) + 15) & ~(size_t)15) + (size_t)c->nInstances * sizeof(DevInstance) + (size_t)c->nMaterials * sizeof(DevMaterial) +
            (size_t)c->nLightsUp * sizeof(uint2);
 }
@@ -210,6 +214,8 @@ size_t coopTailLds(const surf_ctx* c) {
 size_t pairTailLds(const surf_ctx* c) {
     return coopTailLds(c) + ((size_t)recStackWords(c) + 16u * c->nInstances) * sizeof(float);
 }
+/* the one-ray-per-wave kernels' LDS: stack + prologue table per wave (+ tables) within 64 KiB */
+bool coopLdsOk(const surf_ctx* c) { return pairTailLds(c) <= 65536; }
 size_t traversalLds(const surf_ctx* c, uint32_t block) {
     size_t b = (size_t)stackWords(c, block) * sizeof(uint32_t);
     if (c->ldsTables) b += (size_t)c->nInstances * (sizeof(TraceInst) + sizeof(uint32_t));
@@ -227,7 +233,7 @@ struct TreeWalk {
 };
 
 TreeWalk walkTree(const surf_bvh_node* nodes, uint32_t nodeCount, uint32_t offset, uint32_t idxCount, uint32_t idxOffset,
-                  std::vector<float4>& out, std::vector<uint8_t>& leafSeen) {
+                  std::vector<float4>& out, std::vector<uint8_t>& leafSeen, std::vector<uint32_t>* owner = nullptr) {
     TreeWalk w;
     std::vector<std::pair<uint32_t, uint32_t>> st{{0u, 0u}};
     size_t visits = 0;
@@ -239,6 +245,7 @@ TreeWalk walkTree(const surf_bvh_node* nodes, uint32_t nodeCount, uint32_t offse
         if (g >= nodeCount) { w.ok = false; w.why = "BVH node index out of range"; return w; }
         const surf_bvh_node& n = nodes[g];
         float4* rec = &out[4 * g];
+        if (owner) (*owner)[g] = offset;
         rec[0].w = u2f(n.left_first);
         rec[1].w = u2f(n.count);
         if (n.count != 0) {
@@ -572,9 +579,11 @@ void launchTail(surf_ctx* c, Pool in, uint32_t n, uint32_t lpw, uint32_t firstCo
  * segment -- the quantity the last paths of a drain are bound by. */
 /* The cooperative drain uses the lanes-as-planes wave traversal (traceWave):
  * single-leaf TLAS of <= 64 instances, stack of node records in 64 lanes. */
-bool waveEligible(const surf_ctx* c) { return c->coopEligible && c->stackDepth <= 64; }
-/* The four-rows traversal: as the wave traversal, with at most one instance per lane of a row. */
-bool rowsEligible(const surf_ctx* c) { return waveEligible(c) && c->S.tlasLeafCount <= kRowInst; }
+/* Any TLAS (traceWaveTlas walks one whose root splits or that holds > 64
+ * instances); the TLAS stack is one VGPR (<= 64 entries). */
+bool waveEligible(const surf_ctx* c) { return c->hasScene && c->stackDepth <= 64 && coopLdsOk(c); }
+/* The four-rows traversal: a single-leaf TLAS with at most one instance per lane of a row, LDS tables. */
+bool rowsEligible(const surf_ctx* c) { return waveEligible(c) && c->coopEligible && c->S.tlasLeafCount <= kRowInst; }
 
 /* Regen counted each pool-0 path's next extension ray (firstCounted). */
 int runTail(surf_ctx* c) {
@@ -610,18 +619,20 @@ int runTail(surf_ctx* c) {
              * taking paths from the queue; idle waves trace their sibling's
              * shadow rays once the queue is empty */
             int per = 0;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_tail_pair, 128, pairTailLds(c)) != hipSuccess || per < 1)
+            auto kern = c->ldsTables ? k_tail_pair<true> : k_tail_pair<false>;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, 128, pairTailLds(c)) != hipSuccess || per < 1)
                 per = 2 * SURF_COOP_WAVES;
             const uint32_t blocks = std::max<uint32_t>(1u, std::min<uint32_t>((cnt + 1u) / 2u, c->cus * (uint32_t)per));
             SURF_CHECK(c, hipMemsetAsync(&c->ctr->rowNext, 0, sizeof(uint32_t), c->stream));
-            hipLaunchKernelGGL(k_tail_pair, dim3(blocks), dim3(128), pairTailLds(c), c->stream, c->S, in, cnt, c->rad, c->frameDone,
+            hipLaunchKernelGGL(kern, dim3(blocks), dim3(128), pairTailLds(c), c->stream, c->S, in, cnt, c->rad, c->frameDone,
                                c->npx, c->window, c->ctr, recStackWords(c), firstCounted);
             SURF_CHECK(c, hipGetLastError());
             c->stats.tail_survivors += cnt;
             break;
         }
         if (waveEligible(c) && cnt <= c->coopAll) {
-            hipLaunchKernelGGL(k_tail_coop, dim3(cnt), dim3(64), coopTailLds(c), c->stream, c->S, in, cnt, c->rad, c->frameDone,
+            hipLaunchKernelGGL(c->ldsTables ? k_tail_coop<true> : k_tail_coop<false>, dim3(cnt), dim3(64), coopTailLds(c), c->stream,
+                               c->S, in, cnt, c->rad, c->frameDone,
                                c->npx, c->window, c->ctr, recStackWords(c), firstCounted);
             SURF_CHECK(c, hipGetLastError());
             c->stats.tail_survivors += cnt;
@@ -952,7 +963,7 @@ int surf_set_trace_mode(surf_ctx* c, int mode) {
     if (!c) return fail(nullptr, SURF_ERR_INVALID, "ctx is NULL");
     if (mode < 0 || mode > 2) return fail(c, SURF_ERR_INVALID, "trace mode must be 0, 1 or 2");
     if (mode == 1 && !waveEligible(c))
-        return fail(c, SURF_ERR_INVALID, "one-ray-per-wave traversal needs a single-leaf TLAS of <= 64 instances and a BVH stack <= 64");
+        return fail(c, SURF_ERR_INVALID, "one-ray-per-wave traversal needs a BVH stack <= 64 entries");
     if (mode == 2 && !rowsEligible(c))
         return fail(c, SURF_ERR_INVALID, "one-ray-per-row traversal needs a single-leaf TLAS of <= 16 instances and a BVH stack <= 64");
     c->traceMode = mode;
@@ -1108,6 +1119,7 @@ int surf_upload_scene(surf_ctx* c, const surf_scene_desc* d) {
     std::vector<int64_t> idxTri(d->blas_index_count, -1);   /* idx slot -> tri offset owner */
     std::vector<float4> nodes((size_t)d->blas_node_count * 4, make_float4(0, 0, 0, 0));
     std::vector<uint8_t> seen(d->blas_index_count, 0), walked(d->blas_node_count, 0);
+    std::vector<uint32_t> owner(d->blas_node_count, kUnset);    /* BLAS node offset of every reachable node */
     uint32_t maxBlasDepth = 0;
     for (uint32_t i = 0; i < d->instance_count; ++i) {
         const surf_gpu_instance& g = d->instances[i];
@@ -1125,7 +1137,8 @@ int surf_upload_scene(surf_ctx* c, const surf_scene_desc* d) {
         D.affine = affine(g.transform) ? 1u : 0u;
         if (!walked[g.bvh_node_offset]) {
             std::vector<uint8_t> leaf(d->blas_index_count, 0);
-            TreeWalk w = walkTree(d->blas_nodes, d->blas_node_count, g.bvh_node_offset, d->blas_index_count, g.bvh_idx_offset, nodes, leaf);
+            TreeWalk w = walkTree(d->blas_nodes, d->blas_node_count, g.bvh_node_offset, d->blas_index_count, g.bvh_idx_offset, nodes, leaf,
+                                  &owner);
             if (!w.ok) return fail(c, SURF_ERR_INVALID, "instance " + std::to_string(i) + ": " + w.why);
             maxBlasDepth = std::max(maxBlasDepth, w.depth);
             walked[g.bvh_node_offset] = 1;
@@ -1192,6 +1205,34 @@ int surf_upload_scene(surf_ctx* c, const surf_scene_desc* d) {
     DevScene S{};
     int rc;
     if ((rc = upload(c, nodes, &S.nodes))) return rc;
+    /* two-level records for the wave walk (blasWalk2): W(g) = the records of g
+     * and of its two children, each in the lanes-as-planes order (lane l of a
+     * row = dword planeDword(l) of the 64-B record), 48 floats; a leaf's W holds
+     * its own record.  192-B offsets are 32-bit buffer offsets: at most 22.3 M nodes. */
+    static const bool walk2 = !(std::getenv("SURF_WALK2") && std::getenv("SURF_WALK2")[0] == '0');   /* A/B: 0 = one-level walk */
+    if (walk2 && (uint64_t)d->blas_node_count * 192u < (1ull << 32)) {
+        std::vector<float> W((size_t)d->blas_node_count * 48, 0.0f);
+        auto putRec = [&](size_t g, size_t row, uint64_t src) {
+            const float* r = reinterpret_cast<const float*>(&nodes[4 * src]);
+            for (uint32_t l = 0; l < 14; ++l) {
+                const uint32_t dw = l < 12u ? (l / 6u) * 8u + (l & 1u) * 4u + ((l % 6u) >> 1) : (l == 12u ? 3u : 7u);
+                W[48 * g + 16 * row + l] = r[dw];
+            }
+        };
+        for (uint32_t g = 0; g < d->blas_node_count; ++g) {
+            if (owner[g] == kUnset) continue;
+            putRec(g, 0, g);
+            const surf_bvh_node& n = d->blas_nodes[g];
+            if (n.count == 0) {
+                putRec(g, 1, (uint64_t)owner[g] + n.left_first);
+                putRec(g, 2, (uint64_t)owner[g] + n.left_first + 1);
+            }
+        }
+        const float* dW = nullptr;
+        if ((rc = upload(c, W, &dW))) return rc;
+        S.wnodes = dW;
+        S.nWnodes = d->blas_node_count;
+    }
     if ((rc = upload(c, tris, &S.tris))) return rc;
     if ((rc = upload(c, normals, &S.normals))) return rc;
     if ((rc = upload(c, verts, &S.verts))) return rc;
@@ -1457,7 +1498,8 @@ int surf_trace_closest(surf_ctx* c, uint32_t n, const float* o, const float* d, 
         hipLaunchKernelGGL(k_trace_closest_rows, dim3((n + 3) / 4), dim3(64), rowsLds(c), c->stream, c->S, (const float*)dO,
                            (const float*)dD, n, dT, dI, recStackWords(c));
     else if (c->traceMode == 1)
-        hipLaunchKernelGGL(k_trace_closest_coop, dim3(n), dim3(64), coopLds(c), c->stream, c->S, (const float*)dO, (const float*)dD,
+        hipLaunchKernelGGL(c->ldsTables ? k_trace_closest_coop<true> : k_trace_closest_coop<false>, dim3(n), dim3(64), coopLds(c),
+                           c->stream, c->S, (const float*)dO, (const float*)dD,
                            n, dT, dI, recStackWords(c));
     else if (c->ldsTables)
         hipLaunchKernelGGL(k_trace_closest<true>, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), traversalLds(c, kBlock), c->stream,
@@ -1495,7 +1537,8 @@ int surf_trace_any(surf_ctx* c, uint32_t n, const float* o, const float* d, cons
         hipLaunchKernelGGL(k_trace_any_rows, dim3((n + 3) / 4), dim3(64), rowsLds(c), c->stream, c->S, (const float*)dO,
                            (const float*)dD, (const float*)dM, n, dR, recStackWords(c));
     else if (c->traceMode == 1)
-        hipLaunchKernelGGL(k_trace_any_coop, dim3(n), dim3(64), coopLds(c), c->stream, c->S, (const float*)dO, (const float*)dD,
+        hipLaunchKernelGGL(c->ldsTables ? k_trace_any_coop<true> : k_trace_any_coop<false>, dim3(n), dim3(64), coopLds(c), c->stream,
+                           c->S, (const float*)dO, (const float*)dD,
                            (const float*)dM, n, dR, recStackWords(c));
     else if (c->ldsTables)
         hipLaunchKernelGGL(k_trace_any<true>, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), traversalLds(c, kBlock), c->stream,

@@ -427,33 +427,41 @@ def test_general_tlas_bitexact(variant):
     bvh.cpp:654-778; ray_extend.comp:105-165): near-first child order, the far
     child pushed, leaf instance loops, on scenes whose TLAS splits (depth > 0)
     -- with <= 64 instances (LDS trace/shading tables) and > 64 (global
-    tables).  Hit records, any-hit and a render with its event counts equal
-    the oracle's bit for bit."""
+    tables), in the lane traversal and in the drain's wave traversal.  Hit
+    records, any-hit and a render (its drain on the cooperative engine) with
+    its event counts equal the oracle's bit for bit."""
     o = oracle.OracleScene(variant=variant)
     p = surf_amd.Scene.indoor(variant=variant)
     try:
         assert p.bvh_depths()[0] > 0, "TLAS did not split"
         W, H = 64, 48
         r = surf_amd.Renderer(p, W, H, frame_batch=16)
-        for mode in (1, 2):
-            with pytest.raises(surf_amd.SurfError):
-                r.set_trace_mode(mode)    # the cooperative traversals need a single-leaf TLAS
+        with pytest.raises(surf_amd.SurfError):
+            r.set_trace_mode(2)           # the four-rows traversal needs a single-leaf TLAS
         (eo, ed), (so, sd, st) = o.record_rays(W, H, 0, 0, W * H)
         rng = np.random.default_rng(7)
         ro = rng.uniform([-9, -0.9, -9], [9, 8.9, 9], size=(20000, 3)).astype(np.float32)
         rd = rng.normal(size=(20000, 3)).astype(np.float32)
         rd /= np.linalg.norm(rd, axis=1, keepdims=True)
         oo, dd = np.concatenate([eo, so, ro]), np.concatenate([ed, sd, rd])
-        gpu, cpu = r.trace_closest(oo, dd), o.trace_closest(oo, dd)
-        for n, g, c in zip(["t", "u", "v", "inst", "prim"], gpu, cpu):
-            bad = np.nonzero(g.view(np.uint32) != c.view(np.uint32))[0]
-            assert len(bad) == 0, f"{n}: {len(bad)} of {len(g)} differ, first {bad[:5]}"
-        assert len(np.unique(gpu[3][gpu[3] != UNSET])) > 30, "rays should hit many instances"
-        assert len(so) > 500 and np.array_equal(r.trace_any(so, sd, st), o.trace_any(so, sd, st))
+        cpu = o.trace_closest(oo, dd)
+        cpu_any = o.trace_any(so, sd, st)
+        # mode 0: one ray per lane; mode 1: one ray per wave (the drain's walk,
+        # here the general-TLAS wave walk: traceWaveTlas)
+        for mode in (0, 1):
+            r.set_trace_mode(mode)
+            gpu = r.trace_closest(oo, dd)
+            for n, g, c in zip(["t", "u", "v", "inst", "prim"], gpu, cpu):
+                bad = np.nonzero(g.view(np.uint32) != c.view(np.uint32))[0]
+                assert len(bad) == 0, f"mode {mode} {n}: {len(bad)} of {len(g)} differ, first {bad[:5]}"
+            assert len(np.unique(gpu[3][gpu[3] != UNSET])) > 30, "rays should hit many instances"
+            assert len(so) > 500 and np.array_equal(r.trace_any(so, sd, st), cpu_any), f"mode {mode} any-hit"
+        r.set_trace_mode(0)
         r.render(3, 0, 0)
         g = r.accumulator()
         stats = r.stats()
         r.close()
+        assert stats["tail_survivors"] > 0, "the drain should run the cooperative (one path per wave) engine"
         oracle.set_zero_cutoff(True)
         try:
             c, cnt, _ = o.render(W, H, 3)
