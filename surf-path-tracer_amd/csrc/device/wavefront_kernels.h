@@ -98,6 +98,7 @@ struct DevScene {
     uint32_t nodes4G;         /* every BLAS-local record offset (64 B each) fits 32 bits: the asm wave walk's buffer offsets */
     const float* wnodes;      /* two-level records (48 floats per BLAS node, see surf_upload_scene), or null */
     uint32_t nWnodes;         /* nodes in wnodes (every 192-B offset fits 32 bits) */
+    uint32_t laneW;           /* the one-ray-per-lane traversal walks the two-level records too (HBM-resident BVHs) */
     uint32_t bgType;
     float bgColor[3], bgA[3], bgB[3];
     float cellLo[3], cellScale[3];   /* ray-order cells: the TLAS root box split in 2 per axis (scale 0: one cell) */
@@ -342,6 +343,108 @@ __device__ __forceinline__ bool blasTrace(const DevScene& S, const TraceInst& I,
     return any;
 }
 
+/* blasTrace over the two-level records (S.wnodes, S.laneW): one memory round
+ * trip per two BVH levels -- for BVHs that live in HBM, where every level of
+ * the one-level walk waits for a DRAM access.  A W record holds three node
+ * records (X, X.left, X.right) in the lanes-as-planes order (surf_upload_scene):
+ * per row the two child boxes (min.x, max.x, min.y, max.y, min.z, max.z),
+ * leftFirst, count, and, for an interior row node, its two children as packed
+ * leaf references (kLeafTag | count << 24 | leftFirst when they are leaves
+ * that fit, else 0).  The decisions are blasTrace's (near child first, far
+ * pushed when hit, pop when both miss), taken for two levels from one record:
+ * exact, as no leaf lies between the levels (the depth is the same).  Stack
+ * entries are node indices, or packed leaf references (a popped leaf needs no
+ * record). */
+constexpr uint32_t kLeafTag = 0x80000000u;
+struct WRow { float4 a, b, c, d; };
+template <bool FIN>
+__device__ __forceinline__ void wBoxes(const WRow& r, V3 o, V3 rd, float depth, float& d0, float& d1) {
+    d0 = FIN ? slabFinite(r.a.x, r.a.z, r.b.x, r.a.y, r.a.w, r.b.y, o, rd, depth) : slab(r.a.x, r.a.z, r.b.x, r.a.y, r.a.w, r.b.y, o, rd, depth);
+    d1 = FIN ? slabFinite(r.b.z, r.c.x, r.c.z, r.b.w, r.c.y, r.c.w, o, rd, depth) : slab(r.b.z, r.c.x, r.c.z, r.b.w, r.c.y, r.c.w, o, rd, depth);
+}
+__device__ __forceinline__ WRow wSel(bool c, const WRow& x, const WRow& y) {
+    WRow r;
+    r.a = c ? y.a : x.a; r.b = c ? y.b : x.b; r.c = c ? y.c : x.c; r.d = c ? y.d : x.d;
+    return r;
+}
+template <bool ANY, bool FIN>
+__device__ __forceinline__ bool blasTraceW(const DevScene& S, const TraceInst& I, V3 o, V3 d, V3 rd, float& depth,
+                                           float& hu, float& hv, uint32_t& hprim, uint32_t* stk, uint32_t stride, uint32_t base) {
+    const uint32_t nodeOff = I.meta.x;
+    const float4* tri = S.tris + 3u * I.meta.y;
+    const uint32_t rlf = f2u(I.r0.w), rcnt = f2u(I.r1.w);
+    if (rcnt != 0u) return leafTestUniform<ANY>(tri, rlf, rcnt, o, d, depth, hu, hv, hprim);
+    const float4* W = reinterpret_cast<const float4*>(S.wnodes);
+    uint32_t* const bottom = stk + base * stride;
+    uint32_t* sp = bottom;
+    uint32_t ref = nodeOff;                 /* the root: its children are tested in its first visit */
+    bool any = false;
+    for (;;) {
+        uint32_t lf = 0u, cnt = 0u;
+        if (ref & kLeafTag) {
+            lf = ref & 0xFFFFFFu; cnt = (ref >> 24) & 0x7Fu;
+        } else {
+            const float4* w = W + 12u * ref;
+            WRow r0{w[0], w[1], w[2], w[3]}, r1{w[4], w[5], w[6], w[7]}, r2{w[8], w[9], w[10], w[11]};
+            pin(r0.a); pin(r0.b); pin(r0.c); pin(r0.d); pin(r1.a); pin(r1.b); pin(r1.c); pin(r1.d);
+            pin(r2.a); pin(r2.b); pin(r2.c); pin(r2.d);
+            cnt = f2u(r0.d.y);
+            lf = f2u(r0.d.x);
+            if (cnt == 0u) {
+                /* level 1: X's children */
+                float dL, dR;
+                wBoxes<FIN>(r0, o, rd, depth, dL, dR);
+                bool c;                       /* near child is the right one */
+                if (ANY) c = dL == kFarAway;
+                else c = dL > dR;
+                const float dn = c ? dR : dL, df = c ? dL : dR;
+                if (dn == kFarAway) goto pop;
+                {
+                    const WRow rc = wSel(c, r1, r2), rf = wSel(c, r2, r1);
+                    const uint32_t cC = f2u(rc.d.y), lC = f2u(rc.d.x), cF = f2u(rf.d.y), lF = f2u(rf.d.x);
+                    /* the far child as a stack entry: a packed leaf, or its node index */
+                    const uint32_t refF = (cF != 0u && lF < (1u << 24) && cF < 128u) ? (kLeafTag | (cF << 24) | lF)
+                                                                                       : nodeOff + lf + (c ? 0u : 1u);
+                    if (cC != 0u) {
+                        /* near child is a leaf: the far child pushed, then the leaf */
+                        if (df != kFarAway) { *sp = refF; sp += stride; }
+                        lf = lC; cnt = cC;
+                    } else {
+                        /* level 2: the near child's children, at the same depth */
+                        float eL, eR;
+                        wBoxes<FIN>(rc, o, rd, depth, eL, eR);
+                        bool g;
+                        if (ANY) g = eL == kFarAway;
+                        else g = eL > eR;
+                        const float en = g ? eR : eL, ef = g ? eL : eR;
+                        if (en == kFarAway) {
+                            /* the reference pushes the far child and pops it at once */
+                            if (df == kFarAway) goto pop;
+                            ref = refF;
+                            continue;
+                        }
+                        if (df != kFarAway) { *sp = refF; sp += stride; }
+                        const uint32_t pN = f2u(g ? rc.d.w : rc.d.z), pF = f2u(g ? rc.d.z : rc.d.w);
+                        if (ef != kFarAway) { *sp = pF ? pF : nodeOff + lC + (g ? 0u : 1u); sp += stride; }
+                        ref = pN ? pN : nodeOff + lC + (g ? 1u : 0u);
+                        continue;
+                    }
+                }
+            }
+        }
+        /* a leaf */
+        if (leafTest<ANY>(tri, lf, cnt, o, d, depth, hu, hv, hprim)) {
+            if (ANY) return true;
+            any = true;
+        }
+    pop:
+        if (sp == bottom) break;
+        sp -= stride;
+        ref = *sp;
+    }
+    return any;
+}
+
 /* Instance::intersect(Any) (bvh.cpp:481-513): origin (M^-1 (o,1)).xyz / w,
  * direction (M^-1 (d,0)).xyz (not renormalized: t is shared with world space).
  * For an affine M^-1 (row 3 = 0,0,0,1) w is exactly 1 for finite o and x/1 = x,
@@ -353,7 +456,7 @@ __device__ __forceinline__ float rowDot(float4 r, float x, float y, float z, flo
     return a + b;
 }
 
-template <bool ANY>
+template <bool ANY, bool LW = false>
 __device__ __forceinline__ bool instanceTrace(const DevScene& S, const TraceInst& I, V3 o, V3 d, float& depth, float& hu,
                                               float& hv, uint32_t& hprim, uint32_t* stk, uint32_t stride, uint32_t base) {
     V3 oo = mk3(rowDot(I.m0, o.x, o.y, o.z, 1.0f), rowDot(I.m1, o.x, o.y, o.z, 1.0f), rowDot(I.m2, o.x, o.y, o.z, 1.0f));
@@ -364,8 +467,11 @@ __device__ __forceinline__ bool instanceTrace(const DevScene& S, const TraceInst
         return leafTestUniform<ANY>(S.tris + 3u * I.meta.y, f2u(I.r0.w), f2u(I.r1.w), oo, dd, depth, hu, hv, hprim);
     const V3 rd = mk3(1.0f / dd.x, 1.0f / dd.y, 1.0f / dd.z);
     /* S.finiteBoxes: every BLAS box is finite (checked at upload) */
-    if (S.finiteBoxes && finite3(oo) && finite3(rd))
-        return blasTrace<ANY, true>(S, I, oo, dd, rd, depth, hu, hv, hprim, stk, stride, base);
+    const bool fin = S.finiteBoxes && finite3(oo) && finite3(rd);
+    if (LW)
+        return fin ? blasTraceW<ANY, true>(S, I, oo, dd, rd, depth, hu, hv, hprim, stk, stride, base)
+                   : blasTraceW<ANY, false>(S, I, oo, dd, rd, depth, hu, hv, hprim, stk, stride, base);
+    if (fin) return blasTrace<ANY, true>(S, I, oo, dd, rd, depth, hu, hv, hprim, stk, stride, base);
     return blasTrace<ANY, false>(S, I, oo, dd, rd, depth, hu, hv, hprim, stk, stride, base);
 }
 
@@ -394,7 +500,7 @@ __device__ __forceinline__ TraceTables traceTables(const DevScene& S, uint32_t* 
 }
 
 /* BvhTLAS::intersect / intersectAny (bvh.cpp:654-778). */
-template <bool ANY>
+template <bool ANY, bool LW = false>
 __device__ __forceinline__ bool traceScene(const DevScene& S, const TraceTables& Tt, V3 o, V3 d, float& depth, float& hu, float& hv,
                                            uint32_t& hinst, uint32_t& hprim, uint32_t* stk, uint32_t stride) {
     bool any = false;
@@ -420,7 +526,7 @@ __device__ __forceinline__ bool traceScene(const DevScene& S, const TraceTables&
                 const float t1 = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
                 if (t1 < t0 || t1 < 0.0f || t0 >= depth) continue;
             }
-            if (instanceTrace<ANY>(S, I, o, d, depth, hu, hv, hprim, stk, stride, 0u)) {
+            if (instanceTrace<ANY, LW>(S, I, o, d, depth, hu, hv, hprim, stk, stride, 0u)) {
                 if (ANY) return true;
                 any = true;
                 hinst = ii;
@@ -438,7 +544,7 @@ __device__ __forceinline__ bool traceScene(const DevScene& S, const TraceTables&
         if (cnt != 0u) {
             for (uint32_t k = 0; k < cnt; ++k) {
                 const uint32_t ii = Tt.order[lf + k];
-                if (instanceTrace<ANY>(S, Tt.inst[ii], o, d, depth, hu, hv, hprim, stk, stride, sp)) {
+                if (instanceTrace<ANY, LW>(S, Tt.inst[ii], o, d, depth, hu, hv, hprim, stk, stride, sp)) {
                     if (ANY) return true;
                     any = true;
                     hinst = ii;
@@ -1636,7 +1742,7 @@ __global__ __launch_bounds__(kSortThreads) void k_binscatter(const uint8_t* __re
 }
 
 /* ------------------------------------------------------------------ kernels */
-template <bool LDS>
+template <bool LDS, bool LW = false>
 __global__ __launch_bounds__(kBlock, SURF_TRACE_WAVES) void k_extend(DevScene S, Pool cur, float4* __restrict__ hitTUV,
                                                    uint32_t* __restrict__ hitInst, const Counters* C, int par, uint32_t stackWords,
                                                    const uint32_t* __restrict__ order) {
@@ -1653,7 +1759,7 @@ __global__ __launch_bounds__(kBlock, SURF_TRACE_WAVES) void k_extend(DevScene S,
         const float4 o = ldS(&cur.od[2u * (j)]), d = ldS(&cur.od[2u * (j) + 1u]);
         float depth = kFarAway, u = 0.0f, v = 0.0f;
         uint32_t inst = kUnset, prim = kUnset;
-        const bool hit = traceScene<false>(S, Tt, xyz(o), xyz(d), depth, u, v, inst, prim, stk, stride);
+        const bool hit = traceScene<false, LW>(S, Tt, xyz(o), xyz(d), depth, u, v, inst, prim, stk, stride);
         stS(&hitTUV[i], make_float4(depth, u, v, u2f(prim)));
         stSu(&hitInst[i], hit ? inst : kUnset);
     }
@@ -2010,7 +2116,7 @@ __global__ __launch_bounds__(kBlock, SURF_SHADE_WAVES) void k_shade(DevScene S, 
     blockCount<5>(C, {1, 2, 3, 4, 7}, {cHit, cCont, cSh, cAcc, cCap});
 }
 
-template <bool LDS>
+template <bool LDS, bool LW = false>
 __global__ __launch_bounds__(kBlock, SURF_TRACE_WAVES) void k_connect(DevScene S, ShadowQ Q, float4* __restrict__ rad, Counters* C, int par,
                                                     uint32_t stackWords, const uint32_t* __restrict__ order) {
     extern __shared__ uint32_t lds[];
@@ -2028,7 +2134,7 @@ __global__ __launch_bounds__(kBlock, SURF_TRACE_WAVES) void k_connect(DevScene S
             const float4 o = ldS(&Q.o[i]), d = ldS(&Q.d[i]);
             float depth = o.w, u = 0.0f, v = 0.0f;
             uint32_t inst = kUnset, prim = kUnset;
-            const bool occ = traceScene<true>(S, Tt, xyz(o), xyz(d), depth, u, v, inst, prim, stk, stride);
+            const bool occ = traceScene<true, LW>(S, Tt, xyz(o), xyz(d), depth, u, v, inst, prim, stk, stride);
             if (!occ) {
                 const float4 c = ldS(&Q.c[i]);
                 addRadiance(rad, f2u(d.w), xyz(c));
@@ -2520,7 +2626,7 @@ __global__ __launch_bounds__(kBlock) void k_energy_terms(const float4* __restric
 }
 
 /* Traversal entry points for kernel-level parity tests. */
-template <bool LDS>
+template <bool LDS, bool LW = false>
 __global__ __launch_bounds__(kBlock) void k_trace_closest(DevScene S, const float* __restrict__ o, const float* __restrict__ d,
                                                           uint32_t n, float4* __restrict__ tuv, uint2* __restrict__ ip,
                                                           uint32_t stackWords) {
@@ -2530,12 +2636,12 @@ __global__ __launch_bounds__(kBlock) void k_trace_closest(DevScene S, const floa
     if (i >= n) return;
     float depth = kFarAway, u = 0.0f, v = 0.0f;
     uint32_t inst = kUnset, prim = kUnset;
-    const bool hit = traceScene<false>(S, Tt, mk3(o[3 * i], o[3 * i + 1], o[3 * i + 2]), mk3(d[3 * i], d[3 * i + 1], d[3 * i + 2]),
+    const bool hit = traceScene<false, LW>(S, Tt, mk3(o[3 * i], o[3 * i + 1], o[3 * i + 2]), mk3(d[3 * i], d[3 * i + 1], d[3 * i + 2]),
                                        depth, u, v, inst, prim, lds + threadIdx.x, blockDim.x);
     tuv[i] = make_float4(depth, hit ? u : 0.0f, hit ? v : 0.0f, 0.0f);
     ip[i] = make_uint2(hit ? inst : kUnset, hit ? prim : kUnset);
 }
-template <bool LDS>
+template <bool LDS, bool LW = false>
 __global__ __launch_bounds__(kBlock) void k_trace_any(DevScene S, const float* __restrict__ o, const float* __restrict__ d,
                                                       const float* __restrict__ tmaxv, uint32_t n, uint8_t* __restrict__ occ,
                                                       uint32_t stackWords) {
@@ -2545,7 +2651,7 @@ __global__ __launch_bounds__(kBlock) void k_trace_any(DevScene S, const float* _
     if (i >= n) return;
     float depth = tmaxv[i], u = 0.0f, v = 0.0f;
     uint32_t inst = kUnset, prim = kUnset;
-    occ[i] = traceScene<true>(S, Tt, mk3(o[3 * i], o[3 * i + 1], o[3 * i + 2]), mk3(d[3 * i], d[3 * i + 1], d[3 * i + 2]),
+    occ[i] = traceScene<true, LW>(S, Tt, mk3(o[3 * i], o[3 * i + 1], o[3 * i + 2]), mk3(d[3 * i], d[3 * i + 1], d[3 * i + 2]),
                               depth, u, v, inst, prim, lds + threadIdx.x, blockDim.x) ? 1 : 0;
 }
 

@@ -405,12 +405,11 @@ void launchPhase(surf_ctx* c, int ph, hipEvent_t* ev) {
     }
     if (ev) (void)hipEventRecord(ev[1], c->stream);
     const Pool cur = c->pool[par];                 /* the pool k_extend / k_shade read */
-    if (c->ldsTables)
-        hipLaunchKernelGGL(k_extend<true>, dim3(c->gridExtend), dim3(c->extBlock), traversalLds(c, c->extBlock), c->stream, c->S,
-                           cur, c->hitTUV, c->hitInst, (const Counters*)c->ctr, par, stackWords(c, c->extBlock), order);
-    else
-        hipLaunchKernelGGL(k_extend<false>, dim3(c->gridExtend), dim3(c->extBlock), traversalLds(c, c->extBlock), c->stream, c->S,
-                           cur, c->hitTUV, c->hitInst, (const Counters*)c->ctr, par, stackWords(c, c->extBlock), order);
+    /* LW: the two-level records in the lane traversal (HBM-resident BVHs, S.laneW) */
+    auto extendK = c->S.laneW ? (c->ldsTables ? k_extend<true, true> : k_extend<false, true>)
+                              : (c->ldsTables ? k_extend<true, false> : k_extend<false, false>);
+    hipLaunchKernelGGL(extendK, dim3(c->gridExtend), dim3(c->extBlock), traversalLds(c, c->extBlock), c->stream, c->S,
+                       cur, c->hitTUV, c->hitInst, (const Counters*)c->ctr, par, stackWords(c, c->extBlock), order);
     if (ev) (void)hipEventRecord(ev[2], c->stream);
     if (c->ldsTables)
         hipLaunchKernelGGL(k_shade<true>, dim3(c->gridWork), dim3(kBlock), 0, c->stream, c->S, cur, c->pool[par ^ 1],
@@ -426,12 +425,11 @@ void launchPhase(surf_ctx* c, int ph, hipEvent_t* ev) {
         qorder = c->order;
     }
     if (ev) (void)hipEventRecord(ev[4], c->stream);
-    if (c->ldsTables && !c->connectGlobal)
-        hipLaunchKernelGGL(k_connect<true>, dim3(c->gridConnect), dim3(kBlock), traversalLds(c, kBlock), c->stream, c->S, c->Q,
-                           c->rad, c->ctr, par, sw, qorder);
-    else   /* global tables: LDS holds only the traversal stack */
-        hipLaunchKernelGGL(k_connect<false>, dim3(c->gridConnect), dim3(kBlock), (size_t)sw * sizeof(uint32_t), c->stream, c->S,
-                           c->Q, c->rad, c->ctr, par, sw, qorder);
+    const bool ldsC = c->ldsTables && !c->connectGlobal;   /* else global tables: LDS holds only the traversal stack */
+    auto connectK = c->S.laneW ? (ldsC ? k_connect<true, true> : k_connect<false, true>)
+                               : (ldsC ? k_connect<true, false> : k_connect<false, false>);
+    hipLaunchKernelGGL(connectK, dim3(c->gridConnect), dim3(kBlock), ldsC ? traversalLds(c, kBlock) : (size_t)sw * sizeof(uint32_t),
+                       c->stream, c->S, c->Q, c->rad, c->ctr, par, sw, qorder);
     if (ev) (void)hipEventRecord(ev[5], c->stream);
     hipLaunchKernelGGL(k_regen, dim3(c->gridRegen), dim3(kBlock), 0, c->stream, c->cam, c->pool[par ^ 1], c->rad, c->ctr, par,
                        c->capacity, geom(c));
@@ -1212,11 +1210,23 @@ int surf_upload_scene(surf_ctx* c, const surf_scene_desc* d) {
     static const bool walk2 = !(std::getenv("SURF_WALK2") && std::getenv("SURF_WALK2")[0] == '0');   /* A/B: 0 = one-level walk */
     if (walk2 && (uint64_t)d->blas_node_count * 192u < (1ull << 32)) {
         std::vector<float> W((size_t)d->blas_node_count * 48, 0.0f);
+        /* lanes 14 / 15 of a row (unused by the wave walk): the row node's two
+         * children as packed leaf references for the lane walk (blasTraceW):
+         * kLeafTag | count << 24 | leftFirst, 0 when not a leaf or too large */
+        auto packLeaf = [&](uint64_t m) -> uint32_t {
+            const surf_bvh_node& q = d->blas_nodes[m];
+            return (q.count != 0 && q.count < 128u && q.left_first < (1u << 24)) ? (kLeafTag | (q.count << 24) | q.left_first) : 0u;
+        };
         auto putRec = [&](size_t g, size_t row, uint64_t src) {
             const float* r = reinterpret_cast<const float*>(&nodes[4 * src]);
             for (uint32_t l = 0; l < 14; ++l) {
                 const uint32_t dw = l < 12u ? (l / 6u) * 8u + (l & 1u) * 4u + ((l % 6u) >> 1) : (l == 12u ? 3u : 7u);
                 W[48 * g + 16 * row + l] = r[dw];
+            }
+            const surf_bvh_node& q = d->blas_nodes[src];
+            if (q.count == 0 && owner[src] != kUnset) {
+                W[48 * g + 16 * row + 14] = u2f(packLeaf((uint64_t)owner[src] + q.left_first));
+                W[48 * g + 16 * row + 15] = u2f(packLeaf((uint64_t)owner[src] + q.left_first + 1));
             }
         };
         for (uint32_t g = 0; g < d->blas_node_count; ++g) {
@@ -1232,6 +1242,12 @@ int surf_upload_scene(surf_ctx* c, const surf_scene_desc* d) {
         if ((rc = upload(c, W, &dW))) return rc;
         S.wnodes = dW;
         S.nWnodes = d->blas_node_count;
+        /* the lane traversal walks them too when the BVH cannot stay in the
+         * caches (nodes + triangles past the 256 MB of MALL): one DRAM round
+         * trip per two levels instead of one per level (SURF_LANEW=0|1: A/B) */
+        const uint64_t bvhBytes = (uint64_t)d->blas_node_count * 64u + (uint64_t)d->blas_index_count * 48u;
+        S.laneW = bvhBytes > (256ull << 20) ? 1u : 0u;
+        if (const char* e = std::getenv("SURF_LANEW")) S.laneW = e[0] == '1' ? 1u : 0u;
     }
     if ((rc = upload(c, tris, &S.tris))) return rc;
     if ((rc = upload(c, normals, &S.normals))) return rc;
@@ -1501,11 +1517,10 @@ int surf_trace_closest(surf_ctx* c, uint32_t n, const float* o, const float* d, 
         hipLaunchKernelGGL(c->ldsTables ? k_trace_closest_coop<true> : k_trace_closest_coop<false>, dim3(n), dim3(64), coopLds(c),
                            c->stream, c->S, (const float*)dO, (const float*)dD,
                            n, dT, dI, recStackWords(c));
-    else if (c->ldsTables)
-        hipLaunchKernelGGL(k_trace_closest<true>, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), traversalLds(c, kBlock), c->stream,
-                           c->S, (const float*)dO, (const float*)dD, n, dT, dI, stackWords(c, kBlock));
     else
-        hipLaunchKernelGGL(k_trace_closest<false>, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), traversalLds(c, kBlock), c->stream,
+        hipLaunchKernelGGL(c->S.laneW ? (c->ldsTables ? k_trace_closest<true, true> : k_trace_closest<false, true>)
+                                      : (c->ldsTables ? k_trace_closest<true, false> : k_trace_closest<false, false>),
+                           dim3((n + kBlock - 1) / kBlock), dim3(kBlock), traversalLds(c, kBlock), c->stream,
                            c->S, (const float*)dO, (const float*)dD, n, dT, dI, stackWords(c, kBlock));
     std::vector<float4> t(n);
     std::vector<uint2> ip(n);
@@ -1540,11 +1555,10 @@ int surf_trace_any(surf_ctx* c, uint32_t n, const float* o, const float* d, cons
         hipLaunchKernelGGL(c->ldsTables ? k_trace_any_coop<true> : k_trace_any_coop<false>, dim3(n), dim3(64), coopLds(c), c->stream,
                            c->S, (const float*)dO, (const float*)dD,
                            (const float*)dM, n, dR, recStackWords(c));
-    else if (c->ldsTables)
-        hipLaunchKernelGGL(k_trace_any<true>, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), traversalLds(c, kBlock), c->stream,
-                           c->S, (const float*)dO, (const float*)dD, (const float*)dM, n, dR, stackWords(c, kBlock));
     else
-        hipLaunchKernelGGL(k_trace_any<false>, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), traversalLds(c, kBlock), c->stream,
+        hipLaunchKernelGGL(c->S.laneW ? (c->ldsTables ? k_trace_any<true, true> : k_trace_any<false, true>)
+                                      : (c->ldsTables ? k_trace_any<true, false> : k_trace_any<false, false>),
+                           dim3((n + kBlock - 1) / kBlock), dim3(kBlock), traversalLds(c, kBlock), c->stream,
                            c->S, (const float*)dO, (const float*)dD, (const float*)dM, n, dR, stackWords(c, kBlock));
     (void)hipMemcpyAsync(occ, dR, n, hipMemcpyDeviceToHost, c->stream);
     hipError_t e = hipStreamSynchronize(c->stream);

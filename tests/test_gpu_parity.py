@@ -96,6 +96,42 @@ def test_any_hit_bitexact(oracle_scene, product_scene, mode):
     assert np.array_equal(g, c)
 
 
+def test_lane_two_level_walk_bitexact(oracle_scene, monkeypatch):
+    """The one-ray-per-lane traversal over the two-level records (blasTraceW:
+    one fetch per two BVH levels, the default for HBM-resident BVHs such as
+    C5's), forced on the bundled scene (SURF_LANEW=1): closest-hit records,
+    any-hit and a render with its event counts equal the oracle's."""
+    monkeypatch.setenv("SURF_LANEW", "1")
+    p = surf_amd.Scene.indoor()
+    try:
+        W = H = 96
+        (eo, ed), (so, sd, st) = oracle_scene.record_rays(W, H, 0, 0, W * H)
+        rng = np.random.default_rng(13)
+        ro = rng.uniform([-9, -0.9, -9], [9, 8.9, 9], size=(20000, 3)).astype(np.float32)
+        rd = rng.normal(size=(20000, 3)).astype(np.float32)
+        rd /= np.linalg.norm(rd, axis=1, keepdims=True)
+        o, d = np.concatenate([eo, so, ro]), np.concatenate([ed, sd, rd])
+        r = surf_amd.Renderer(p, W, H)
+        gpu, cpu = r.trace_closest(o, d), oracle_scene.trace_closest(o, d)
+        for n, g, c in zip(["t", "u", "v", "inst", "prim"], gpu, cpu):
+            bad = np.nonzero(g.view(np.uint32) != c.view(np.uint32))[0]
+            assert len(bad) == 0, f"{n}: {len(bad)} of {len(g)} differ, first {bad[:5]}"
+        assert np.array_equal(r.trace_any(so, sd, st), oracle_scene.trace_any(so, sd, st))
+        r.render(4, 0, 0)
+        g = r.accumulator()
+        stats = r.stats()
+        r.close()
+        oracle.set_zero_cutoff(True)
+        try:
+            c, cnt, _ = oracle_scene.render(W, H, 4)
+        finally:
+            oracle.set_zero_cutoff(False)
+        _assert_bitexact(g, c, "lane two-level walk 96x96x4")
+        _assert_counts(stats, cnt)
+    finally:
+        p.close()
+
+
 def _render_both(oracle_scene, product_scene, W, H, frames, first=0, max_seg=0, **kw):
     """GPU render (zero-throughput cutoff on, the product default) against the
     oracle in reference semantics (no cutoff) for radiance, and against the
