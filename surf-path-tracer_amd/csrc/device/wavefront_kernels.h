@@ -1410,7 +1410,7 @@ __device__ __forceinline__ bool blasWalkFallback(const DevScene& S, uint32_t nod
  * its prologue entry pk (LDS, one address for the wave: a broadcast): the
  * world-box cull and the root children's depth tests at the current depth,
  * then the BLAS walk (or the root leaf's triangles). */
-template <bool ANY>
+template <bool ANY, bool W2 = false>
 __device__ __forceinline__ bool waveInstance(const DevScene& S, const TraceInst& I, const float4* pk, float& depth, float& hu,
                                              float& hv, uint32_t& hprim, float* rs, SegStats* ss) {
     /* wave-uniform (the tables may be read through a generic pointer: LDS or global) */
@@ -1431,7 +1431,12 @@ __device__ __forceinline__ bool waveInstance(const DevScene& S, const TraceInst&
     if (dn == kFarAway) return false;
     const V3 rk = xyz(q2);
     const bool fin = S.finiteBoxes && finite3(ok) && finite3(rk);
-    if (fin && S.wnodes) return blasWalk2<ANY>(S, nodeOff, tri, ok, dk, rk, depth, hu, hv, hprim, rs);
+    if (W2) {
+        /* kernels built for two-level records carry no one-level asm walk (its
+         * registers and code): a non-finite ray takes the C++ walk */
+        if (fin) return blasWalk2<ANY>(S, nodeOff, tri, ok, dk, rk, depth, hu, hv, hprim, rs);
+        return blasWalk<ANY, false>(S, nodeOff, tri, ok, dk, rk, dn, df, cn, cf, depth, hu, hv, hprim, rs, ss);
+    }
     return blasWalkFallback<ANY>(S, nodeOff, tri, ok, dk, rk, dn, df, cn, cf, depth, hu, hv, hprim, rs, ss, fin);
 }
 
@@ -1442,7 +1447,7 @@ __device__ __forceinline__ bool waveInstance(const DevScene& S, const TraceInst&
  * child first, the far child pushed when hit (a stack of node indices, entry
  * k in lane k of one VGPR), a leaf's instances in index order, each at its
  * turn with the depth the earlier ones left (waveInstance). */
-template <bool ANY>
+template <bool ANY, bool W2 = false>
 __device__ __forceinline__ bool traceWaveTlas(const DevScene& S, const TraceTables& Tt, V3 o, V3 d, float& depth, float& hu,
                                               float& hv, uint32_t& hinst, uint32_t& hprim, float* rs, float4* pro, SegStats* ss) {
     const uint32_t lane = __lane_id();
@@ -1465,7 +1470,7 @@ __device__ __forceinline__ bool traceWaveTlas(const DevScene& S, const TraceTabl
         if (cnt != 0u) {
             for (uint32_t k = 0; k < cnt; ++k) {
                 const uint32_t ii = Tt.order[lf + k];
-                if (waveInstance<ANY>(S, Tt.inst[ii], pro + 4u * ii, depth, hu, hv, hprim, rs, ss)) {
+                if (waveInstance<ANY, W2>(S, Tt.inst[ii], pro + 4u * ii, depth, hu, hv, hprim, rs, ss)) {
                     if (ANY) return true;
                     any = true;
                     hinst = ii;
@@ -1500,12 +1505,12 @@ __device__ __forceinline__ bool traceWaveTlas(const DevScene& S, const TraceTabl
  * applying the depth tests at its turn (a missed instance costs a few
  * readlanes instead of a serial transform, three divisions and a slab test).
  * Any other TLAS: traceWaveTlas. */
-template <bool ANY>
+template <bool ANY, bool W2 = false>
 __device__ __forceinline__ bool traceWave(const DevScene& S, const TraceTables& Tt, V3 o, V3 d, float& depth, float& hu,
                                           float& hv, uint32_t& hinst, uint32_t& hprim, float* rs, float4* pro, SegStats* ss = nullptr) {
     bool any = false;
     const uint32_t nI = S.tlasLeafCount;
-    if (nI == 0u || nI > 64u) return traceWaveTlas<ANY>(S, Tt, o, d, depth, hu, hv, hinst, hprim, rs, pro, ss);
+    if (nI == 0u || nI > 64u) return traceWaveTlas<ANY, W2>(S, Tt, o, d, depth, hu, hv, hinst, hprim, rs, pro, ss);
 #if SURF_SEG_TIMING
     unsigned long long t0 = segClock();
 #endif
@@ -1526,7 +1531,7 @@ __device__ __forceinline__ bool traceWave(const DevScene& S, const TraceTables& 
 #if SURF_SEG_TIMING
         if (ss) { const unsigned long long t1 = segClock(); ss->cycInst += t1 - t0; t0 = t1; }
 #endif
-        const bool h = waveInstance<ANY>(S, Tt.inst[ii], pro + 4u * k, depth, hu, hv, hprim, rs, ss);
+        const bool h = waveInstance<ANY, W2>(S, Tt.inst[ii], pro + 4u * k, depth, hu, hv, hprim, rs, ss);
 #if SURF_SEG_TIMING
         if (ss) { const unsigned long long t1 = segClock(); ss->cycLoop += t1 - t0; t0 = t1; }
 #endif
@@ -2307,7 +2312,7 @@ __global__ __launch_bounds__(64, SURF_TAIL_WAVES) void k_tail(DevScene S, Pool c
  * (stackWords = 16 x depth words), then the trace tables; the shading tables
  * are read from global memory (wave-uniform reads): LDS copies would cap the
  * one-wave blocks at ~2 waves per SIMD. */
-template <bool LDS>
+template <bool LDS, bool W2 = false>
 __global__ __launch_bounds__(64, SURF_COOP_WAVES) void k_tail_coop(DevScene S, Pool cur, uint32_t n, float4* __restrict__ rad,
                                                   uint32_t* __restrict__ frameDone, uint32_t npx, uint32_t window, Counters* C,
                                                   uint32_t stackWords, uint32_t firstCounted) {
@@ -2342,7 +2347,7 @@ __global__ __launch_bounds__(64, SURF_COOP_WAVES) void k_tail_coop(DevScene S, P
 #if SURF_SEG_TIMING
         const unsigned long long c0 = segClock();
 #endif
-        const bool hit = traceWave<false>(S, Tt, xyz(o4), xyz(d4), depth, u, v, inst, prim, rstk, pro, ssp);
+        const bool hit = traceWave<false, W2>(S, Tt, xyz(o4), xyz(d4), depth, u, v, inst, prim, rstk, pro, ssp);
         (void)ssp;
         ++nExt;
         ShadeOut r;
@@ -2361,7 +2366,7 @@ __global__ __launch_bounds__(64, SURF_COOP_WAVES) void k_tail_coop(DevScene S, P
             ++nSh;
             float sdep = r.so.w, su = 0.0f, sv = 0.0f;
             uint32_t si = kUnset, sp = kUnset;
-            const bool occ = traceWave<true>(S, Tt, xyz(r.so), xyz(r.sd), sdep, su, sv, si, sp, rstk, pro);
+            const bool occ = traceWave<true, W2>(S, Tt, xyz(r.so), xyz(r.sd), sdep, su, sv, si, sp, rstk, pro);
             if (!occ) {
                 if (lead) addRadiance(rad, f2u(r.sd.w), xyz(r.sc));
                 ++nUn; ++nAcc;
@@ -2436,6 +2441,7 @@ struct PairCounts { uint32_t ext, hit, cont, sh, acc, un, paths; };
 
 /* One path of the queue on the calling wave (w); its shadow rays go to the
  * sibling while box.help[w] is set. */
+template <bool W2>
 __device__ __forceinline__ void pairPath(const DevScene& S, const TraceTables& Tt, const ShadeTables& Tb, PairBox& box, uint32_t w,
                                          float4 o4, float4 d4, float4 T4, float4* __restrict__ rad, uint32_t* __restrict__ frameDone,
                                          uint32_t npx, uint32_t window, Counters* C, float* rstk, float4* pro, bool lead,
@@ -2446,7 +2452,7 @@ __device__ __forceinline__ void pairPath(const DevScene& S, const TraceTables& T
     for (;;) {
         float depth = kFarAway, u = 0.0f, v = 0.0f;
         uint32_t inst = kUnset, prim = kUnset;
-        const bool hit = traceWave<false>(S, Tt, xyz(o4), xyz(d4), depth, u, v, inst, prim, rstk, pro);
+        const bool hit = traceWave<false, W2>(S, Tt, xyz(o4), xyz(d4), depth, u, v, inst, prim, rstk, pro);
         ++pc.ext;
         if (pend) {
             while (ldsLoadAcq(&box.done[w]) != posted) __builtin_amdgcn_s_sleep(1);
@@ -2472,7 +2478,7 @@ __device__ __forceinline__ void pairPath(const DevScene& S, const TraceTables& T
             } else {
                 float sdep = r.so.w, su = 0.0f, sv = 0.0f;
                 uint32_t si = kUnset, sp = kUnset;
-                if (!traceWave<true>(S, Tt, xyz(r.so), xyz(r.sd), sdep, su, sv, si, sp, rstk, pro)) {
+                if (!traceWave<true, W2>(S, Tt, xyz(r.so), xyz(r.sd), sdep, su, sv, si, sp, rstk, pro)) {
                     if (lead) addRadiance(rad, f2u(r.sd.w), xyz(r.sc));
                     ++pc.un; ++pc.acc;
                 }
@@ -2500,7 +2506,7 @@ __device__ __forceinline__ void pairPath(const DevScene& S, const TraceTables& T
     }
 }
 
-template <bool LDS>
+template <bool LDS, bool W2 = false>
 __global__ __launch_bounds__(128, SURF_COOP_WAVES) void k_tail_pair(DevScene S, Pool cur, uint32_t n, float4* __restrict__ rad,
                                                    uint32_t* __restrict__ frameDone, uint32_t npx, uint32_t window, Counters* C,
                                                    uint32_t stackWords, uint32_t firstCounted) {
@@ -2526,7 +2532,7 @@ __global__ __launch_bounds__(128, SURF_COOP_WAVES) void k_tail_pair(DevScene S, 
         if (lead) i = atomicAdd(&C->rowNext, 1u);
         i = __builtin_amdgcn_readfirstlane(i);
         if (i >= n) break;
-        pairPath(S, Tt, Tb, box, w, cur.od[2u * i], cur.od[2u * i + 1u], cur.T[i], rad, frameDone, npx, window, C, rstk, pro,
+        pairPath<W2>(S, Tt, Tb, box, w, cur.od[2u * i], cur.od[2u * i + 1u], cur.T[i], rad, frameDone, npx, window, C, rstk, pro,
                  lead, posted, pc);
     }
     /* queue empty: leave the path loop, then serve the sibling's shadow rays
@@ -2542,7 +2548,7 @@ __global__ __launch_bounds__(128, SURF_COOP_WAVES) void k_tail_pair(DevScene S, 
                 const float4 so = box.so[m], sd = box.sd[m];
                 float sdep = so.w, su = 0.0f, sv = 0.0f;
                 uint32_t si = kUnset, sp = kUnset;
-                const bool occ = traceWave<true>(S, Tt, xyz(so), xyz(sd), sdep, su, sv, si, sp, rstk, pro);
+                const bool occ = traceWave<true, W2>(S, Tt, xyz(so), xyz(sd), sdep, su, sv, si, sp, rstk, pro);
                 if (lead) {
                     box.occ[m] = occ ? 1u : 0u;
                     ldsStoreRel(&box.done[m], p);
@@ -2658,7 +2664,7 @@ __global__ __launch_bounds__(kBlock) void k_trace_any(DevScene S, const float* _
 /* Cooperative traversal entry points (one ray per 64-lane block, the
  * lanes-as-planes traversal of the cooperative tail): the same results as
  * k_trace_closest / k_trace_any, for parity tests and latency measurements. */
-template <bool LDS>
+template <bool LDS, bool W2 = false>
 __global__ __launch_bounds__(64) void k_trace_closest_coop(DevScene S, const float* __restrict__ o, const float* __restrict__ d,
                                                            uint32_t n, float4* __restrict__ tuv, uint2* __restrict__ ip,
                                                            uint32_t stackWords) {
@@ -2669,14 +2675,14 @@ __global__ __launch_bounds__(64) void k_trace_closest_coop(DevScene S, const flo
     float depth = kFarAway, u = 0.0f, v = 0.0f;
     uint32_t inst = kUnset, prim = kUnset;
     const V3 ro = mk3(o[3 * i], o[3 * i + 1], o[3 * i + 2]), rdir = mk3(d[3 * i], d[3 * i + 1], d[3 * i + 2]);
-    const bool hit = traceWave<false>(S, Tt, ro, rdir, depth, u, v, inst, prim, reinterpret_cast<float*>(lds),
+    const bool hit = traceWave<false, W2>(S, Tt, ro, rdir, depth, u, v, inst, prim, reinterpret_cast<float*>(lds),
                                       reinterpret_cast<float4*>(lds + stackWords));
     if (threadIdx.x == 0) {
         tuv[i] = make_float4(depth, hit ? u : 0.0f, hit ? v : 0.0f, 0.0f);
         ip[i] = make_uint2(hit ? inst : kUnset, hit ? prim : kUnset);
     }
 }
-template <bool LDS>
+template <bool LDS, bool W2 = false>
 __global__ __launch_bounds__(64) void k_trace_any_coop(DevScene S, const float* __restrict__ o, const float* __restrict__ d,
                                                        const float* __restrict__ tmaxv, uint32_t n, uint8_t* __restrict__ occ,
                                                        uint32_t stackWords) {
@@ -2687,7 +2693,7 @@ __global__ __launch_bounds__(64) void k_trace_any_coop(DevScene S, const float* 
     const V3 ro = mk3(o[3 * i], o[3 * i + 1], o[3 * i + 2]), rdir = mk3(d[3 * i], d[3 * i + 1], d[3 * i + 2]);
     float depth = tmaxv[i], u = 0.0f, v = 0.0f;
     uint32_t inst = kUnset, prim = kUnset;
-    const bool oc = traceWave<true>(S, Tt, ro, rdir, depth, u, v, inst, prim, reinterpret_cast<float*>(lds),
+    const bool oc = traceWave<true, W2>(S, Tt, ro, rdir, depth, u, v, inst, prim, reinterpret_cast<float*>(lds),
                                     reinterpret_cast<float4*>(lds + stackWords));
     if (threadIdx.x == 0) occ[i] = oc ? 1 : 0;
 }

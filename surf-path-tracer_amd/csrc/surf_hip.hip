@@ -617,7 +617,9 @@ int runTail(surf_ctx* c) {
              * taking paths from the queue; idle waves trace their sibling's
              * shadow rays once the queue is empty */
             int per = 0;
-            auto kern = c->ldsTables ? k_tail_pair<true> : k_tail_pair<false>;
+            const bool w2 = c->S.wnodes != nullptr;
+            auto kern = c->ldsTables ? (w2 ? k_tail_pair<true, true> : k_tail_pair<true, false>)
+                                     : (w2 ? k_tail_pair<false, true> : k_tail_pair<false, false>);
             if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, 128, pairTailLds(c)) != hipSuccess || per < 1)
                 per = 2 * SURF_COOP_WAVES;
             const uint32_t blocks = std::max<uint32_t>(1u, std::min<uint32_t>((cnt + 1u) / 2u, c->cus * (uint32_t)per));
@@ -629,7 +631,10 @@ int runTail(surf_ctx* c) {
             break;
         }
         if (waveEligible(c) && cnt <= c->coopAll) {
-            hipLaunchKernelGGL(c->ldsTables ? k_tail_coop<true> : k_tail_coop<false>, dim3(cnt), dim3(64), coopTailLds(c), c->stream,
+            const bool w2 = c->S.wnodes != nullptr;
+            hipLaunchKernelGGL(c->ldsTables ? (w2 ? k_tail_coop<true, true> : k_tail_coop<true, false>)
+                                            : (w2 ? k_tail_coop<false, true> : k_tail_coop<false, false>),
+                               dim3(cnt), dim3(64), coopTailLds(c), c->stream,
                                c->S, in, cnt, c->rad, c->frameDone,
                                c->npx, c->window, c->ctr, recStackWords(c), firstCounted);
             SURF_CHECK(c, hipGetLastError());
@@ -1514,7 +1519,9 @@ int surf_trace_closest(surf_ctx* c, uint32_t n, const float* o, const float* d, 
         hipLaunchKernelGGL(k_trace_closest_rows, dim3((n + 3) / 4), dim3(64), rowsLds(c), c->stream, c->S, (const float*)dO,
                            (const float*)dD, n, dT, dI, recStackWords(c));
     else if (c->traceMode == 1)
-        hipLaunchKernelGGL(c->ldsTables ? k_trace_closest_coop<true> : k_trace_closest_coop<false>, dim3(n), dim3(64), coopLds(c),
+        hipLaunchKernelGGL(c->ldsTables ? (c->S.wnodes ? k_trace_closest_coop<true, true> : k_trace_closest_coop<true, false>)
+                                        : (c->S.wnodes ? k_trace_closest_coop<false, true> : k_trace_closest_coop<false, false>),
+                           dim3(n), dim3(64), coopLds(c),
                            c->stream, c->S, (const float*)dO, (const float*)dD,
                            n, dT, dI, recStackWords(c));
     else
@@ -1552,7 +1559,9 @@ int surf_trace_any(surf_ctx* c, uint32_t n, const float* o, const float* d, cons
         hipLaunchKernelGGL(k_trace_any_rows, dim3((n + 3) / 4), dim3(64), rowsLds(c), c->stream, c->S, (const float*)dO,
                            (const float*)dD, (const float*)dM, n, dR, recStackWords(c));
     else if (c->traceMode == 1)
-        hipLaunchKernelGGL(c->ldsTables ? k_trace_any_coop<true> : k_trace_any_coop<false>, dim3(n), dim3(64), coopLds(c), c->stream,
+        hipLaunchKernelGGL(c->ldsTables ? (c->S.wnodes ? k_trace_any_coop<true, true> : k_trace_any_coop<true, false>)
+                                        : (c->S.wnodes ? k_trace_any_coop<false, true> : k_trace_any_coop<false, false>),
+                           dim3(n), dim3(64), coopLds(c), c->stream,
                            c->S, (const float*)dO, (const float*)dD,
                            (const float*)dM, n, dR, recStackWords(c));
     else
