@@ -1,0 +1,15 @@
+#!/bin/bash
+# Round-3 bench lines: the default (C3) line, C2 / C4 / C5 lines, and the N = 2
+# bench path rehearsed on one GPU (two ranks sharing device 0, gloo gather;
+# the assembled frame checked against the oracle).  usage: tools/r3_benches.sh OUT
+OUT=${1:-gpurun_out/r3_bench}
+mkdir -p "$OUT"
+timeout -k 10 400 python bench.py > "$OUT/bench_c3.json" 2> "$OUT/bench_c3.err" || { tail -5 "$OUT/bench_c3.err"; exit 1; }
+echo "C3 $(python3 -c "import json;j=json.load(open('$OUT/bench_c3.json'));print(j['value'], j['parity']['bitexact'], j['gpu_vs_cpu'])")"
+for wl in C2 C4 C5; do
+    timeout -k 10 500 python bench.py --workload $wl > "$OUT/bench_${wl,,}.json" 2> "$OUT/bench_${wl,,}.err" || { tail -5 "$OUT/bench_${wl,,}.err"; exit 1; }
+    echo "$wl $(python3 -c "import json;j=json.load(open('$OUT/bench_${wl,,}.json'));print(j['value'], j['parity']['bitexact'], j['gpu_vs_cpu'], j['roofline']['frac'])")"
+done
+SURF_BENCH_BACKEND=gloo timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+    --master-port 29517 bench.py --gpus 2 --steps 2 --warmup 1 > "$OUT/dist_n2.json" 2> "$OUT/dist_n2.err" || { tail -5 "$OUT/dist_n2.err"; exit 1; }
+echo "N2 $(tail -1 $OUT/dist_n2.json | python3 -c "import json,sys;j=json.loads(sys.stdin.read());print(j['value'], j['parity'])")"
