@@ -204,6 +204,13 @@ int surf_set_tail_coop(surf_ctx* ctx, uint32_t max_paths);
  * min(count, 64, max) of them (one per workgroup 0..63 that capped a path;
  * unused entries are 0xffffffff). */
 int surf_debug_capped(surf_ctx* ctx, uint32_t* sample_ids, uint32_t max, uint64_t* count);
+/* Diagnostics: shader-clock cycles of one drain segment's pieces on a lone
+ * wave, each repeated `reps` times on the same path record path12 = (origin,
+ * sample id bits), (direction, flag bits), (throughput, rng state bits):
+ * cycles7[0] closest-hit wave walk, [1] shading, [2] the shadow ray's any-hit
+ * walk, [3] the cosine sample alone, [4] the light sample alone, [5] the hit
+ * normal alone (sums over reps); [6] a checksum.  No reference counterpart. */
+int surf_debug_segment_cycles(surf_ctx* ctx, const float* path12, uint32_t reps, uint64_t* cycles7);
 /* When enabled, per-kernel device times are measured with HIP events on the
  * render stream (slower: disables the graph replay). */
 int surf_set_profiling(surf_ctx* ctx, int enabled);

@@ -2698,4 +2698,95 @@ __global__ __launch_bounds__(64) void k_trace_any_coop(DevScene S, const float* 
     if (threadIdx.x == 0) occ[i] = oc ? 1 : 0;
 }
 
+/* Diagnostics (surf_debug_segment_cycles): the latency of one drain segment's
+ * pieces on a lone wave, each repeated `reps` times on the same inputs (the
+ * cooperative drain's device functions): cyc[0] the closest-hit wave walk
+ * (instance prologue included), cyc[1] shadePath, cyc[2] the shadow ray's
+ * any-hit walk, cyc[3] the cosine sample alone, cyc[4] the light sample
+ * alone, cyc[5] the hit-normal fetch + normalization alone; shader clock
+ * cycles (s_memtime) summed over the repetitions. */
+__device__ __forceinline__ unsigned long long clockNow() {
+    __builtin_amdgcn_s_waitcnt(0);                   /* every memory operation in flight has landed */
+    unsigned long long t = __builtin_amdgcn_s_memtime();
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    uint32_t lo = (uint32_t)t, hi = (uint32_t)(t >> 32);
+    asm volatile("" : "+v"(lo), "+v"(hi));           /* a VGPR value: no scalar value crosses the branches */
+    return ((unsigned long long)hi << 32) | lo;
+}
+template <bool LDS, bool W2>
+__global__ __launch_bounds__(64) void k_segment_cycles(DevScene S, float4 o4, float4 d4, float4 T4, uint32_t reps,
+                                                       unsigned long long* __restrict__ cyc, uint32_t stackWords) {
+    extern __shared__ uint32_t lds[];
+    const TraceTables Tt = coopTrace<LDS>(S, lds, stackWords + proWords(S));
+    const ShadeTables Tb = coopShade<LDS>(S, lds, (stackWords + proWords(S) + S.nInst * (uint32_t)((sizeof(TraceInst) + 4u) / 4u) + 3u) & ~3u);
+    float* rstk = reinterpret_cast<float*>(lds);
+    float4* pro = reinterpret_cast<float4*>(lds + stackWords);
+    unsigned long long c[6] = {0, 0, 0, 0, 0, 0};
+    uint32_t sink = 0;
+    for (uint32_t k = 0; k < reps; ++k) {
+        const unsigned long long t0 = clockNow();
+        float depth = kFarAway, u = 0.0f, v = 0.0f;
+        uint32_t inst = kUnset, prim = kUnset;
+        const bool hit = traceWave<false, W2>(S, Tt, xyz(o4), xyz(d4), depth, u, v, inst, prim, rstk, pro);
+        const unsigned long long t1 = clockNow();
+        ShadeOut r;
+        shadePath<true>(S, Tb, o4, d4, T4, make_float4(depth, u, v, u2f(prim)), hit ? inst : kUnset, 0u, 1u, r);
+        const unsigned long long t2 = clockNow();
+        bool occ = false;
+        if (r.shadow) {
+            float sdep = r.so.w, su = 0.0f, sv = 0.0f;
+            uint32_t si = kUnset, sp = kUnset;
+            occ = traceWave<true, W2>(S, Tt, xyz(r.so), xyz(r.sd), sdep, su, sv, si, sp, rstk, pro);
+        }
+        const unsigned long long t3 = clockNow();
+        c[0] += t1 - t0; c[1] += t2 - t1; c[2] += t3 - t2;
+        sink += (occ ? 1u : 0u) + f2u(r.o.x);
+        /* the pieces alone, on this segment's inputs */
+        if (hit) {
+            const DevInstance& I = Tb.inst[inst];
+            const uint32_t seed0 = f2u(T4.w);
+            V3 N;
+            {
+                const unsigned long long a = clockNow();
+                const float4* nr = S.normals + 3u * (I.triOffset + prim);
+                const float4 n0 = nr[0], n1 = nr[1], n2 = nr[2];
+                const float w = (1.0f - u) - v;
+                const V3 no = add(add(lscl(u, xyz(n0)), lscl(v, xyz(n2))), lscl(w, xyz(n1)));
+                const float* M = I.M;
+                const float nx4 = mrow(M, 0, no.x, no.y, no.z, 0.0f), ny4 = mrow(M, 1, no.x, no.y, no.z, 0.0f);
+                const float nz4 = mrow(M, 2, no.x, no.y, no.z, 0.0f), nw4 = mrow(M, 3, no.x, no.y, no.z, 0.0f);
+                const float nn = (nx4 * nx4 + ny4 * ny4) + (nz4 * nz4 + nw4 * nw4);
+                const float ninv = 1.0f / sqrtf(nn);
+                N = mk3(nx4 * ninv, ny4 * ninv, nz4 * ninv);
+                asm volatile("" : "+v"(N.x), "+v"(N.y), "+v"(N.z));
+                c[5] += clockNow() - a;
+            }
+            {
+                uint32_t sd = seed0;
+                V3 R1;
+                const unsigned long long a = clockNow();
+                const bool ok = cosineTry(sd, N, R1);
+                asm volatile("" : "+v"(R1.x), "+v"(R1.y), "+v"(R1.z));
+                c[3] += clockNow() - a;
+                sink += ok ? 1u : 0u;
+            }
+            {
+                uint32_t sd = seed0;
+                ShadeOut q;
+                q.shadow = false;
+                const V3 P = add(xyz(o4), lscl(depth, xyz(d4)));
+                const unsigned long long a = clockNow();
+                sampleNEE(S, Tb, sd, P, N, mk3(1.0f, 0.0f, 0.0f), mk3(0.3f, 0.0f, 0.0f), 0u, q);
+                asm volatile("" : "+v"(q.so.x), "+v"(q.sc.x));
+                c[4] += clockNow() - a;
+                sink += q.shadow ? 1u : 0u;
+            }
+        }
+    }
+    if (threadIdx.x == 0) {
+        for (int k = 0; k < 6; ++k) cyc[k] = c[k];
+        cyc[6] = sink;
+    }
+}
+
 }  // namespace surfdev

@@ -1576,6 +1576,27 @@ int surf_trace_any(surf_ctx* c, uint32_t n, const float* o, const float* d, cons
     return SURF_OK;
 }
 
+int surf_debug_segment_cycles(surf_ctx* c, const float* path12, uint32_t reps, uint64_t* cycles7) {
+    if (!c || !path12 || !cycles7 || reps == 0) return SURF_ERR_INVALID;
+    if (!c->hasScene) return fail(c, SURF_ERR_NO_SCENE, "no scene uploaded");
+    if (!waveEligible(c)) return fail(c, SURF_ERR_INVALID, "scene does not fit the one-ray-per-wave traversal");
+    SURF_CHECK(c, hipSetDevice(c->device));
+    unsigned long long* d = nullptr;
+    SURF_CHECK(c, hipMalloc(&d, 8 * sizeof(unsigned long long)));
+    const float4 o4 = make_float4(path12[0], path12[1], path12[2], path12[3]);
+    const float4 d4 = make_float4(path12[4], path12[5], path12[6], path12[7]);
+    const float4 T4 = make_float4(path12[8], path12[9], path12[10], path12[11]);
+    const bool w2 = c->S.wnodes != nullptr;
+    hipLaunchKernelGGL(c->ldsTables ? (w2 ? k_segment_cycles<true, true> : k_segment_cycles<true, false>)
+                                    : (w2 ? k_segment_cycles<false, true> : k_segment_cycles<false, false>),
+                       dim3(1), dim3(64), coopTailLds(c), c->stream, c->S, o4, d4, T4, reps, d, recStackWords(c));
+    hipError_t e = hipMemcpyAsync(cycles7, d, 7 * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    (void)hipFree(d);
+    if (e != hipSuccess) return fail(c, SURF_ERR_HIP, std::string("segment cycles: ") + hipGetErrorString(e));
+    return SURF_OK;
+}
+
 /* Host restatements of the glibc kernels' libm, for CPU tests (same source as the device). */
 float surf_ref_sinf(float x) { return surfdev::gSinf(x); }
 float surf_ref_cosf(float x) { return surfdev::gCosf(x); }

@@ -98,6 +98,7 @@ def load() -> C.CDLL:
         "surf_set_pool_capacity": ([P, U32], I32), "surf_set_frame_batch": ([P, U32], I32),
         "surf_set_profiling": ([P, I32], I32), "surf_set_zero_cutoff": ([P, I32], I32), "surf_set_trace_mode": ([P, I32], I32), "surf_set_tail_policy": ([P, U32, U32, U32], I32), "surf_set_tail_coop": ([P, U32], I32),
         "surf_debug_capped": ([P, P, U32, C.POINTER(C.c_uint64)], I32),
+        "surf_debug_segment_cycles": ([P, P, U32, P], I32),
         "surf_upload_scene": ([P, C.POINTER(SceneDesc)], I32),
         "surf_set_camera": ([P, P], I32),
         "surf_render": ([P, U32, U32, U32, U32], I32),
@@ -307,6 +308,23 @@ class Renderer:
         n = C.c_uint64()
         _check(load().surf_debug_capped(self._h, _ptr(ids), 64, C.byref(n)), "surf_debug_capped", self._h)
         return int(n.value), ids[ids != 0xFFFFFFFF]
+
+    def debug_segment_cycles(self, origin, direction, throughput, seed: int, segment: int = 1, reps: int = 64):
+        """Diagnostics: mean shader-clock cycles of one drain segment's pieces on
+        a lone wave (surf_debug_segment_cycles): walk, shade, shadow walk,
+        cosine sample, light sample, hit normal."""
+        rec = np.zeros(12, np.float32)
+        rec[0:3] = origin
+        rec[4:7] = direction
+        rec[8:11] = throughput
+        u = rec.view(np.uint32)
+        u[3] = 0
+        u[7] = (segment << 2)
+        u[11] = seed & 0xFFFFFFFF
+        out = np.zeros(7, np.uint64)
+        _check(load().surf_debug_segment_cycles(self._h, _ptr(rec), reps, _ptr(out)), "surf_debug_segment_cycles", self._h)
+        names = ("walk", "shade", "shadow_walk", "cosine", "light_sample", "normal")
+        return {k: float(out[i]) / reps for i, k in enumerate(names)}
 
     def set_zero_cutoff(self, on: bool):
         _check(load().surf_set_zero_cutoff(self._h, 1 if on else 0), "surf_set_zero_cutoff", self._h)
