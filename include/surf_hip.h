@@ -209,8 +209,11 @@ int surf_debug_capped(surf_ctx* ctx, uint32_t* sample_ids, uint32_t max, uint64_
  * sample id bits), (direction, flag bits), (throughput, rng state bits):
  * cycles7[0] closest-hit wave walk, [1] shading, [2] the shadow ray's any-hit
  * walk, [3] the cosine sample alone, [4] the light sample alone, [5] the hit
- * normal alone (sums over reps); [6] a checksum.  No reference counterpart. */
-int surf_debug_segment_cycles(surf_ctx* ctx, const float* path12, uint32_t reps, uint64_t* cycles7);
+ * normal alone (sums over reps); [6] a checksum; [7..14] with a walk-profile
+ * build (SURF_WALK_PROFILE) the closest and any-hit walks' split: interior
+ * cycles, leaf cycles, walks, leaves, triangles, two-level visits, prologue
+ * cycles, instance-loop cycles (else 0).  No reference counterpart. */
+int surf_debug_segment_cycles(surf_ctx* ctx, const float* path12, uint32_t reps, uint64_t* cycles15);
 /* When enabled, per-kernel device times are measured with HIP events on the
  * render stream (slower: disables the graph replay). */
 int surf_set_profiling(surf_ctx* ctx, int enabled);

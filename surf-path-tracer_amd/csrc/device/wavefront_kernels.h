@@ -1169,6 +1169,7 @@ __device__ __forceinline__ bool blasWave(const DevScene& S, const TraceInst& I, 
     "v_readlane_b32 %[lf], %[st], 12\n\t"                                                              \
     "s_cmp_lg_u32 %[cnt], 0\n\t"                                                                       \
     "s_cbranch_scc1 L_exit_%=\n\t"                                                                     \
+    SURF_W2_VISIT                                                                                      \
     /* candidate loads: W of the grandchildren (n0..n3) and of the children (f0, f1) */                \
     "v_readlane_b32 %[lfL], %[st], 28\n\t"                                                             \
     "v_readlane_b32 %[lfR], %[st], 44\n\t"                                                             \
@@ -1271,9 +1272,10 @@ __device__ __forceinline__ bool blasWave(const DevScene& S, const TraceInst& I, 
     "v_readlane_b32 %[lf], %[st], %[idx]\n\t"                                                          \
     "v_add_u32 %[addr], %[sp], %[stk]\n\t"                                                             \
     "s_waitcnt vmcnt(0)\n\t"                                                                           \
+    "v_cndmask_b32_e64 %[t], %[f1], %[f0], %[sc]\n\t"                                                  \
+    "v_cndmask_b32_e64 %[st], %[f0], %[f1], %[sc]\n\t"   /* W(C): the leaf's triangles */              \
     "s_cmp_eq_u32 %[b0], 0\n\t"                                                                        \
     "s_cbranch_scc1 L_exit_%=\n\t"                                                                     \
-    "v_cndmask_b32_e64 %[t], %[f1], %[f0], %[sc]\n\t"                                                  \
     "ds_write_b32 %[addr], %[t]\n\t"                                                                   \
     "s_add_u32 %[sp], %[sp], 256\n\t"                                                                  \
     "s_branch L_exit_%=\n"                                                                             \
@@ -1301,7 +1303,7 @@ __device__ __forceinline__ bool blasWave(const DevScene& S, const TraceInst& I, 
     "L_exit_%=:"
 
 #define SURF_W2_OPERANDS                                                                               \
-    : [st] "+v"(st), [sp] "+s"(spb), [lf] "=&s"(lf), [cnt] "=&s"(cnt), [n0] "=&v"(n0), [n1] "=&v"(n1),  \
+    : [st] "+v"(st), [sp] "+s"(spb), [nv] "+s"(nv), [lf] "=&s"(lf), [cnt] "=&s"(cnt), [n0] "=&v"(n0), [n1] "=&v"(n1),  \
       [n2] "=&v"(n2), [n3] "=&v"(n3), [f0] "=&v"(f0), [f1] "=&v"(f1), [t] "=&v"(t), [t0a] "=&v"(t0a),    \
       [t1a] "=&v"(t1a), [m0] "=&v"(m0), [m1] "=&v"(m1), [mp] "=&v"(mp), [ta] "=&v"(ta), [tb] "=&v"(tb),  \
       [sl0] "=&v"(sl0), [addr] "=&v"(addr), [lfL] "=&s"(lfL), [lfR] "=&s"(lfR), [o0] "=&s"(o0),          \
@@ -1312,9 +1314,28 @@ __device__ __forceinline__ bool blasWave(const DevScene& S, const TraceInst& I, 
       [stk] "v"(stkLane), [m410] "s"(m410)                                                               \
     : "memory", "scc"
 
+/* SURF_WALK_PROFILE builds (diagnostics, surf_debug_segment_cycles): cycles and
+ * counts of the wave walk's parts, accumulated by lane 0 of a lone wave */
+#ifndef SURF_WALK_PROFILE
+#define SURF_WALK_PROFILE 0
+#endif
+__device__ unsigned long long g_walkProf[8];   /* interior cycles, leaf cycles, walks, leaves, triangles, 2-level visits, prologue cycles, instance loop cycles */
+__device__ __forceinline__ unsigned long long profClock() {
+    __builtin_amdgcn_s_waitcnt(0);
+    return __builtin_amdgcn_s_memtime();
+}
+__device__ __forceinline__ void profAdd(int k, unsigned long long v) {
+    if (SURF_WALK_PROFILE && __lane_id() == 0) g_walkProf[k] += v;
+}
+#if SURF_WALK_PROFILE
+#define SURF_W2_VISIT "s_add_u32 %[nv], %[nv], 1\n\t"
+#else
+#define SURF_W2_VISIT ""
+#endif
+
 template <bool ANY>
 __device__ __forceinline__ void walk2Fin(float& st, uint32_t& spb, uint32_t& lf, uint32_t& cnt, float oA, float rdA, float depth,
-                                         surfI4 rsrc, uint32_t laneOff, uint32_t stkLane) {
+                                         surfI4 rsrc, uint32_t laneOff, uint32_t stkLane, uint32_t& nv) {
     float n0, n1, n2, n3, f0, f1, t, t0a, t1a, m0, m1, mp, ta, tb, sl0;
     uint32_t addr, lfL, lfR, o0, o2, of, c, cc, k16, idx, b0, b1;
     unsigned long long h, tt, g = 0, a, sc, scc, sb0;
@@ -1328,6 +1349,43 @@ __device__ __forceinline__ void walk2Fin(float& st, uint32_t& spb, uint32_t& lf,
                      SURF_W2_OPERANDS);
     }
 }
+
+/* A leaf of <= 3 triangles whose two-level record W(leaf) holds them (row j:
+ * lanes 0..2 v0, 3..5 e1, 6..8 e2, 9 prim -- surf_upload_scene), in st: every
+ * lane of row j takes triangle j's components by DPP row_newbcast, tests it
+ * (triHitFlat), and the hits are accepted in index order as leafWave does --
+ * with no memory trip: the record came with the visit's candidate loads. */
+template <int L>
+__device__ __forceinline__ float rowBcast(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x150 + L, 0xF, 0xF, false));
+}
+template <bool ANY>
+__device__ __forceinline__ bool leafWaveW(float st, uint32_t cnt, V3 o, V3 d, float& depth, float& hu, float& hv, uint32_t& hprim) {
+    const uint32_t row = __lane_id() >> 4;
+    const V3 v0 = mk3(rowBcast<0>(st), rowBcast<1>(st), rowBcast<2>(st));
+    const V3 e1 = mk3(rowBcast<3>(st), rowBcast<4>(st), rowBcast<5>(st));
+    const V3 e2 = mk3(rowBcast<6>(st), rowBcast<7>(st), rowBcast<8>(st));
+    const uint32_t prim = f2u(rowBcast<9>(st));
+    float t = depth, u = 0.0f, v = 0.0f;
+    const bool h = row < cnt && triHitFlat(v0, e1, e2, o, d, depth, t, u, v);
+    unsigned long long m = __ballot(h) & 0x0000000100010001ull;   /* lane 16 j: triangle j hit */
+    if (ANY) return m != 0ull;
+    bool any = false;
+    while (m) {
+        const int j = __ffsll((long long)m) - 1;
+        m &= m - 1ull;
+        const float tj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t), j));
+        if (tj < depth) {
+            depth = tj;
+            hu = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(u), j));
+            hv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
+            hprim = (uint32_t)__builtin_amdgcn_readlane((int)prim, j);
+            any = true;
+        }
+    }
+    return any;
+}
+constexpr uint32_t kLeafInW = 3;     /* triangles a two-level leaf record holds */
 
 /* blasWalk with two-level visits (S.wnodes): the DFS below one BLAS root from
  * W(root) -- its first visit re-tests the root's children at the current
@@ -1347,16 +1405,24 @@ __device__ __forceinline__ bool blasWalk2(const DevScene& S, uint32_t nodeOff, c
     waitLoads(st);
     uint32_t sp = 0u;
     bool any = false;
+    uint32_t nv = 0u;
+    if (SURF_WALK_PROFILE) profAdd(2, 1);
     for (;;) {
         uint32_t lf, cnt;
         const float dS = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(depth)));   /* wave-uniform */
-        walk2Fin<ANY>(st, sp, lf, cnt, oA, rdA, dS, rsrc, laneOff, stkLane);
-        if (cnt == 0u) return any;
-        if (leafWave<ANY>(tri, lf, cnt, o, d, depth, hu, hv, hprim)) {
-            if (ANY) return true;
+        unsigned long long tA = 0;
+        if (SURF_WALK_PROFILE) tA = profClock();
+        walk2Fin<ANY>(st, sp, lf, cnt, oA, rdA, dS, rsrc, laneOff, stkLane, nv);
+        if (SURF_WALK_PROFILE) { const unsigned long long tB = profClock(); profAdd(0, tB - tA); tA = tB; }
+        if (cnt == 0u) { if (SURF_WALK_PROFILE) profAdd(5, nv); return any; }
+        const bool lh = cnt <= kLeafInW ? leafWaveW<ANY>(st, cnt, o, d, depth, hu, hv, hprim)
+                                         : leafWave<ANY>(tri, lf, cnt, o, d, depth, hu, hv, hprim);
+        if (SURF_WALK_PROFILE) { profAdd(1, profClock() - tA); profAdd(3, 1); profAdd(4, cnt); }
+        if (lh) {
+            if (ANY) { if (SURF_WALK_PROFILE) profAdd(5, nv); return true; }
             any = true;
         }
-        if (sp == 0u) return any;
+        if (sp == 0u) { if (SURF_WALK_PROFILE) profAdd(5, nv); return any; }
         sp -= 256u;
         st = rs[sp / 4u + lane];
     }
@@ -1521,9 +1587,12 @@ __device__ __forceinline__ bool traceWave(const DevScene& S, const TraceTables& 
      * and its loads every segment */
     const V3 rdw = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     const bool cullOk = finite3(o) && finite3(rdw);
+    unsigned long long tP = 0;
+    if (SURF_WALK_PROFILE) tP = profClock();
     bool keep = false;
     if (lane < nI) keep = waveProEntry(Tt.inst[Tt.order[lane]], o, d, rdw, cullOk, depth, pro + 4u * lane);
     unsigned long long cand = __ballot(keep);
+    if (SURF_WALK_PROFILE) { const unsigned long long t = profClock(); profAdd(6, t - tP); tP = t; }
     while (cand) {
         const uint32_t k = (uint32_t)(__ffsll((long long)cand) - 1);
         cand &= cand - 1ull;
@@ -1544,6 +1613,7 @@ __device__ __forceinline__ bool traceWave(const DevScene& S, const TraceTables& 
 #if SURF_SEG_TIMING
     if (ss) ss->cycInst += segClock() - t0;
 #endif
+    if (SURF_WALK_PROFILE) profAdd(7, profClock() - tP);
     return any;
 }
 
@@ -2786,6 +2856,7 @@ __global__ __launch_bounds__(64) void k_segment_cycles(DevScene S, float4 o4, fl
     if (threadIdx.x == 0) {
         for (int k = 0; k < 6; ++k) cyc[k] = c[k];
         cyc[6] = sink;
+        for (int k = 0; k < 8; ++k) { cyc[7 + k] = g_walkProf[k]; g_walkProf[k] = 0ull; }
     }
 }
 

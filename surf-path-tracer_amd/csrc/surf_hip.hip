@@ -1234,6 +1234,12 @@ int surf_upload_scene(surf_ctx* c, const surf_scene_desc* d) {
                 W[48 * g + 16 * row + 15] = u2f(packLeaf((uint64_t)owner[src] + q.left_first + 1));
             }
         };
+        /* a leaf's W holds its own record in row 0 and, for <= kLeafInW
+         * triangles, the triangles themselves (row j: lanes 0..2 v0, 3..5 e1,
+         * 6..8 e2, 9 prim -- the BVH-ordered records of its index slots), so the
+         * wave walk tests them from the record its visit loaded (leafWaveW) */
+        std::map<uint32_t, uint32_t> idxOfNode;                      /* BLAS node offset -> index offset */
+        for (uint32_t i = 0; i < d->instance_count; ++i) idxOfNode[d->instances[i].bvh_node_offset] = d->instances[i].bvh_idx_offset;
         for (uint32_t g = 0; g < d->blas_node_count; ++g) {
             if (owner[g] == kUnset) continue;
             putRec(g, 0, g);
@@ -1241,6 +1247,16 @@ int surf_upload_scene(surf_ctx* c, const surf_scene_desc* d) {
             if (n.count == 0) {
                 putRec(g, 1, (uint64_t)owner[g] + n.left_first);
                 putRec(g, 2, (uint64_t)owner[g] + n.left_first + 1);
+            } else if (n.count <= kLeafInW) {
+                const uint64_t slot0 = (uint64_t)idxOfNode[owner[g]] + n.left_first;
+                for (uint32_t j = 0; j < n.count; ++j) {
+                    const float4* t = &tris[3 * (slot0 + j)];
+                    float* w = &W[48 * (size_t)g + 16 * j];
+                    w[0] = t[0].x; w[1] = t[0].y; w[2] = t[0].z;
+                    w[3] = t[1].x; w[4] = t[1].y; w[5] = t[1].z;
+                    w[6] = t[2].x; w[7] = t[2].y; w[8] = t[2].z;
+                    w[9] = t[0].w;
+                }
             }
         }
         const float* dW = nullptr;
@@ -1576,13 +1592,13 @@ int surf_trace_any(surf_ctx* c, uint32_t n, const float* o, const float* d, cons
     return SURF_OK;
 }
 
-int surf_debug_segment_cycles(surf_ctx* c, const float* path12, uint32_t reps, uint64_t* cycles7) {
-    if (!c || !path12 || !cycles7 || reps == 0) return SURF_ERR_INVALID;
+int surf_debug_segment_cycles(surf_ctx* c, const float* path12, uint32_t reps, uint64_t* cycles15) {
+    if (!c || !path12 || !cycles15 || reps == 0) return SURF_ERR_INVALID;
     if (!c->hasScene) return fail(c, SURF_ERR_NO_SCENE, "no scene uploaded");
     if (!waveEligible(c)) return fail(c, SURF_ERR_INVALID, "scene does not fit the one-ray-per-wave traversal");
     SURF_CHECK(c, hipSetDevice(c->device));
     unsigned long long* d = nullptr;
-    SURF_CHECK(c, hipMalloc(&d, 8 * sizeof(unsigned long long)));
+    SURF_CHECK(c, hipMalloc(&d, 16 * sizeof(unsigned long long)));
     const float4 o4 = make_float4(path12[0], path12[1], path12[2], path12[3]);
     const float4 d4 = make_float4(path12[4], path12[5], path12[6], path12[7]);
     const float4 T4 = make_float4(path12[8], path12[9], path12[10], path12[11]);
@@ -1590,7 +1606,7 @@ int surf_debug_segment_cycles(surf_ctx* c, const float* path12, uint32_t reps, u
     hipLaunchKernelGGL(c->ldsTables ? (w2 ? k_segment_cycles<true, true> : k_segment_cycles<true, false>)
                                     : (w2 ? k_segment_cycles<false, true> : k_segment_cycles<false, false>),
                        dim3(1), dim3(64), coopTailLds(c), c->stream, c->S, o4, d4, T4, reps, d, recStackWords(c));
-    hipError_t e = hipMemcpyAsync(cycles7, d, 7 * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream);
+    hipError_t e = hipMemcpyAsync(cycles15, d, 15 * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     (void)hipFree(d);
     if (e != hipSuccess) return fail(c, SURF_ERR_HIP, std::string("segment cycles: ") + hipGetErrorString(e));

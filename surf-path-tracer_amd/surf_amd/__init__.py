@@ -321,10 +321,11 @@ class Renderer:
         u[3] = 0
         u[7] = (segment << 2)
         u[11] = seed & 0xFFFFFFFF
-        out = np.zeros(7, np.uint64)
+        out = np.zeros(15, np.uint64)
         _check(load().surf_debug_segment_cycles(self._h, _ptr(rec), reps, _ptr(out)), "surf_debug_segment_cycles", self._h)
-        names = ("walk", "shade", "shadow_walk", "cosine", "light_sample", "normal")
-        return {k: float(out[i]) / reps for i, k in enumerate(names)}
+        names = ("walk", "shade", "shadow_walk", "cosine", "light_sample", "normal", "checksum", "interior_cycles",
+                 "leaf_cycles", "walks", "leaves", "triangles", "visits2", "prologue_cycles", "instance_loop_cycles")
+        return {k: float(out[i]) / reps for i, k in enumerate(names) if k != "checksum"}
 
     def set_zero_cutoff(self, on: bool):
         _check(load().surf_set_zero_cutoff(self._h, 1 if on else 0), "surf_set_zero_cutoff", self._h)
