@@ -2793,6 +2793,15 @@ __global__ __launch_bounds__(64) void k_segment_cycles(DevScene S, float4 o4, fl
     float4* pro = reinterpret_cast<float4*>(lds + stackWords);
     unsigned long long c[6] = {0, 0, 0, 0, 0, 0};
     uint32_t sink = 0;
+    if (reps & 0x80000000u) {
+        /* the closest-hit wave walk alone (for PMC counters of just the walk) */
+        for (uint32_t k = 0; k < (reps & 0x7FFFFFFFu); ++k) {
+            float depth = kFarAway, u = 0.0f, v = 0.0f;
+            uint32_t inst = kUnset, prim = kUnset;
+            sink += traceWave<false, W2>(S, Tt, xyz(o4), xyz(d4), depth, u, v, inst, prim, rstk, pro) ? prim : 0u;
+        }
+        reps = 0;
+    }
     for (uint32_t k = 0; k < reps; ++k) {
         const unsigned long long t0 = clockNow();
         float depth = kFarAway, u = 0.0f, v = 0.0f;
