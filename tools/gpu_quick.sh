@@ -6,7 +6,7 @@ mkdir -p "$OUT"
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
     -k "drain_policies or general_tlas or render_64 or c1_256 or closest_hit or any_hit" > "$OUT/pytest.log" 2>&1
 rc=$?; tail -2 "$OUT/pytest.log"; [ $rc -ne 0 ] && exit $rc
-timeout -k 10 120 python tools/chain_probe2.py > "$OUT/chain.txt" 2>&1 || exit 1
+timeout -k 10 120 python tools/chain_probe.py > "$OUT/chain.txt" 2>&1 || exit 1
 tail -1 "$OUT/chain.txt"
 timeout -k 10 200 python tools/shard_breakdown.py 8 1 > "$OUT/shard.txt" 2>&1 || exit 1
 sed -n 2,3p "$OUT/shard.txt"

@@ -1,5 +1,5 @@
 """Where a drain segment's latency goes (diagnostics): surf_debug_segment_cycles
-on extension rays of the long C3 path of tools/chain_probe2.py (pixel 630758,
+on extension rays of the long C3 path of tools/chain_probe.py (pixel 630758,
 frame 0: 3086 segments inside the red Suzanne; rays recorded once from the
 oracle into tools/chainpath_rays.npz), one lone wave, each piece repeated.
     python tools/segment_cycles.py [N_RAYS]"""
