@@ -137,6 +137,11 @@ typedef struct surf_scene surf_scene;   /* host-side scene built by this library
 
 /* ---- version / device ---- */
 int surf_abi_version(void);
+/* Optional engines compiled into this library (bit mask): SURF_FEATURE_ROWS_ENGINE
+ * -- the four-paths-per-wave drain and trace mode 2 (make ROWS=1; measured
+ * equal to the default partner-wave drain).  No reference counterpart. */
+#define SURF_FEATURE_ROWS_ENGINE 1
+int surf_build_features(void);
 int surf_device_count(int* count);
 
 /* ---- context ----

@@ -24,7 +24,14 @@
 
 #include "surf_hip.h"
 #include "device/wavefront_kernels.h"
+/* The four-paths-per-wave engine (k_tail_rows, trace mode 2) is measured equal
+ * to the partner-wave drain and built only with SURF_ROWS_ENGINE=1 (make ROWS=1). */
+#ifndef SURF_ROWS_ENGINE
+#define SURF_ROWS_ENGINE 0
+#endif
+#if SURF_ROWS_ENGINE
 #include "device/rows_tail.h"
+#endif
 
 using namespace surfdev;
 
@@ -194,9 +201,11 @@ uint32_t stackWords(const surf_ctx* c, uint32_t block) { return c->stackDepth * 
  * entry -- 64 with two-level records (blasWalk2 pushes whole W records) */
 uint32_t recStackWords(const surf_ctx* c) { return c->stackDepth * (c->S.wnodes ? 64u : 16u); }
 /* Dynamic LDS of the four-rows kernels: four record stacks, then the trace tables. */
+#if SURF_ROWS_ENGINE
 size_t rowsLds(const surf_ctx* c) {
     return ((size_t)4 * recStackWords(c) + kRowProWords) * sizeof(float) + (size_t)c->nInstances * (sizeof(TraceInst) + sizeof(uint32_t));
 }
+#endif
 /* Dynamic LDS of the one-ray-per-wave kernels: the record stack, the prologue
  * table (16 words per instance), then the trace tables; k_tail_coop adds the
  * shading tables (coopTailLds). */
@@ -581,7 +590,11 @@ void launchTail(surf_ctx* c, Pool in, uint32_t n, uint32_t lpw, uint32_t firstCo
  * instances); the TLAS stack is one VGPR (<= 64 entries). */
 bool waveEligible(const surf_ctx* c) { return c->hasScene && c->stackDepth <= 64 && coopLdsOk(c); }
 /* The four-rows traversal: a single-leaf TLAS with at most one instance per lane of a row, LDS tables. */
+#if SURF_ROWS_ENGINE
 bool rowsEligible(const surf_ctx* c) { return waveEligible(c) && c->coopEligible && c->S.tlasLeafCount <= kRowInst; }
+#else
+bool rowsEligible(const surf_ctx*) { return false; }
+#endif
 
 /* Regen counted each pool-0 path's next extension ray (firstCounted). */
 int runTail(surf_ctx* c) {
@@ -600,6 +613,7 @@ int runTail(surf_ctx* c) {
             const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
             std::fprintf(stderr, "[surf tail] stage %d: %u paths at %.2f ms\n", stage, cnt, ms);
         }
+#if SURF_ROWS_ENGINE
         if (c->tailRows && rowsEligible(c) && cnt <= c->coopAll) {
             /* every remaining path through the row queue: as many four-row
              * waves as are resident at once, each row taking the next path
@@ -612,6 +626,7 @@ int runTail(surf_ctx* c) {
             c->stats.tail_survivors += cnt;
             break;
         }
+#endif
         if (c->tailPair && waveEligible(c) && cnt <= c->coopAll) {
             /* as many two-wave workgroups as are resident at once, each wave
              * taking paths from the queue; idle waves trace their sibling's
@@ -850,6 +865,8 @@ extern "C" {
 
 int surf_abi_version(void) { return SURF_ABI_VERSION; }
 
+int surf_build_features(void) { return SURF_ROWS_ENGINE ? SURF_FEATURE_ROWS_ENGINE : 0; }
+
 int surf_device_count(int* count) {
     if (!count) return SURF_ERR_INVALID;
     *count = 0;
@@ -967,6 +984,8 @@ int surf_set_trace_mode(surf_ctx* c, int mode) {
     if (mode < 0 || mode > 2) return fail(c, SURF_ERR_INVALID, "trace mode must be 0, 1 or 2");
     if (mode == 1 && !waveEligible(c))
         return fail(c, SURF_ERR_INVALID, "one-ray-per-wave traversal needs a BVH stack <= 64 entries");
+    if (mode == 2 && !SURF_ROWS_ENGINE)
+        return fail(c, SURF_ERR_INVALID, "one-ray-per-row traversal: this build has no rows engine (make ROWS=1)");
     if (mode == 2 && !rowsEligible(c))
         return fail(c, SURF_ERR_INVALID, "one-ray-per-row traversal needs a single-leaf TLAS of <= 16 instances and a BVH stack <= 64");
     c->traceMode = mode;
@@ -1531,10 +1550,13 @@ int surf_trace_closest(surf_ctx* c, uint32_t n, const float* o, const float* d, 
         (rc = devAlloc(c, tmp, &dT, n)) || (rc = devAlloc(c, tmp, &dI, n))) { freeList(tmp); return rc; }
     (void)hipMemcpyAsync(dO, o, 12 * (size_t)n, hipMemcpyHostToDevice, c->stream);
     (void)hipMemcpyAsync(dD, d, 12 * (size_t)n, hipMemcpyHostToDevice, c->stream);
+#if SURF_ROWS_ENGINE
     if (c->traceMode == 2)
         hipLaunchKernelGGL(k_trace_closest_rows, dim3((n + 3) / 4), dim3(64), rowsLds(c), c->stream, c->S, (const float*)dO,
                            (const float*)dD, n, dT, dI, recStackWords(c));
-    else if (c->traceMode == 1)
+    else
+#endif
+    if (c->traceMode == 1)
         hipLaunchKernelGGL(c->ldsTables ? (c->S.wnodes ? k_trace_closest_coop<true, true> : k_trace_closest_coop<true, false>)
                                         : (c->S.wnodes ? k_trace_closest_coop<false, true> : k_trace_closest_coop<false, false>),
                            dim3(n), dim3(64), coopLds(c),
@@ -1571,10 +1593,13 @@ int surf_trace_any(surf_ctx* c, uint32_t n, const float* o, const float* d, cons
     (void)hipMemcpyAsync(dO, o, 12 * (size_t)n, hipMemcpyHostToDevice, c->stream);
     (void)hipMemcpyAsync(dD, d, 12 * (size_t)n, hipMemcpyHostToDevice, c->stream);
     (void)hipMemcpyAsync(dM, tm, 4 * (size_t)n, hipMemcpyHostToDevice, c->stream);
+#if SURF_ROWS_ENGINE
     if (c->traceMode == 2)
         hipLaunchKernelGGL(k_trace_any_rows, dim3((n + 3) / 4), dim3(64), rowsLds(c), c->stream, c->S, (const float*)dO,
                            (const float*)dD, (const float*)dM, n, dR, recStackWords(c));
-    else if (c->traceMode == 1)
+    else
+#endif
+    if (c->traceMode == 1)
         hipLaunchKernelGGL(c->ldsTables ? (c->S.wnodes ? k_trace_any_coop<true, true> : k_trace_any_coop<true, false>)
                                         : (c->S.wnodes ? k_trace_any_coop<false, true> : k_trace_any_coop<false, false>),
                            dim3(n), dim3(64), coopLds(c), c->stream,

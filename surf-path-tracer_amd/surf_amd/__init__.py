@@ -90,7 +90,7 @@ def load() -> C.CDLL:
     lib = C.CDLL(path)
     P, U32, I32, F = C.c_void_p, C.c_uint32, C.c_int, C.c_float
     sig = {
-        "surf_abi_version": ([], I32), "surf_device_count": ([C.POINTER(I32)], I32),
+        "surf_abi_version": ([], I32), "surf_build_features": ([], I32), "surf_device_count": ([C.POINTER(I32)], I32),
         "surf_create": ([I32, U32, U32, U32, U32, C.POINTER(P)], I32),
         "surf_create_sharded": ([I32, U32, U32, U32, U32, U32, C.POINTER(P)], I32),
         "surf_destroy": ([P], None), "surf_last_error": ([P], C.c_char_p),
@@ -144,6 +144,14 @@ def device_count() -> int:
     n = C.c_int(0)
     rc = load().surf_device_count(C.byref(n))
     return n.value if rc == SURF_OK else 0
+
+
+FEATURE_ROWS_ENGINE = 1
+
+
+def rows_engine() -> bool:
+    """Whether the library was built with the four-paths-per-wave engine (make ROWS=1)."""
+    return bool(load().surf_build_features() & FEATURE_ROWS_ENGINE)
 
 
 class Scene:
