@@ -91,6 +91,7 @@ def parse():
                     help="renders re-run with per-kernel HIP events for the roofline (0 = none)")
     ap.add_argument("--tail", type=str, default="", help="tuning: drain policy 'threshold,lanes_per_wave,stage_segments'")
     ap.add_argument("--tail-coop", type=int, default=-1, help="tuning: cooperative drain when <= N paths remain")
+    ap.add_argument("--pool", type=int, default=0, help="tuning: paths in flight (0: the library default, ~4 frames)")
     return ap.parse_args()
 
 
@@ -268,7 +269,7 @@ def main():
     scene = surf_amd.Scene.indoor(variant=1 if wl["scene"] == "c5" else 0)
     scene_build_s = time.perf_counter() - tb
     spec = surf_amd.ShardSpec(rank, world, args.row_block if world > 1 else 0)
-    r = surf_amd.Renderer(scene, W, H, device=local, shard=spec)
+    r = surf_amd.Renderer(scene, W, H, device=local, shard=spec, pool_capacity=args.pool or None)
     if args.tail:
         r.set_tail_policy(*[int(x) for x in args.tail.split(",")])
     if args.tail_coop >= 0:
