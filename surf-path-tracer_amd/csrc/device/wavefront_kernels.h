@@ -102,6 +102,10 @@ struct DevScene {
     uint32_t bgType;
     float bgColor[3], bgA[3], bgB[3];
     float cellLo[3], cellScale[3];   /* ray-order cells: the TLAS root box split in 2 per axis (scale 0: one cell) */
+    /* ray-order membership key (single-leaf TLAS): the world boxes of the (at
+     * most 3) instances with the largest BLASes; keyMode 1: pool key by them */
+    uint32_t nHeavy, keyMode;
+    float4 hvLo[3], hvHi[3];
 };
 
 struct DevCamera {
@@ -1674,21 +1678,46 @@ constexpr uint32_t kSortThreads = 1024; /* threads per k_bincount / k_binscatter
 #endif
 static_assert(kBins <= 256u, "pool/shadow keys are one byte");
 
-/* Pool order key: the instance the path starts on (<= 14; camera rays: kBins - 1)
- * x the x/z quadrant of the scene box holding its origin.  1 M recorded
- * extension rays (tools/order_probe.py, order_probe2.py): 634 us shuffled,
- * 345 by start instance, 334 by start x quadrant. */
+/* Which of the heavy instances' world boxes the ray's line meets in [0, tmax)
+ * (bit h for S.hvLo/hvHi[h]).  A sort key only -- approximate reciprocals and
+ * any NaN outcome are fine: the order of traversal changes no ray's result. */
+__device__ __forceinline__ uint32_t heavyMask(const DevScene& S, float4 o, float4 d, float tmax) {
+    const float rx = __builtin_amdgcn_rcpf(d.x), ry = __builtin_amdgcn_rcpf(d.y), rz = __builtin_amdgcn_rcpf(d.z);
+    uint32_t m = 0;
+    for (uint32_t h = 0; h < S.nHeavy; ++h) {
+        const float4 lo = S.hvLo[h], hi = S.hvHi[h];
+        const float tx0 = (lo.x - o.x) * rx, tx1 = (hi.x - o.x) * rx;
+        const float ty0 = (lo.y - o.y) * ry, ty1 = (hi.y - o.y) * ry;
+        const float tz0 = (lo.z - o.z) * rz, tz1 = (hi.z - o.z) * rz;
+        const float t0 = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fminf(tz0, tz1));
+        const float t1 = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
+        m |= (t1 >= t0 && t1 > 0.0f && t0 < tmax) ? (1u << h) : 0u;
+    }
+    return m;
+}
+
+/* Pool order key.  Default (single-leaf TLAS with heavy instances): which of
+ * the heavy BLASes the ray's line reaches x the x/z quadrant of its origin, so
+ * a wave's lanes enter the same expensive BVHs -- the wave-uniform instance
+ * loop pays, per instance, its slowest lane in it (recorded C3 extension rays,
+ * lock-step visit steps per 64 rays, tools/lockstep_sim.cpp: 53.8 by start
+ * instance x quadrant, 37.7 by heavy-instance mask).  Otherwise the instance
+ * the path starts on (<= 14; camera rays: kBins - 1) x the quadrant: 1 M
+ * recorded extension rays (tools/order_probe.py, order_probe2.py): 634 us
+ * shuffled, 345 by start instance, 334 by start x quadrant. */
 __device__ __forceinline__ uint8_t poolKey(const DevScene& S, uint32_t inst, float4 o, float4 d) {
     const uint32_t cx = (o.x - S.cellLo[0]) * S.cellScale[0] >= 1.0f ? 1u : 0u;
     const uint32_t cz = (o.z - S.cellLo[2]) * S.cellScale[2] >= 1.0f ? 1u : 0u;
-    (void)d;
+    if (S.keyMode) return (uint8_t)(heavyMask(S, o, d, kFarAway) * 4u + cx + 2u * cz);
     return (uint8_t)((inst < 14u ? inst : 14u) * 4u + cx + 2u * cz);
 }
 
 /* Shadow-ray order key: light slot (mod 2) x the octant cell of the scene box
  * holding the ray's origin.  1 M recorded shadow rays (tools/order_probe2.py):
  * 340 us shuffled, 277 sorted by light, 238 by light x octant cell, 286 by
- * light x 4x4x4 cells (too fine: the bins stop sharing paths through the BVH). */
+ * light x 4x4x4 cells (too fine: the bins stop sharing paths through the BVH).
+ * The pool's heavy-instance mask (of the segment [0, tmax)) x light x x/z
+ * quadrant was measured slower: k_connect 147 -> 174 ms per C3 render. */
 __device__ __forceinline__ uint8_t shadowKey(const DevScene& S, uint32_t light, float4 o) {
     uint32_t cell = 0;
     const float p[3] = {o.x, o.y, o.z};

@@ -86,6 +86,8 @@ struct surf_ctx {
     uint32_t nMaterials = 0, nLightsUp = 0, tlasNodeCount = 0, maxBlasDepth = 0;
     std::map<std::tuple<uint32_t, uint32_t, uint32_t>, std::array<float4, 4>> blasRoots;  /* (node, idx, tri offset) -> root record */
     std::map<uint32_t, std::array<double, 6>> blasBounds;   /* tri offset -> bounds of its BLAS's triangles (v0, v0+e1, v0+e2) */
+    std::map<uint32_t, uint32_t> blasSlots;                  /* tri offset -> index slots (triangles) of its BLAS */
+    uint32_t keyMode = 1;          /* pool ray-order key (SURF_KEY): 1 heavy-instance mask x quadrant, 0 start instance x quadrant */
     /* camera */
     bool hasCamera = false;
     DevCamera cam{};
@@ -837,6 +839,7 @@ int createCtx(int dev, uint32_t w, uint32_t h, std::vector<uint32_t> rows, surf_
         c->sortShadow = e[0] != '2';
     }
     if (const char* e = std::getenv("SURF_CONNECT_GLOBAL")) c->connectGlobal = e[0] != '0';
+    if (const char* e = std::getenv("SURF_KEY")) c->keyMode = e[0] == '0' ? 0u : 1u;
     if (const char* e = std::getenv("SURF_TAIL_ROWS")) c->tailRows = e[0] == '1';
     if (const char* e = std::getenv("SURF_TAIL_PAIR")) c->tailPair = e[0] != '0';
     c->width = w;
@@ -1018,7 +1021,19 @@ struct InstanceTables {
     std::vector<uint32_t> tidx;
     std::vector<uint2> lights;
     uint32_t tlasDepth = 0, tlasLeafCount = 0;
+    uint32_t nHeavy = 0;
+    float4 hvLo[3], hvHi[3];
 };
+
+/* The heavy-instance boxes of the ray-order keys (kernel arguments). */
+void setKeys(const surf_ctx* c, DevScene& S, const InstanceTables& T) {
+    S.nHeavy = T.nHeavy;
+    for (uint32_t h = 0; h < 3; ++h) {
+        S.hvLo[h] = h < T.nHeavy ? T.hvLo[h] : make_float4(0, 0, 0, 0);
+        S.hvHi[h] = h < T.nHeavy ? T.hvHi[h] : make_float4(0, 0, 0, 0);
+    }
+    S.keyMode = T.nHeavy ? c->keyMode : 0u;
+}
 
 int buildInstanceTables(surf_ctx* c, const surf_gpu_instance* instances, uint32_t n, const uint32_t* tlasIdx,
                         const surf_bvh_node* tlasNodes, uint32_t nTlas, const surf_light* lights, uint32_t nLights, InstanceTables& T) {
@@ -1106,6 +1121,22 @@ int buildInstanceTables(surf_ctx* c, const surf_gpu_instance* instances, uint32_
     for (uint32_t v : T.tidx) if (v >= n) return fail(c, SURF_ERR_INVALID, "TLAS index out of range");
     T.tlasLeafCount = tlasNodes[0].count;        /* root leaf: wave-uniform instance loop */
     if (T.tlasLeafCount && tlasNodes[0].left_first != 0) T.tlasLeafCount = 0;   /* general path unless indices start at 0 */
+    /* ray-order membership key: the (at most 3) instances of a single-leaf
+     * TLAS with the largest BLASes (>= 64 triangles) and a usable world box */
+    if (T.tlasLeafCount) {
+        std::vector<std::pair<uint32_t, uint32_t>> big;     /* (triangles, instance) */
+        for (uint32_t i = 0; i < n; ++i) {
+            const auto it = c->blasSlots.find(instances[i].tri_offset);
+            const uint32_t tris = it == c->blasSlots.end() ? 0u : it->second;
+            if (tris >= 64 && T.tinst[i].wlo.w != 0.0f) big.push_back({tris, i});
+        }
+        std::stable_sort(big.begin(), big.end(), [](const auto& a, const auto& b) { return a.first > b.first; });
+        for (size_t h = 0; h < big.size() && h < 3; ++h) {
+            T.hvLo[h] = T.tinst[big[h].second].wlo;
+            T.hvHi[h] = T.tinst[big[h].second].whi;
+            T.nHeavy = (uint32_t)h + 1;
+        }
+    }
     T.lights.resize(nLights);
     for (uint32_t l = 0; l < nLights; ++l) {
         const surf_light& L = lights[l];
@@ -1193,8 +1224,10 @@ int surf_upload_scene(surf_ctx* c, const surf_scene_desc* d) {
     /* object-space bounds of each BLAS's triangles as the traversal sees them
      * (v0, v0 + e1, v0 + e2 of the slot records), for the world-box cull */
     c->blasBounds.clear();
+    c->blasSlots.clear();
     for (uint32_t k = 0; k < d->blas_index_count; ++k) {
         if (idxTri[k] < 0) continue;
+        ++c->blasSlots[(uint32_t)idxTri[k]];
         auto it = c->blasBounds.emplace((uint32_t)idxTri[k], std::array<double, 6>{HUGE_VAL, HUGE_VAL, HUGE_VAL, -HUGE_VAL, -HUGE_VAL, -HUGE_VAL}).first;
         const float4 a = tris[3 * (size_t)k], e1 = tris[3 * (size_t)k + 1], e2 = tris[3 * (size_t)k + 2];
         const double v[3][3] = {{a.x, a.y, a.z}, {(double)a.x + e1.x, (double)a.y + e1.y, (double)a.z + e1.z},
@@ -1306,6 +1339,7 @@ int surf_upload_scene(surf_ctx* c, const surf_scene_desc* d) {
     for (const float4& q : nodes)
         if (!(std::fabs(q.x) <= FLT_MAX && std::fabs(q.y) <= FLT_MAX && std::fabs(q.z) <= FLT_MAX)) { S.finiteBoxes = 0u; break; }
     S.tlasLeafCount = IT.tlasLeafCount;
+    setKeys(c, S, IT);
     const surf_background& bg = *d->background;
     S.bgType = bg.type;
     S.bgColor[0] = bg.color.x; S.bgColor[1] = bg.color.y; S.bgColor[2] = bg.color.z;
@@ -1358,6 +1392,7 @@ int surf_update_instances(surf_ctx* c, const surf_gpu_instance* instances, uint3
     SURF_CHECK(c, put(c->S.tlasIdx, IT.tidx.data(), IT.tidx.size() * sizeof(uint32_t)));
     if (nLights) SURF_CHECK(c, put(c->S.lights, IT.lights.data(), IT.lights.size() * sizeof(uint2)));
     c->S.tlasLeafCount = IT.tlasLeafCount;
+    setKeys(c, c->S, IT);
     c->coopEligible = c->ldsTables && c->S.tlasLeafCount > 0 && c->S.tlasLeafCount <= 64;
     c->stackDepth = std::max(c->stackDepth, depth);
     destroyGraph(c);                  /* kernel arguments carry the scene descriptor */
