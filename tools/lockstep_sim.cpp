@@ -17,9 +17,16 @@ int main(int argc, char** argv) {
     Scene& S = *h->s;
     FILE* f = fopen(argv[1], "rb"); uint32_t n = 0;
     if (!f || fread(&n, 4, 1, f) != 1) return 1;
-    std::vector<float> od(6 * (size_t)n);
-    if (fread(od.data(), 4, od.size(), f) != od.size()) return 1;
+    const bool ANY = getenv("LOCKSTEP_ANY") != nullptr;     /* shadow rays: 7 floats (o, d, tmax), any-hit */
+    const int RS = ANY ? 7 : 6;
+    std::vector<float> raw((size_t)RS * n);
+    if (fread(raw.data(), 4, raw.size(), f) != raw.size()) return 1;
     fclose(f);
+    std::vector<float> od(6 * (size_t)n), tmx(n, kFarAway);
+    for (uint32_t i = 0; i < n; ++i) {
+        for (int q = 0; q < 6; ++q) od[6 * i + q] = raw[(size_t)RS * i + q];
+        if (ANY) tmx[i] = raw[(size_t)RS * i + 6];
+    }
     if (argc > 2 && std::string(argv[2]) == "mask") {
         // membership of every ray: bit k = instance k's world box is hit within [0, inf)
         const Bvh& T = S.tlas; const Node& root = T.nodes[0];
@@ -39,7 +46,8 @@ int main(int argc, char** argv) {
     std::map<int,double> hist;
     for (uint32_t g = 0; g + 64 <= n; g += 64) {
         V3 o[64], d[64]; float depth[64];
-        for (int l = 0; l < 64; ++l) { o[l] = mk(od[6*(g+l)], od[6*(g+l)+1], od[6*(g+l)+2]); d[l] = mk(od[6*(g+l)+3], od[6*(g+l)+4], od[6*(g+l)+5]); depth[l] = kFarAway; }
+        bool occ[64];
+        for (int l = 0; l < 64; ++l) { o[l] = mk(od[6*(g+l)], od[6*(g+l)+1], od[6*(g+l)+2]); d[l] = mk(od[6*(g+l)+3], od[6*(g+l)+4], od[6*(g+l)+5]); depth[l] = tmx[g + l]; occ[l] = false; }
         const Bvh& T = S.tlas;
         const Node& root = T.nodes[0];
         for (uint32_t k = 0; k < root.cnt; ++k) {
@@ -48,16 +56,22 @@ int main(int argc, char** argv) {
             V3 oo[64], dd[64]; uint32_t node[64]; std::vector<uint32_t> st[64]; bool act[64];
             for (int l = 0; l < 64; ++l) {
                 act[l] = false;
-                if (slab(in.bounds, o[l], d[l], depth[l]) == kFarAway) continue;
+                if (occ[l] || slab(in.bounds, o[l], d[l], depth[l]) == kFarAway) continue;
                 V4 tp = mul(in.Minv, v4(o[l], 1.0f)), td = mul(in.Minv, v4(d[l], 0.0f));
                 oo[l] = xyz(tp) / tp.w; dd[l] = xyz(td);
                 const Node& r = b.nodes[0];
                 if (r.cnt) { // root leaf: uniform scalar path on GPU; test here
-                    for (uint32_t i = 0; i < r.cnt; ++i) { float u, v; hitTri(in.blas->mesh->tris[b.idx[r.lf + i]], oo[l], dd[l], depth[l], u, v); }
+                    for (uint32_t i = 0; i < r.cnt; ++i) { float u, v; if (hitTri(in.blas->mesh->tris[b.idx[r.lf + i]], oo[l], dd[l], depth[l], u, v) && ANY) { occ[l] = true; break; } }
                     continue;
                 }
                 uint32_t cn = r.lf, cf = r.lf + 1;
                 float dn = slab(b.nodes[cn].box, oo[l], dd[l], depth[l]), df = slab(b.nodes[cf].box, oo[l], dd[l], depth[l]);
+                if (ANY) {
+                    if (dn == kFarAway && df == kFarAway) continue;
+                    node[l] = dn != kFarAway ? cn : cf; st[l].clear(); if (dn != kFarAway && df != kFarAway) st[l].push_back(cf);
+                    act[l] = true;
+                    continue;
+                }
                 if (dn > df) { std::swap(dn, df); std::swap(cn, cf); }
                 if (dn == kFarAway) continue;
                 node[l] = cn; st[l].clear(); if (df != kFarAway) st[l].push_back(cf);
@@ -74,13 +88,20 @@ int main(int argc, char** argv) {
                     bool pop = false;
                     if (nd.cnt) {
                         anyLeaf = true;
-                        for (uint32_t i = 0; i < nd.cnt; ++i) { ts.insert(nd.lf + i); triLoads++; float u, v; hitTri(in.blas->mesh->tris[b.idx[nd.lf + i]], oo[l], dd[l], depth[l], u, v); }
+                        bool h = false;
+                        for (uint32_t i = 0; i < nd.cnt; ++i) { ts.insert(nd.lf + i); triLoads++; float u, v; if (hitTri(in.blas->mesh->tris[b.idx[nd.lf + i]], oo[l], dd[l], depth[l], u, v) && ANY) { h = true; break; } }
+                        if (h) { occ[l] = true; act[l] = false; continue; }
                         pop = true;
                     } else {
                         uint32_t cn = nd.lf, cf = nd.lf + 1;
                         float dn = slab(b.nodes[cn].box, oo[l], dd[l], depth[l]), df = slab(b.nodes[cf].box, oo[l], dd[l], depth[l]);
-                        if (dn > df) { std::swap(dn, df); std::swap(cn, cf); }
-                        if (dn == kFarAway) pop = true; else { node[l] = cn; if (df != kFarAway) st[l].push_back(cf); }
+                        if (ANY) {
+                            if (dn == kFarAway && df == kFarAway) pop = true;
+                            else { node[l] = dn != kFarAway ? cn : cf; if (dn != kFarAway && df != kFarAway) st[l].push_back(cf); }
+                        } else {
+                            if (dn > df) { std::swap(dn, df); std::swap(cn, cf); }
+                            if (dn == kFarAway) pop = true; else { node[l] = cn; if (df != kFarAway) st[l].push_back(cf); }
+                        }
                     }
                     if (pop) { if (st[l].empty()) act[l] = false; else { node[l] = st[l].back(); st[l].pop_back(); } }
                 }
