@@ -136,6 +136,14 @@ struct surf_ctx {
     /* ray order (k_bincount / k_binscan / k_binscatter each phase) */
     uint32_t* order = nullptr;
     uint32_t* binHist = nullptr;
+    /* connect overlapped with the next phase's regen / pool sort / extend
+     * (SURF_OVERLAP=0: one stream): its own stream in the graph capture, its
+     * own shadow order and histograms */
+    bool overlap = true;
+    hipStream_t side = nullptr;
+    hipEvent_t capEv[2 * kPhasesPerGraph] = {};
+    uint32_t* orderQ = nullptr;
+    uint32_t* binHistQ = nullptr;
     uint32_t tailLanes = 0;
     uint32_t segMaxBase = 0;       /* longest path of finished streams */
     uint64_t tailFirstRays = 0;    /* first extension rays of drained paths: counted by regen, traced by the tail */
@@ -308,6 +316,8 @@ int allocWavefront(surf_ctx* c) {
     }
     if ((rc = devAlloc(c, c->wfAllocs, &c->order, cap))) return rc;
     if ((rc = devAlloc(c, c->wfAllocs, &c->binHist, (size_t)kBins * kSortBlocks))) return rc;
+    if ((rc = devAlloc(c, c->wfAllocs, &c->orderQ, cap))) return rc;
+    if ((rc = devAlloc(c, c->wfAllocs, &c->binHistQ, (size_t)kBins * kSortBlocks))) return rc;
     /* grid: 8 workgroups of 256 per CU saturate the 256-CU chip; grid-stride beyond */
     int cus = 256;
     hipDeviceProp_t prop;
@@ -391,58 +401,71 @@ StreamGeom geom(const surf_ctx* c) { return StreamGeom{c->dRows, c->width, c->np
 
 /* Counting sort of the pool (which 0) or shadow queue (which 1) of phase par
  * by its 4-bit key into c->order. */
-void launchSort(surf_ctx* c, const uint8_t* key, int par, int which) {
-    hipLaunchKernelGGL(k_bincount, dim3(kSortBlocks), dim3(kSortThreads), 0, c->stream, key, (const Counters*)c->ctr, par, which,
-                       c->binHist);
+void launchSort(surf_ctx* c, const uint8_t* key, int par, int which, hipStream_t st, uint32_t* hist, uint32_t* out) {
+    hipLaunchKernelGGL(k_bincount, dim3(kSortBlocks), dim3(kSortThreads), 0, st, key, (const Counters*)c->ctr, par, which, hist);
 #if !SURF_SORT_FUSED_SCAN
-    hipLaunchKernelGGL(k_binscan, dim3(1), dim3(1024), 0, c->stream, c->binHist, kBins * kSortBlocks);
+    hipLaunchKernelGGL(k_binscan, dim3(1), dim3(1024), 0, st, hist, kBins * kSortBlocks);
 #endif
-    hipLaunchKernelGGL(k_binscatter, dim3(kSortBlocks), dim3(kSortThreads), 0, c->stream, key, (const Counters*)c->ctr, par, which,
-                       (const uint32_t*)c->binHist, c->order);
+    hipLaunchKernelGGL(k_binscatter, dim3(kSortBlocks), dim3(kSortThreads), 0, st, key, (const Counters*)c->ctr, par, which,
+                       (const uint32_t*)hist, out);
 }
 
 /* One wavefront phase (ph = 0..kPhasesPerGraph-1): sort -> extend -> shade
  * -> sort -> connect -> regen.  With ev != null, ev[0..5] are recorded before
  * the pool sort, k_extend, k_shade, the shadow sort, k_connect and k_regen
- * (the phase ends at the next phase's ev[0]). */
+ * (the phase ends at the next phase's ev[0]); everything on one stream.
+ * Overlapped (graph capture, c->overlap): the shadow sort and k_connect of
+ * phase ph run on the side stream, beside k_regen and the next phase's pool
+ * sort and k_extend, which do not touch what they use (the shadow queue, its
+ * order and histograms, the radiance of paths still being shaded); the next
+ * k_shade waits for them: it reuses the shadow queue, and a path's NEE
+ * contribution of bounce i must be added before what bounce i+1 adds. */
 void launchPhase(surf_ctx* c, int ph, hipEvent_t* ev) {
     const int par = ph & 1;
     const uint32_t sw = stackWords(c, kBlock);
-    if (ev) (void)hipEventRecord(ev[0], c->stream);
+    const bool ovl = !ev && c->overlap;
+    hipStream_t s0 = c->stream, s1 = ovl ? c->side : c->stream;
+    if (ev) (void)hipEventRecord(ev[0], s0);
     const uint32_t* order = nullptr;
     if (c->sortRays && c->sortPool) {
-        launchSort(c, c->pool[par].key, par, 0);
+        launchSort(c, c->pool[par].key, par, 0, s0, c->binHist, c->order);
         order = c->order;
     }
-    if (ev) (void)hipEventRecord(ev[1], c->stream);
+    if (ev) (void)hipEventRecord(ev[1], s0);
     const Pool cur = c->pool[par];                 /* the pool k_extend / k_shade read */
     /* LW: the two-level records in the lane traversal (HBM-resident BVHs, S.laneW) */
     auto extendK = c->S.laneW ? (c->ldsTables ? k_extend<true, true> : k_extend<false, true>)
                               : (c->ldsTables ? k_extend<true, false> : k_extend<false, false>);
-    hipLaunchKernelGGL(extendK, dim3(c->gridExtend), dim3(c->extBlock), traversalLds(c, c->extBlock), c->stream, c->S,
+    hipLaunchKernelGGL(extendK, dim3(c->gridExtend), dim3(c->extBlock), traversalLds(c, c->extBlock), s0, c->S,
                        cur, c->hitTUV, c->hitInst, (const Counters*)c->ctr, par, stackWords(c, c->extBlock), order);
-    if (ev) (void)hipEventRecord(ev[2], c->stream);
+    if (ev) (void)hipEventRecord(ev[2], s0);
+    if (ovl && ph > 0) (void)hipStreamWaitEvent(s0, c->capEv[2 * (ph - 1) + 1], 0);   /* the previous phase's connect */
     if (c->ldsTables)
-        hipLaunchKernelGGL(k_shade<true>, dim3(c->gridWork), dim3(kBlock), 0, c->stream, c->S, cur, c->pool[par ^ 1],
+        hipLaunchKernelGGL(k_shade<true>, dim3(c->gridWork), dim3(kBlock), 0, s0, c->S, cur, c->pool[par ^ 1],
                            c->hitTUV, (const uint32_t*)c->hitInst, c->Q, c->rad, c->frameDone, c->npx, c->window, c->ctr, par, order);
     else
-        hipLaunchKernelGGL(k_shade<false>, dim3(c->gridWork), dim3(kBlock), 0, c->stream, c->S, cur, c->pool[par ^ 1],
+        hipLaunchKernelGGL(k_shade<false>, dim3(c->gridWork), dim3(kBlock), 0, s0, c->S, cur, c->pool[par ^ 1],
                            c->hitTUV, (const uint32_t*)c->hitInst, c->Q, c->rad, c->frameDone, c->npx, c->window, c->ctr, par, order);
-    if (ev) (void)hipEventRecord(ev[3], c->stream);
-    /* shadow rays toward the same light together (the pool order no longer needed: reuse it) */
+    if (ev) (void)hipEventRecord(ev[3], s0);
+    if (ovl) {
+        (void)hipEventRecord(c->capEv[2 * ph], s0);
+        (void)hipStreamWaitEvent(s1, c->capEv[2 * ph], 0);
+    }
+    /* shadow rays toward the same light together */
     const uint32_t* qorder = nullptr;
     if (c->sortRays && c->sortShadow) {
-        launchSort(c, c->Q.key, par, 1);
-        qorder = c->order;
+        launchSort(c, c->Q.key, par, 1, s1, ovl ? c->binHistQ : c->binHist, ovl ? c->orderQ : c->order);
+        qorder = ovl ? c->orderQ : c->order;
     }
-    if (ev) (void)hipEventRecord(ev[4], c->stream);
+    if (ev) (void)hipEventRecord(ev[4], s0);
     const bool ldsC = c->ldsTables && !c->connectGlobal;   /* else global tables: LDS holds only the traversal stack */
     auto connectK = c->S.laneW ? (ldsC ? k_connect<true, true> : k_connect<false, true>)
                                : (ldsC ? k_connect<true, false> : k_connect<false, false>);
     hipLaunchKernelGGL(connectK, dim3(c->gridConnect), dim3(kBlock), ldsC ? traversalLds(c, kBlock) : (size_t)sw * sizeof(uint32_t),
-                       c->stream, c->S, c->Q, c->rad, c->ctr, par, sw, qorder);
-    if (ev) (void)hipEventRecord(ev[5], c->stream);
-    hipLaunchKernelGGL(k_regen, dim3(c->gridRegen), dim3(kBlock), 0, c->stream, c->cam, c->pool[par ^ 1], c->rad, c->ctr, par,
+                       s1, c->S, c->Q, c->rad, c->ctr, par, sw, qorder);
+    if (ovl) (void)hipEventRecord(c->capEv[2 * ph + 1], s1);
+    if (ev) (void)hipEventRecord(ev[5], s0);
+    hipLaunchKernelGGL(k_regen, dim3(c->gridRegen), dim3(kBlock), 0, s0, c->cam, c->pool[par ^ 1], c->rad, c->ctr, par,
                        c->capacity, geom(c));
 }
 
@@ -450,7 +473,9 @@ int buildGraph(surf_ctx* c) {
     if (c->graphExec) return SURF_OK;
     for (int shortG = 0; shortG < 2; ++shortG) {
         SURF_CHECK(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-        for (int ph = 0; ph < (shortG ? kPhasesShort : kPhasesPerGraph); ++ph) launchPhase(c, ph, nullptr);
+        const int nph = shortG ? kPhasesShort : kPhasesPerGraph;
+        for (int ph = 0; ph < nph; ++ph) launchPhase(c, ph, nullptr);
+        if (c->overlap) (void)hipStreamWaitEvent(c->stream, c->capEv[2 * (nph - 1) + 1], 0);   /* join the last connect */
         hipGraph_t& g = shortG ? c->graphShort : c->graph;
         hipError_t e = hipStreamEndCapture(c->stream, &g);
         if (e != hipSuccess) return fail(c, SURF_ERR_HIP, std::string("graph capture: ") + hipGetErrorString(e));
@@ -840,6 +865,7 @@ int createCtx(int dev, uint32_t w, uint32_t h, std::vector<uint32_t> rows, surf_
     }
     if (const char* e = std::getenv("SURF_CONNECT_GLOBAL")) c->connectGlobal = e[0] != '0';
     if (const char* e = std::getenv("SURF_KEY")) c->keyMode = e[0] == '0' ? 0u : 1u;
+    if (const char* e = std::getenv("SURF_OVERLAP")) c->overlap = e[0] != '0';
     if (const char* e = std::getenv("SURF_TAIL_ROWS")) c->tailRows = e[0] == '1';
     if (const char* e = std::getenv("SURF_TAIL_PAIR")) c->tailPair = e[0] != '0';
     c->width = w;
@@ -847,10 +873,16 @@ int createCtx(int dev, uint32_t w, uint32_t h, std::vector<uint32_t> rows, surf_
     c->rows = std::move(rows);
     c->npx = (uint32_t)(w * c->rows.size());
     if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return fail(nullptr, SURF_ERR_HIP, "stream/event creation failed");
     }
+    for (auto& e : c->capEv)
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+            delete c;
+            return fail(nullptr, SURF_ERR_HIP, "event creation failed");
+        }
     if (hipMalloc(&c->acc, (size_t)c->npx * sizeof(float4)) != hipSuccess ||
         hipMalloc(&c->dRows, c->rows.size() * sizeof(uint32_t)) != hipSuccess) {
         surf_destroy(c);
@@ -905,6 +937,9 @@ void surf_destroy(surf_ctx* c) {
     if (c->dRows) (void)hipFree(c->dRows);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
+    for (auto& e : c->capEv)
+        if (e) (void)hipEventDestroy(e);
+    if (c->side) (void)hipStreamDestroy(c->side);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }

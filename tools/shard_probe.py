@@ -5,7 +5,9 @@ i.e. what an N = G run takes per GPU before the gather.  Diagnostics only.
     python tools/shard_probe.py [G,G,...]
     env: W H (frame size, default 1280x720), F (frames per render, default 256),
          STEPS (timed renders per shard, default 1), ROWBLOCK (rows per
-         interleave block, default 1), TAIL / COOP (drain policy knobs)
+         interleave block, default 1), TAIL / COOP (drain policy knobs),
+         POOL (paths in flight per shard, default: the library's ~4 full frames),
+         ONLY (comma list: render only these shards of each G, e.g. for a profile)
 
 Each shard: one untimed 16-frame warm-up render, then STEPS complete renders
 of F frames (frames 16.., each drained), timed together."""
@@ -25,8 +27,10 @@ scene = surf_amd.Scene.indoor()
 base = None
 for G in gs:
     times, maxseg = [], []
-    for k in range(G):
-        r = surf_amd.Renderer(scene, W, H, shard=surf_amd.ShardSpec(k, G, ROWBLOCK if G > 1 else 0))
+    only = [int(x) for x in os.environ["ONLY"].split(",")] if os.environ.get("ONLY") else range(G)
+    for k in only:
+        r = surf_amd.Renderer(scene, W, H, shard=surf_amd.ShardSpec(k, G, ROWBLOCK if G > 1 else 0),
+                              pool_capacity=int(os.environ["POOL"]) if os.environ.get("POOL") else None)
         if os.environ.get("TAIL"):
             r.set_tail_policy(*[int(x) for x in os.environ["TAIL"].split(",")])
         if os.environ.get("COOP"):
@@ -41,7 +45,7 @@ for G in gs:
         st = r.stats()
         maxseg.append(st.get("max_segments"))
         r.close()
-        print(json.dumps({"G": G, "shard": k, "ms": round(times[-1] * 1e3, 1), "tail_paths": st["tail_paths"],
+        print(json.dumps({"G": G, "shard": k, "ms": round(times[-1] * 1e3, 1), "tail_paths": st["tail_paths"], "tail_ms": st.get("ms_tail"),
                           "max_seg": st.get("max_segments"), "iters": st["iterations"]}), flush=True)
     t = max(times)
     base = base or t
