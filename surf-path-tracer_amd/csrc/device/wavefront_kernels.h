@@ -135,7 +135,10 @@ struct Counters {
     uint32_t survN;                  /* k_tail survivors appended (may exceed survCap) */
     uint32_t survCap;
     uint32_t rowNext;                /* k_tail_rows work queue: next path to hand out */
-    uint32_t _pad2[2];
+    /* issue order of the stream's first permFrames frames: every frame's
+     * samples of the permA pixels listed first in StreamGeom::perm, then each
+     * frame's other pixels frame by frame (0: frame-major throughout) */
+    uint32_t permFrames, permA;
     unsigned long long issued[2];    /* stream samples issued, per parity */
     unsigned long long limit;        /* host-written issue limit (frame window) */
     unsigned long long baseFrame;    /* absolute frame index of stream frame 0 */
@@ -167,6 +170,7 @@ __device__ __forceinline__ void noteCapped(Counters* C, uint32_t sid) {
 struct StreamGeom {
     const uint32_t* rows;            /* shard rows */
     uint32_t width, npx, window;
+    const uint32_t* perm;            /* local pixels, class A (Counters::permA of them) first */
 };
 
 SURF_HD V3 ld3(const float* p) { return mk3(p[0], p[1], p[2]); }
@@ -2267,11 +2271,22 @@ __global__ __launch_bounds__(kBlock) void k_regen(DevCamera cam, Pool nxt, float
     /* frame / pixel of the first new sample, then step without 64-bit divisions */
     const unsigned long long f0 = iss / G.npx;
     const uint32_t lp0 = (uint32_t)(iss - f0 * G.npx);
+    /* the permuted head of the stream (surf_hip.hip classifyPixels) */
+    const uint32_t nA = C->permA, nB = G.npx - C->permA;
+    const unsigned long long endA = (unsigned long long)nA * C->permFrames, endP = (unsigned long long)G.npx * C->permFrames;
     for (uint32_t k = gid; k < nnew; k += gridDim.x * blockDim.x) {
-        uint32_t lp = lp0 + k;
-        const uint32_t df = lp / G.npx;
-        lp -= df * G.npx;
-        const unsigned long long f = f0 + df;
+        uint32_t lp;
+        unsigned long long f;
+        if (iss + k < endP) {
+            const unsigned long long s = iss + k;
+            if (s < endA) { f = s / nA; lp = G.perm[(uint32_t)(s - f * nA)]; }
+            else { const unsigned long long j = s - endA; f = j / nB; lp = G.perm[nA + (uint32_t)(j - f * nB)]; }
+        } else {
+            lp = lp0 + k;
+            const uint32_t df = lp / G.npx;
+            lp -= df * G.npx;
+            f = f0 + df;
+        }
         const uint32_t slot = (uint32_t)(f % G.window);
         const uint32_t rowi = lp / G.width;
         const uint32_t x = lp - rowi * G.width;

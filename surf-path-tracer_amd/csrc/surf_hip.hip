@@ -87,6 +87,14 @@ struct surf_ctx {
     std::map<std::tuple<uint32_t, uint32_t, uint32_t>, std::array<float4, 4>> blasRoots;  /* (node, idx, tri offset) -> root record */
     std::map<uint32_t, std::array<double, 6>> blasBounds;   /* tri offset -> bounds of its BLAS's triangles (v0, v0+e1, v0+e2) */
     std::map<uint32_t, uint32_t> blasSlots;                  /* tri offset -> index slots (triangles) of its BLAS */
+    /* issue order: the pixels whose centre ray first hits a heavy instance
+     * (long Russian-roulette paths start there) are issued for all frames of a
+     * multi-frame stream before the rest (SURF_REORDER=0: frame-major) */
+    bool reorder = true;
+    bool permValid = false;
+    uint32_t* dPerm = nullptr;
+    uint32_t permA = 0, permFrames = 0;
+    std::vector<uint32_t> heavyInst;
     uint32_t keyMode = 1;          /* pool ray-order key (SURF_KEY): 1 heavy-instance mask x quadrant, 0 start instance x quadrant */
     /* camera */
     bool hasCamera = false;
@@ -317,6 +325,7 @@ int allocWavefront(surf_ctx* c) {
     if ((rc = devAlloc(c, c->wfAllocs, &c->order, cap))) return rc;
     if ((rc = devAlloc(c, c->wfAllocs, &c->binHist, (size_t)kBins * kSortBlocks))) return rc;
     if ((rc = devAlloc(c, c->wfAllocs, &c->orderQ, cap))) return rc;
+    if ((rc = devAlloc(c, c->wfAllocs, &c->dPerm, c->npx))) return rc;
     if ((rc = devAlloc(c, c->wfAllocs, &c->binHistQ, (size_t)kBins * kSortBlocks))) return rc;
     /* grid: 8 workgroups of 256 per CU saturate the 256-CU chip; grid-stride beyond */
     int cus = 256;
@@ -397,7 +406,7 @@ int ensureWindow(surf_ctx* c, uint64_t frames) {
     return SURF_OK;
 }
 
-StreamGeom geom(const surf_ctx* c) { return StreamGeom{c->dRows, c->width, c->npx, c->window}; }
+StreamGeom geom(const surf_ctx* c) { return StreamGeom{c->dRows, c->width, c->npx, c->window, c->dPerm}; }
 
 /* Counting sort of the pool (which 0) or shadow queue (which 1) of phase par
  * by its 4-bit key into c->order. */
@@ -484,10 +493,74 @@ int buildGraph(surf_ctx* c) {
     return SURF_OK;
 }
 
+/* Pixel classes of the issue order (cached until the camera, the scene or
+ * the instances change): class A = the local pixels whose centre camera ray
+ * first hits one of the heavy instances (setKeys).  Long Russian-roulette
+ * paths start there (C3 frame 2: 67 % of the paths longer than 100 segments
+ * from 4.3 % of the pixels, the two Suzannes); issuing those samples first
+ * gives their paths more wavefront phases before the drain takes the
+ * survivors.  Only the issue order changes: each sample is the same function
+ * of (pixel, frame) and frames are still accumulated in order. */
+int classifyPixels(surf_ctx* c) {
+    if (c->permValid) return SURF_OK;
+    const uint32_t n = c->npx;
+    std::vector<float> o(3 * (size_t)n), d(3 * (size_t)n);
+    const DevCamera& k = c->cam;
+    for (uint32_t lp = 0; lp < n; ++lp) {
+        const uint32_t x = lp % c->width, row = c->rows[lp / c->width];
+        const float u = (float)x * k.invW, v = (float)row * k.invH;
+        float dir[3], len2 = 0.0f;
+        for (int a = 0; a < 3; ++a) {
+            dir[a] = k.firstPixel[a] + u * k.uVec[a] + v * k.vVec[a] - k.pos[a];
+            len2 += dir[a] * dir[a];
+        }
+        const float inv = 1.0f / std::sqrt(len2);
+        for (int a = 0; a < 3; ++a) { o[3 * (size_t)lp + a] = k.pos[a]; d[3 * (size_t)lp + a] = dir[a] * inv; }
+    }
+    std::vector<void*> tmp;
+    float *dO, *dD; float4* dT; uint2* dI;
+    int rc;
+    if ((rc = devAlloc(c, tmp, &dO, 3 * (size_t)n)) || (rc = devAlloc(c, tmp, &dD, 3 * (size_t)n)) ||
+        (rc = devAlloc(c, tmp, &dT, n)) || (rc = devAlloc(c, tmp, &dI, n))) { freeList(tmp); return rc; }
+    std::vector<uint2> ip(n);
+    (void)hipMemcpyAsync(dO, o.data(), 12 * (size_t)n, hipMemcpyHostToDevice, c->stream);
+    (void)hipMemcpyAsync(dD, d.data(), 12 * (size_t)n, hipMemcpyHostToDevice, c->stream);
+    hipLaunchKernelGGL(c->S.laneW ? (c->ldsTables ? k_trace_closest<true, true> : k_trace_closest<false, true>)
+                                  : (c->ldsTables ? k_trace_closest<true, false> : k_trace_closest<false, false>),
+                       dim3((n + kBlock - 1) / kBlock), dim3(kBlock), traversalLds(c, kBlock), c->stream,
+                       c->S, (const float*)dO, (const float*)dD, n, dT, dI, stackWords(c, kBlock));
+    (void)hipMemcpyAsync(ip.data(), dI, sizeof(uint2) * (size_t)n, hipMemcpyDeviceToHost, c->stream);
+    const hipError_t e = hipStreamSynchronize(c->stream);
+    freeList(tmp);
+    if (e != hipSuccess) return fail(c, SURF_ERR_HIP, std::string("pixel classification: ") + hipGetErrorString(e));
+    std::vector<uint32_t> perm;
+    perm.reserve(n);
+    for (int cls = 0; cls < 2; ++cls)
+        for (uint32_t lp = 0; lp < n; ++lp) {
+            const bool heavy = std::find(c->heavyInst.begin(), c->heavyInst.end(), ip[lp].x) != c->heavyInst.end();
+            if (heavy == (cls == 0)) perm.push_back(lp);
+        }
+    c->permA = (uint32_t)std::count_if(ip.begin(), ip.end(), [&](const uint2& h) {
+        return std::find(c->heavyInst.begin(), c->heavyInst.end(), h.x) != c->heavyInst.end();
+    });
+    SURF_CHECK(c, hipMemcpy(c->dPerm, perm.data(), sizeof(uint32_t) * (size_t)n, hipMemcpyHostToDevice));
+    c->permValid = true;
+    return SURF_OK;
+}
+
 /* ---- sample stream ------------------------------------------------------ */
-int startStream(surf_ctx* c, uint64_t baseFrame, uint32_t maxSeg) {
+int startStream(surf_ctx* c, uint64_t baseFrame, uint32_t maxSeg, uint32_t frames) {
     Counters h{};
     for (uint32_t& v : h.capped) v = kUnset;
+    /* a multi-frame request that fits the window: its pixels in class order */
+    c->permFrames = 0;
+    if (c->reorder && frames >= 2 && frames <= c->window && c->heavyInst.size()) {
+        int rc = classifyPixels(c);
+        if (rc) return rc;
+        if (c->permA > 0 && c->permA < c->npx) c->permFrames = frames;
+    }
+    h.permFrames = c->permFrames;
+    h.permA = c->permFrames ? c->permA : 0u;
     h.maxSeg = maxSeg;
     h.zeroCutoff = c->zeroCutoff ? 1u : 0u;
     h.baseFrame = baseFrame;
@@ -515,6 +588,15 @@ int pushLimit(surf_ctx* c) {
     SURF_CHECK(c, hipMemcpyAsync(&c->ctr->limit, &c->hctr->limit, sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
     c->pushedLimit = lim;
     return SURF_OK;
+}
+
+/* Frames whose every sample is issued after `iss` samples (k_regen's order:
+ * the permuted head of permFrames frames, then frame-major). */
+uint64_t fullyIssuedFrames(const surf_ctx* c, uint64_t iss) {
+    const uint64_t P = c->permFrames;
+    if (!P || iss >= (uint64_t)c->npx * P) return iss / c->npx;
+    const uint64_t endA = (uint64_t)c->permA * P;
+    return iss <= endA ? 0 : (iss - endA) / (c->npx - c->permA);
 }
 
 /* Finished paths of a frame slot: sum over the completion stripes. */
@@ -553,7 +635,7 @@ int syncAndAccumulate(surf_ctx* c) {
      * slot is reused only after its frame is accumulated, so frames beyond the
      * issued range must not be tested (their slot may still count an older frame) */
     uint64_t f = c->accFrames;
-    const uint64_t issuedFrames = c->hctr->issued[0] / c->npx;
+    const uint64_t issuedFrames = fullyIssuedFrames(c, c->hctr->issued[0]);
     while (f < c->targetFrames && f < issuedFrames && framePaths(c, f % c->window) == c->npx) ++f;
     if (f == c->accFrames) return SURF_OK;
     const uint32_t count = (uint32_t)(f - c->accFrames);
@@ -866,6 +948,7 @@ int createCtx(int dev, uint32_t w, uint32_t h, std::vector<uint32_t> rows, surf_
     if (const char* e = std::getenv("SURF_CONNECT_GLOBAL")) c->connectGlobal = e[0] != '0';
     if (const char* e = std::getenv("SURF_KEY")) c->keyMode = e[0] == '0' ? 0u : 1u;
     if (const char* e = std::getenv("SURF_OVERLAP")) c->overlap = e[0] != '0';
+    if (const char* e = std::getenv("SURF_REORDER")) c->reorder = e[0] != '0';
     if (const char* e = std::getenv("SURF_TAIL_ROWS")) c->tailRows = e[0] == '1';
     if (const char* e = std::getenv("SURF_TAIL_PAIR")) c->tailPair = e[0] != '0';
     c->width = w;
@@ -1058,10 +1141,13 @@ struct InstanceTables {
     uint32_t tlasDepth = 0, tlasLeafCount = 0;
     uint32_t nHeavy = 0;
     float4 hvLo[3], hvHi[3];
+    uint32_t hvInst[3] = {0, 0, 0};
 };
 
 /* The heavy-instance boxes of the ray-order keys (kernel arguments). */
-void setKeys(const surf_ctx* c, DevScene& S, const InstanceTables& T) {
+void setKeys(surf_ctx* c, DevScene& S, const InstanceTables& T) {
+    c->heavyInst.assign(T.hvInst, T.hvInst + T.nHeavy);
+    c->permValid = false;                 /* the pixel classes follow the instances */
     S.nHeavy = T.nHeavy;
     for (uint32_t h = 0; h < 3; ++h) {
         S.hvLo[h] = h < T.nHeavy ? T.hvLo[h] : make_float4(0, 0, 0, 0);
@@ -1169,6 +1255,7 @@ int buildInstanceTables(surf_ctx* c, const surf_gpu_instance* instances, uint32_
         for (size_t h = 0; h < big.size() && h < 3; ++h) {
             T.hvLo[h] = T.tinst[big[h].second].wlo;
             T.hvHi[h] = T.tinst[big[h].second].whi;
+            T.hvInst[h] = big[h].second;
             T.nHeavy = (uint32_t)h + 1;
         }
     }
@@ -1458,6 +1545,7 @@ int surf_set_camera(surf_ctx* c, const surf_camera_ubo* u) {
     k.diskU[0] = du.x; k.diskU[1] = du.y; k.diskU[2] = du.z;
     k.diskV[0] = dv.x; k.diskV[1] = dv.y; k.diskV[2] = dv.z;
     c->cam = k;
+    c->permValid = false;
     c->camUbo = *u;
     c->hasCamera = true;
     destroyGraph(c);     /* camera is a kernel argument of the captured graph */
@@ -1478,7 +1566,7 @@ int surf_render(surf_ctx* c, uint32_t frames, uint32_t firstFrame, uint32_t maxS
         if ((rc = endStream(c))) return rc;
     if (!c->streamActive) {
         if ((rc = ensureWindow(c, frames))) return rc;
-        if ((rc = startStream(c, firstFrame, maxSeg))) return rc;
+        if ((rc = startStream(c, firstFrame, maxSeg, frames))) return rc;
     }
     if (!c->profiling && (rc = buildGraph(c))) return rc;         /* (re)captured if the ring moved */
     SURF_CHECK(c, hipEventRecord(c->ev0, c->stream));

@@ -231,6 +231,32 @@ def test_ray_order_and_launch_shapes_bitexact(oracle_scene, product_scene, sort,
     r.close()
 
 
+@pytest.mark.parametrize("reorder,key,overlap", [("1", "1", "1"), ("0", "1", "1"), ("1", "0", "1"), ("1", "1", "0")],
+                         ids=["default", "frame-major-issue", "start-instance-key", "connect-serialized"])
+def test_issue_order_keys_overlap_bitexact(oracle_scene, product_scene, reorder, key, overlap, monkeypatch):
+    """Scheduling only: the class-ordered issue of a multi-frame stream (pixels
+    whose centre ray first hits a heavy instance, all frames first;
+    SURF_REORDER), the pool's ray-order key (heavy-BLAS mask or start
+    instance; SURF_KEY) and k_connect on its own graph stream (SURF_OVERLAP)
+    change no sample: radiance and event counts equal the oracle's."""
+    W, H, F = 96, 64, 6
+    monkeypatch.setenv("SURF_REORDER", reorder)
+    monkeypatch.setenv("SURF_KEY", key)
+    monkeypatch.setenv("SURF_OVERLAP", overlap)
+    r = surf_amd.Renderer(product_scene, W, H, pool_capacity=4096)
+    r.render(F, 0, 0)
+    g = r.accumulator()
+    st = r.stats()
+    oracle.set_zero_cutoff(True)
+    try:
+        c2, cnt, _ = oracle_scene.render(W, H, F)
+    finally:
+        oracle.set_zero_cutoff(False)
+    _assert_bitexact(g, c2, f"reorder={reorder} key={key} overlap={overlap}")
+    _assert_counts(st, cnt)
+    r.close()
+
+
 def test_render_c1_256x256x16_bitexact(oracle_scene, product_scene):
     g, c, stats, cnt, _ = _render_both(oracle_scene, product_scene, 256, 256, 16)
     _assert_bitexact(g, c, "C1 256x256x16")
