@@ -243,7 +243,13 @@ int surf_set_camera(surf_ctx* ctx, const surf_camera_ubo* camera);
  * (multi-sample frames are expressed as consecutive frames).  Returns once every
  * sample is issued: consecutive calls form one sample stream, so the last long
  * paths of a call overlap the next call; any read (accumulator, stats,
- * finalize, synchronize) drains the stream first. */
+ * finalize, synchronize) drains the stream first.  Scheduling only, identical
+ * results (environment at surf_create, for A/B runs): a multi-frame call that
+ * starts a stream issues every frame's samples of the pixels whose centre
+ * camera ray first hits one of the largest BLASes first (SURF_REORDER=0:
+ * frame-major); continuations are traced in the order of the large BLASes
+ * they can reach (SURF_KEY=0: by start instance); each phase's shadow rays are
+ * traced beside the next phase's extension (SURF_OVERLAP=0: serialized). */
 int surf_render(surf_ctx* ctx, uint32_t frames, uint32_t first_frame_index,
                 uint32_t max_segments, uint32_t samples_per_frame);
 int surf_clear_accumulator(surf_ctx* ctx);
