@@ -34,6 +34,17 @@ def counter(path, kernel, name):
     return list(per.values())
 
 
+def counter_by_kernel(path, name):
+    """{kernel short name: per-dispatch values} of one counter."""
+    per = {}
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] == name:
+            k = short(r["Kernel_Name"])
+            per.setdefault(k, {})
+            per[k][r["Dispatch_Id"]] = per[k].get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
+    return {k: list(v.values()) for k, v in per.items()}
+
+
 def main():
     d, out = sys.argv[1], sys.argv[2]
     cmd = sys.argv[3] if len(sys.argv) > 3 else "python3 bench.py --steps 16 --warmup 1 --no-cpu"
@@ -42,6 +53,14 @@ def main():
     fetch = counter(f"{d}/fetch/run_counter_collection.csv", "k_extend", "FETCH_SIZE")
     write = counter(f"{d}/write/run_counter_collection.csv", "k_extend", "WRITE_SIZE")
     bench = json.loads(open(f"{d}/bench_traced.json").read().strip().splitlines()[-1])
+    fk = counter_by_kernel(f"{d}/fetch/run_counter_collection.csv", "FETCH_SIZE")
+    wk = counter_by_kernel(f"{d}/write/run_counter_collection.csv", "WRITE_SIZE")
+    by_kernel = {}
+    for k in sorted(set(fk) | set(wk)):
+        f, w = fk.get(k, []), wk.get(k, [])
+        by_kernel[k] = {"launches": len(f), "fetch_kib_avg_raw": statistics.mean(f) if f else None,
+                        "write_kib_avg": statistics.mean(w) if w else None,
+                        "hbm_bytes_per_launch_corrected": (2 * statistics.mean(f) + statistics.mean(w)) * 1024 if f and w else None}
     res = {
         "command": cmd + "  (under rocprofv3 --kernel-trace --stats; PMC passes: the same command, one counter per pass)",
         "workload": workload,
@@ -54,6 +73,7 @@ def main():
             "hbm_bytes_per_launch_corrected": (2 * statistics.mean(fetch) + statistics.mean(write)) * 1024 if fetch and write else None,
             "correction": "read side x2 (gfx950 FETCH_SIZE halves 16-B/lane reads), KiB x1024",
         },
+        "pmc_by_kernel": by_kernel,
     }
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
