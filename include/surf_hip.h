@@ -158,8 +158,8 @@ const char* surf_last_error(const surf_ctx* ctx);   /* ctx may be NULL: last glo
 /* Rows of this shard in shard order (row_count from surf_shard_rows(ctx, NULL, &n)). */
 int surf_shard_rows(const surf_ctx* ctx, uint32_t* rows, uint32_t* row_count);
 
-/* Paths in flight (default: sized from the shard, >= 1M when possible). Must be
- * called before the first render. */
+/* Paths in flight (default: 5 full frames, W * H * 5, at most 16 M, whatever
+ * the shard). Must be called before the first render. */
 int surf_set_pool_capacity(surf_ctx* ctx, uint32_t paths);
 /* Frame window: frames whose samples may be in flight at once.  Default: the
  * frames the stream being started requests (one render call's frame count),

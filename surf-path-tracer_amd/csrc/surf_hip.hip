@@ -308,12 +308,15 @@ int upload(surf_ctx* c, const std::vector<T>& host, const T** devOut) {
 int allocWavefront(surf_ctx* c) {
     if (c->allocated) return SURF_OK;
     if (c->capacity == 0) {
-        /* default: ~4 full frames of paths in flight, bounded at 4M paths.  Sized
-         * from the whole frame, not the shard: a row shard of G GPUs keeps the
-         * same pool, so its stream needs ~G times fewer wavefront phases (each
-         * phase pays launch and poll latency however few paths it holds). */
-        const uint64_t want = (uint64_t)c->width * c->height * 4;
-        c->capacity = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(want, 65536), 1u << 22);
+        /* default: 5 full frames of paths in flight, bounded at 16M paths
+         * (measured, DESIGN §4 "Pool sizing": C3 435-439 -> 470-475 Mrays/s
+         * from 4 to 5 frames, 4.5 frames no better than 4, 6 slower again).
+         * Sized from the whole frame, not the shard: a row shard of G GPUs
+         * keeps the same pool, so its stream needs ~G times fewer wavefront
+         * phases (each phase pays launch and poll latency however few paths it
+         * holds). */
+        const uint64_t want = (uint64_t)c->width * c->height * 5;
+        c->capacity = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(want, 65536), 1u << 24);
     }
     const size_t cap = c->capacity;
     int rc;
@@ -831,7 +834,15 @@ int runTail(surf_ctx* c) {
     return SURF_OK;
 }
 
-uint32_t tailThreshold(const surf_ctx* c) { return c->tailPaths ? c->tailPaths : std::max<uint32_t>(c->capacity / 16, 4096u); }
+/* Drain hand-over (automatic): a quarter frame of paths (W * H / 4, what
+ * capacity / 16 was at the round-2 pool of 4 frames), at most capacity / 16:
+ * tied to the pool, a larger pool handed C5's deep-BVH drain 280 k paths
+ * (drain 2.2 -> 5.8 s per render). */
+uint32_t tailThreshold(const surf_ctx* c) {
+    if (c->tailPaths) return c->tailPaths;
+    const uint64_t quarter = (uint64_t)c->width * c->height / 4;
+    return (uint32_t)std::max<uint64_t>(std::min<uint64_t>(quarter, c->capacity / 16), 4096u);
+}
 
 /* Runs until every requested sample is issued (drain = false) or until every
  * requested frame is accumulated (drain = true). */
