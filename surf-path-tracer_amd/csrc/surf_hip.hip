@@ -359,10 +359,16 @@ int allocWavefront(surf_ctx* c) {
      * thread (latency hiding across many short-lived blocks), k_connect peaks
      * at 12 workgroups per CU, k_shade at 8 */
     uint64_t extPerCu = 48, conPerCu = 12;
-    if (const char* e = std::getenv("SURF_GRID_EXTEND")) extPerCu = (uint64_t)std::max(1, std::atoi(e));
+    const char* eExt = std::getenv("SURF_GRID_EXTEND");
+    if (eExt) extPerCu = (uint64_t)std::max(1, std::atoi(eExt));
     if (const char* e = std::getenv("SURF_GRID_CONNECT")) conPerCu = (uint64_t)std::max(1, std::atoi(e));
     if (c->extBlock == 128) extPerCu *= 2;                 /* the same threads per CU in half-size workgroups */
     c->gridExtend = (uint32_t)std::min<uint64_t>((cap + c->extBlock - 1) / c->extBlock, (uint64_t)cus * extPerCu);
+    /* k_extend: ~1.5 rays per thread at a full pool (grid-stride).  Measured
+     * (DESIGN §4 "Pool sizing"): the launch is fast at 1.3-1.6 rays per thread
+     * and 15-30 % slower at 1.1-1.2 or >= 1.7 (C3: 48 workgroups per CU = 1.4
+     * -> 120 ms, 56 = 1.2 -> 151 ms; C4: 1.56 -> 1094 ms, 3.1 -> 1170 ms) */
+    if (!eExt) c->gridExtend = (uint32_t)std::max<uint64_t>((uint64_t)cus * 8, (cap * 2 / 3 + c->extBlock - 1) / c->extBlock);
     c->gridConnect = (uint32_t)std::min<uint64_t>(maxBlocks, (uint64_t)cus * conPerCu);
     c->coopMax = (uint32_t)cus * 4 * SURF_TAIL_WAVES;
     c->cus = (uint32_t)cus;
