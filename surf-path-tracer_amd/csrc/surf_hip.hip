@@ -368,7 +368,7 @@ int allocWavefront(surf_ctx* c) {
      * (DESIGN §4 "Pool sizing"): the launch is fast at 1.3-1.6 rays per thread
      * and 15-30 % slower at 1.1-1.2 or >= 1.7 (C3: 48 workgroups per CU = 1.4
      * -> 120 ms, 56 = 1.2 -> 151 ms; C4: 1.56 -> 1094 ms, 3.1 -> 1170 ms) */
-    if (!eExt) c->gridExtend = (uint32_t)std::max<uint64_t>((uint64_t)cus * 8, (cap * 2 / 3 + c->extBlock - 1) / c->extBlock);
+    if (!eExt) c->gridExtend = (uint32_t)std::max<uint64_t>(c->gridExtend, (cap * 2 / 3 + c->extBlock - 1) / c->extBlock);
     c->gridConnect = (uint32_t)std::min<uint64_t>(maxBlocks, (uint64_t)cus * conPerCu);
     c->coopMax = (uint32_t)cus * 4 * SURF_TAIL_WAVES;
     c->cus = (uint32_t)cus;
