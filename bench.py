@@ -91,7 +91,7 @@ def parse():
                     help="renders re-run with per-kernel HIP events for the roofline (0 = none)")
     ap.add_argument("--tail", type=str, default="", help="tuning: drain policy 'threshold,lanes_per_wave,stage_segments'")
     ap.add_argument("--tail-coop", type=int, default=-1, help="tuning: cooperative drain when <= N paths remain")
-    ap.add_argument("--pool", type=int, default=0, help="tuning: paths in flight (0: the library default, ~4 frames)")
+    ap.add_argument("--pool", type=int, default=0, help="tuning: paths in flight (0: the library default, 5 frames)")
     return ap.parse_args()
 
 
