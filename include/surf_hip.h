@@ -157,12 +157,18 @@ void surf_destroy(surf_ctx* ctx);
 const char* surf_last_error(const surf_ctx* ctx);   /* ctx may be NULL: last global error */
 /* Rows of this shard in shard order (row_count from surf_shard_rows(ctx, NULL, &n)). */
 int surf_shard_rows(const surf_ctx* ctx, uint32_t* rows, uint32_t* row_count);
+/* The rows shard shard_index of shard_count owns under surf_create_sharded's
+ * rule, in shard order (rows may be NULL to get the count).  Host only. */
+int surf_shard_row_list(uint32_t height, uint32_t shard_index, uint32_t shard_count, uint32_t row_block, uint32_t* rows,
+                        uint32_t* row_count);
 
 /* Paths in flight (default: 5 full frames, W * H * 5, at most 16 M, whatever
  * the shard). Must be called before the first render. */
 int surf_set_pool_capacity(surf_ctx* ctx, uint32_t paths);
-/* Frame window: frames whose samples may be in flight at once.  Default: the
- * frames the stream being started requests (one render call's frame count),
+/* Frame window: passes (samples per pixel; a frame of spp samples takes spp
+ * consecutive passes) whose samples may be in flight at once -- a multiple of
+ * the stream's samples_per_frame.  Default: the passes the stream being
+ * started requests (one render call's frames x spp, rounded to a multiple of spp),
  * at least 256 (a drop-in loop extends its stream one frame per call), at most
  * 4096 and at most what min(32 GiB, a quarter of the free HBM) holds; a later
  * stream that requests more frames grows the ring (C3 at 1280x720: 256 frames
@@ -173,7 +179,11 @@ int surf_set_pool_capacity(surf_ctx* ctx, uint32_t paths);
  * frame f only once frame f - window is accumulated.  Setting it fixes it
  * (must be called before the first render). */
 int surf_set_frame_batch(surf_ctx* ctx, uint32_t frames);
-/* Throughput cutoff (default on): a path whose throughput T is below FLT_MIN
+/* Throughput cutoff (enabled 1 / 0; -1 = automatic, the default: on for
+ * streams of 1-sample frames, off for multi-sample frames, whose next sample
+ * starts from the RNG state the reference's path ends with -- an early end
+ * would change it, so there the cutoff is a deviation, not a neutral
+ * shortcut): a path whose throughput T is below FLT_MIN
  * (1.17549435e-38) in every channel -- zero or denormal -- ends early.  The
  * reference's Russian roulette ends such a path with certainty at its next
  * diffuse bounce (p = max(T) < 2^-32, the smallest positive randomF32).  The
@@ -235,12 +245,18 @@ int surf_update_instances(surf_ctx* ctx, const surf_gpu_instance* instances, uin
 int surf_set_camera(surf_ctx* ctx, const surf_camera_ubo* camera);
 
 /* ---- rendering ----
- * Renders `frames` frames of one sample per pixel each; frame k is seeded
- * initSeed(pixel + 1799 * (first_frame_index + k)) like the CPU renderer
- * (renderer.cpp:169) and accumulates (rgb, 1) per sample in frame order.
+ * Renders `frames` frames of samples_per_frame (spp) samples per pixel each,
+ * as Renderer::render does per call (renderer.cpp:160-188): frame k is seeded
+ * once per pixel with initSeed(pixel + 1799 * (first_sample_index + k * spp))
+ * (renderer.cpp:169; first_sample_index = the accumulator's totalSamples
+ * before this call, which is the frame index for spp 1), and its spp samples
+ * run in sequence, sample j + 1's jitter, lens sample and path drawing from the
+ * RNG state sample j's path left (renderer.cpp:171-181); (rgb, 1) is
+ * accumulated per sample in sample order (renderer.cpp:180).  On the device a
+ * frame's samples of one pixel form a chain: the kernel that ends sample j's
+ * path (k_shade or a drain kernel) issues sample j + 1 in its place.
  * max_segments: 0 = unbounded + Russian roulette (reference semantics);
- * N > 0 caps each path at N extension rays.  samples_per_frame must be 1
- * (multi-sample frames are expressed as consecutive frames).  Returns once every
+ * N > 0 caps each path at N extension rays.  Returns once every
  * sample is issued: consecutive calls form one sample stream, so the last long
  * paths of a call overlap the next call; any read (accumulator, stats,
  * finalize, synchronize) drains the stream first.  Scheduling only, identical
@@ -250,7 +266,7 @@ int surf_set_camera(surf_ctx* ctx, const surf_camera_ubo* camera);
  * frame-major); continuations are traced in the order of the large BLASes
  * they can reach (SURF_KEY=0: by start instance); each phase's shadow rays are
  * traced beside the next phase's extension (SURF_OVERLAP=0: serialized). */
-int surf_render(surf_ctx* ctx, uint32_t frames, uint32_t first_frame_index,
+int surf_render(surf_ctx* ctx, uint32_t frames, uint32_t first_sample_index,
                 uint32_t max_segments, uint32_t samples_per_frame);
 int surf_clear_accumulator(surf_ctx* ctx);
 /* Float RGBA accumulator of this shard's rows, shard order, rows*width*4 floats. */
@@ -263,6 +279,10 @@ int surf_finalize_rgba8(surf_ctx* ctx, uint32_t* out_rgba8);
 /* The displayed image: fs_quad.frag:22-24 (sqrt gamma) applied to the RGBA8
  * finalize image, written as 8-bit UNORM (round to nearest even), rows*width words. */
 int surf_display_rgba8(surf_ctx* ctx, uint32_t* out_rgba8);
+/* surf_finalize_rgba8 (display 0) / surf_display_rgba8 (display 1) of a host
+ * accumulator, e.g. a frame assembled from row shards (surf_mgpu.h): n pixels
+ * of RGBA floats times inv_samples, the same rounding as the kernels. */
+int surf_pack_rgba8(const float* acc, uint32_t n, float inv_samples, int display, uint32_t* out_rgba8);
 int surf_get_stats(surf_ctx* ctx, surf_stats* out);
 int surf_synchronize(surf_ctx* ctx);
 

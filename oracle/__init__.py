@@ -48,6 +48,7 @@ def load():
         "orc_scene_set_camera": ([P, U32, U32], None), "orc_camera_ubo": ([P, P], None),
         "orc_scene_export": ([P, I32, P], C.c_uint64),
         "orc_render": ([P, U32, U32, U32, U32, U32, U32, U32, I32, P, C.POINTER(Counters)], D),
+        "orc_render_spp": ([P, U32, U32, U32, U32, U32, U32, U32, U32, I32, P, C.POINTER(Counters)], D),
         "orc_trace_closest": ([P, U32, P, P, P, P, P, P, P], None),
         "orc_trace_any": ([P, U32, P, P, P, P], None),
         "orc_trace_brute": ([P, U32, P, P, P, P, P], None),
@@ -112,12 +113,15 @@ class OracleScene:
             out[k] = bytes(buf)[: int(n)]
         return out
 
-    def render(self, width, height, frames, first_frame=0, rows=None, max_segments=0, threads=0):
+    def render(self, width, height, frames, first_frame=0, rows=None, max_segments=0, threads=0, spp=1):
+        """`frames` frames of `spp` samples per pixel (Renderer::render with
+        samplesPerFrame = spp); first_frame is the sample count before the first
+        frame (the accumulator's totalSamples; the frame index when spp = 1)."""
         r0, r1 = (0, height) if rows is None else rows
         acc = np.zeros((r1 - r0, width, 4), np.float32)
         cnt = Counters()
-        secs = load().orc_render(self._h, width, height, r0, r1, first_frame, frames, max_segments, threads,
-                                 _p(acc), C.byref(cnt))
+        secs = load().orc_render_spp(self._h, width, height, r0, r1, first_frame, frames, spp, max_segments, threads,
+                                     _p(acc), C.byref(cnt))
         return acc, cnt.as_dict(), secs
 
     def trace_closest(self, o, d):

@@ -923,15 +923,20 @@ uint64_t orc_scene_export(const orc_scene* h, int which, void* dst) {
 }
 
 /* Renderer::render (renderer.cpp:148-201) over an arbitrary list of image
- * rows: rows dynamic over OpenMP threads (renderer.cpp:163), per-pixel seed per
- * frame, acc += (rgb, 1) per sample (renderer.cpp:166-188).  acc holds
+ * rows: rows dynamic over OpenMP threads (renderer.cpp:163), then per pixel
+ * and per frame: one seed initSeed(p + totalSamples*1799) with totalSamples =
+ * first + f*spp the sample count before the frame (renderer.cpp:169), then
+ * `spp` samples in sequence, each drawing its jitter, disk sample and path
+ * from the RNG state the previous sample's path left (renderer.cpp:171-181),
+ * acc += (rgb, 1) per sample in sample order (renderer.cpp:180).  acc holds
  * nrows x W RGBA floats in list order. */
-double orc_render_rows(orc_scene* h, uint32_t W, uint32_t H, const uint32_t* rows, uint32_t nrows,
-                       uint32_t first, uint32_t frames, uint32_t maxSeg, int threads,
-                       float* acc, orc_counters* cnt) {
+double orc_render_rows_spp(orc_scene* h, uint32_t W, uint32_t H, const uint32_t* rows, uint32_t nrows,
+                           uint32_t first, uint32_t frames, uint32_t spp, uint32_t maxSeg, int threads,
+                           float* acc, orc_counters* cnt) {
     Scene& S = *h->s;
     if (S.scrW != (float)W || S.scrH != (float)H) setCamera(S, W, H);
     if (threads > 0) omp_set_num_threads(threads);
+    if (spp == 0) spp = 1;
     Counters tot; uint32_t smax = 0;
     auto t0 = std::chrono::steady_clock::now();
     #pragma omp parallel
@@ -944,13 +949,16 @@ double orc_render_rows(orc_scene* h, uint32_t W, uint32_t H, const uint32_t* row
                 uint64_t p = (uint64_t)x + (uint64_t)y * W;
                 float* a = acc + 4 * ((uint64_t)k * W + x);
                 for (uint32_t f = 0; f < frames; ++f) {
-                    uint32_t seed = seedOf((uint32_t)(p + (uint64_t)(first + f) * 1799u));
-                    float jy = rndRange(seed, -0.5f, 0.5f);   /* GCC: last argument first */
-                    float jx = rndRange(seed, -0.5f, 0.5f);
-                    V3 o, d;
-                    primaryRay(S, seed, (float)x + jx, (float)y + jy, o, d);
-                    V3 c = trace(S, seed, o, d, maxSeg, C, nullptr, sm);
-                    a[0] += c.x; a[1] += c.y; a[2] += c.z; a[3] += 1.0f;
+                    /* SizeType arithmetic truncated to U32 (renderer.cpp:169) */
+                    uint32_t seed = seedOf((uint32_t)(p + ((uint64_t)first + (uint64_t)f * spp) * 1799u));
+                    for (uint32_t s = 0; s < spp; ++s) {
+                        float jy = rndRange(seed, -0.5f, 0.5f);   /* GCC: last argument first */
+                        float jx = rndRange(seed, -0.5f, 0.5f);
+                        V3 o, d;
+                        primaryRay(S, seed, (float)x + jx, (float)y + jy, o, d);
+                        V3 c = trace(S, seed, o, d, maxSeg, C, nullptr, sm);
+                        a[0] += c.x; a[1] += c.y; a[2] += c.z; a[3] += 1.0f;
+                    }
                 }
             }
         }
@@ -964,19 +972,31 @@ double orc_render_rows(orc_scene* h, uint32_t W, uint32_t H, const uint32_t* row
     auto t1 = std::chrono::steady_clock::now();
     if (smax > S.stackMax) S.stackMax = smax;
     if (cnt) {
-        cnt->samples = (uint64_t)nrows * W * frames;
+        cnt->samples = (uint64_t)nrows * W * frames * spp;
         cnt->n_ext = tot.ext; cnt->n_hit = tot.hit; cnt->n_cont = tot.cont; cnt->n_shadow = tot.sh;
         cnt->n_acc = tot.acc; cnt->n_unocc = tot.unocc; cnt->max_segments = tot.maxSeg;
     }
     return std::chrono::duration<double>(t1 - t0).count();
 }
 
+double orc_render_rows(orc_scene* h, uint32_t W, uint32_t H, const uint32_t* rows, uint32_t nrows,
+                       uint32_t first, uint32_t frames, uint32_t maxSeg, int threads,
+                       float* acc, orc_counters* cnt) {
+    return orc_render_rows_spp(h, W, H, rows, nrows, first, frames, 1, maxSeg, threads, acc, cnt);
+}
+
+double orc_render_spp(orc_scene* h, uint32_t W, uint32_t H, uint32_t r0, uint32_t r1,
+                      uint32_t first, uint32_t frames, uint32_t spp, uint32_t maxSeg, int threads,
+                      float* acc, orc_counters* cnt) {
+    std::vector<uint32_t> rows;
+    for (uint32_t y = r0; y < r1; ++y) rows.push_back(y);
+    return orc_render_rows_spp(h, W, H, rows.data(), (uint32_t)rows.size(), first, frames, spp, maxSeg, threads, acc, cnt);
+}
+
 double orc_render(orc_scene* h, uint32_t W, uint32_t H, uint32_t r0, uint32_t r1,
                   uint32_t first, uint32_t frames, uint32_t maxSeg, int threads,
                   float* acc, orc_counters* cnt) {
-    std::vector<uint32_t> rows;
-    for (uint32_t y = r0; y < r1; ++y) rows.push_back(y);
-    return orc_render_rows(h, W, H, rows.data(), (uint32_t)rows.size(), first, frames, maxSeg, threads, acc, cnt);
+    return orc_render_spp(h, W, H, r0, r1, first, frames, 1, maxSeg, threads, acc, cnt);
 }
 
 void orc_scene_update(orc_scene* h, float dt) {

@@ -75,6 +75,18 @@ double orc_render(orc_scene*, uint32_t width, uint32_t height,
 double orc_render_rows(orc_scene*, uint32_t width, uint32_t height, const uint32_t* rows, uint32_t nrows,
                        uint32_t first_frame, uint32_t frames, uint32_t max_segments, int threads,
                        float* acc, orc_counters* out);
+/* Multi-sample frames (Renderer::render with config().samplesPerFrame = spp,
+ * renderer.cpp:160-188): frame f is seeded once per pixel with
+ * initSeed(p + 1799*(first_sample + f*spp)) and its spp samples run in
+ * sequence, each continuing the RNG state the previous sample's path left.
+ * first_sample is the accumulator's totalSamples before the first frame
+ * (= the frame index for spp 1). */
+double orc_render_spp(orc_scene*, uint32_t width, uint32_t height, uint32_t row_begin, uint32_t row_end,
+                      uint32_t first_sample, uint32_t frames, uint32_t spp, uint32_t max_segments, int threads,
+                      float* acc, orc_counters* counters);
+double orc_render_rows_spp(orc_scene*, uint32_t width, uint32_t height, const uint32_t* rows, uint32_t nrows,
+                           uint32_t first_sample, uint32_t frames, uint32_t spp, uint32_t max_segments, int threads,
+                           float* acc, orc_counters* out);
 
 /* Closest hit of n world-space rays (o,d: 3 floats each, depth starts 1e30).
  * out_t, out_u, out_v (floats), out_inst, out_prim (u32, ~0 when missed). */

@@ -24,7 +24,7 @@
  *               d  : float4(dir.xyz,    flags bits: b0 inMedium, b1 lastSpecular, b2.. segments)
  *               T  : float4(transmission.xyz, rng state bits)
  *   hit         tuv: float4(t, u, v, prim bits), inst: u32
- *   shadow q.   o  : float4(origin.xyz, tmax), d: float4(dir.xyz, sample id bits), c: float4(T*Ld, 0)
+ *   shadow q.   od : float4(origin.xyz, tmax), float4(dir.xyz, sample id bits) interleaved, c: float4(T*Ld, 0)
  *   radiance    float4 per sample of the frame batch (energy of the path)
  */
 #pragma once
@@ -121,7 +121,11 @@ struct DevCamera {
 struct Pool { float4* od; float4* T; uint8_t* key; };
 /* Where a path that used up its segment budget goes. */
 struct Sink { Pool q; uint32_t* n; uint32_t cap; };
-struct ShadowQ { float4* o; float4* d; float4* c; uint8_t* key; };   /* key: ray-order bin (light instance) */
+/* Shadow queue: od[2i] = (origin, tmax), od[2i + 1] = (direction, sample id)
+ * -- the ray k_connect traverses is one 32-B piece of one cache line, also
+ * when gathered through the shadow order -- c[i] = (T * Ld, 0), read only for
+ * an unoccluded ray; key[i] = ray-order bin. */
+struct ShadowQ { float4* od; float4* c; uint8_t* key; };
 
 /* Device counters of the sample stream.  Double-buffered by phase parity so no
  * kernel writes a word another block of the same launch still reads. */
@@ -139,7 +143,12 @@ struct Counters {
      * samples of the permA pixels listed first in StreamGeom::perm, then each
      * frame's other pixels frame by frame (0: frame-major throughout) */
     uint32_t permFrames, permA;
-    unsigned long long issued[2];    /* stream samples issued, per parity */
+    /* samples per frame (config().samplesPerFrame, renderer.cpp:171): a frame's
+     * samples of one pixel form a chain -- sample k + 1 starts from the RNG state
+     * sample k's path left -- so k_regen issues only the first sample of each
+     * (frame, pixel) and the kernel that ends a sample's path starts the next */
+    uint32_t spp;
+    unsigned long long issued[2];    /* stream chains issued (first samples of (frame, pixel)), per parity */
     unsigned long long limit;        /* host-written issue limit (frame window) */
     unsigned long long baseFrame;    /* absolute frame index of stream frame 0 */
     unsigned long long ev[16];       /* ext, hit, cont, shadow, acc, unocc, tail paths, capped paths, wavefront ext */
@@ -166,7 +175,10 @@ __device__ __forceinline__ void noteCapped(Counters* C, uint32_t sid) {
     noteCappedSid(true, C, sid);
 }
 
-/* Where a stream sample lives: radiance slot sid = (frame % window) * npx + pixel. */
+/* Where a stream sample lives: radiance slot sid = (pass % window) * npx + pixel,
+ * pass = the sample's index in the stream (frame * spp + its place in the
+ * frame; window is a multiple of spp, so a frame's samples occupy consecutive
+ * slots and slot % spp is the place in the frame). */
 struct StreamGeom {
     const uint32_t* rows;            /* shard rows */
     uint32_t width, npx, window;
@@ -1904,6 +1916,8 @@ __device__ __forceinline__ void addRadiance(float4* rad, uint32_t sid, V3 c) {
 /* Result of shading one hit: what the path does next. */
 struct ShadeOut {
     bool cont, shadow, hitGeom, accd, capped;
+    bool next;                       /* the path ended and its frame's next sample continues it (k_shade) */
+    uint32_t seedOut;                /* RNG state after the bounce's draws (the next sample of a frame starts from it) */
     bool addRad;                     /* rad[sid] += radd (miss / light hit), done by the caller */
     uint32_t seg;                    /* extension rays of the path so far */
     V3 radd;
@@ -2003,10 +2017,11 @@ __device__ __forceinline__ void sampleNEE(const DevScene& S, const ShadeTables& 
 template <bool SPEC = false>
 __device__ __forceinline__ void shadePath(const DevScene& S, const ShadeTables& Tb, float4 o4, float4 d4, float4 T4, float4 h4,
                                           uint32_t inst, uint32_t maxSeg, uint32_t zeroCutoff, ShadeOut& r) {
-    r.cont = r.shadow = r.hitGeom = r.accd = r.capped = r.addRad = false;
+    r.cont = r.shadow = r.hitGeom = r.accd = r.capped = r.addRad = r.next = false;
     const uint32_t sid = f2u(o4.w);
     uint32_t flags = f2u(d4.w);
     uint32_t seed = f2u(T4.w);
+    r.seedOut = seed;
     const V3 o = xyz(o4), d = xyz(d4);
     V3 T = xyz(T4);
     bool lastSpecular = (flags & kFlagSpecular) != 0u;
@@ -2125,6 +2140,7 @@ __device__ __forceinline__ void shadePath(const DevScene& S, const ShadeTables& 
      * TIR orbits in the glass lens that never terminate in the reference. */
     if (zeroCutoff && T.x < 1.17549435e-38f && T.y < 1.17549435e-38f && T.z < 1.17549435e-38f) alive = false;
     r.capped = alive && (maxSeg != 0u && seg >= maxSeg);
+    r.seedOut = seed;
     if (alive && !(maxSeg != 0u && seg >= maxSeg)) {
         r.cont = true;
         const V3 O = add(P, lscl(kEps, R));
@@ -2133,6 +2149,45 @@ __device__ __forceinline__ void shadePath(const DevScene& S, const ShadeTables& 
         r.d = make_float4(R.x, R.y, R.z, u2f(flags));
         r.T = make_float4(T.x, T.y, T.z, u2f(seed));
     }
+}
+
+/* Camera::getPrimaryRay + sampleDefocusDisk (camera.h:59-87) with the jitter
+ * of renderer.cpp:173-177, drawn from `seed` in g++'s order (last argument
+ * first): the path record of sample `sid` at shard pixel lp. */
+__device__ __forceinline__ void cameraSample(const DevCamera& cam, const StreamGeom& G, uint32_t lp, uint32_t sid, uint32_t seed,
+                                             float4& o4, float4& d4, float4& T4) {
+    const uint32_t rowi = lp / G.width;
+    const uint32_t x = lp - rowi * G.width;
+    const uint32_t row = G.rows[rowi];
+    const float jy = rndRange(seed, -0.5f, 0.5f);
+    const float jx = rndRange(seed, -0.5f, 0.5f);
+    const float u = ((float)x + jx) * cam.invW, v = ((float)row + jy) * cam.invH;
+    V3 origin = ld3(cam.pos);
+    if (cam.defocus) {
+        float sx, sy;
+        do {
+            sy = rndRange(seed, -1.0f, 1.0f);
+            sx = rndRange(seed, -1.0f, 1.0f);
+        } while (sx * sx + sy * sy > 1.0f);
+        origin = add(origin, add(lscl(sx, ld3(cam.diskU)), lscl(sy, ld3(cam.diskV))));
+    }
+    const V3 plane = add(add(ld3(cam.firstPixel), lscl(u, ld3(cam.uVec))), lscl(v, ld3(cam.vVec)));
+    const V3 dir = normalize(sub(plane, origin));
+    o4 = make_float4(origin.x, origin.y, origin.z, u2f(sid));
+    d4 = make_float4(dir.x, dir.y, dir.z, u2f(kFlagSpecular | (1u << 2)));
+    T4 = make_float4(1.0f, 1.0f, 1.0f, u2f(seed));
+}
+
+/* The next sample of a multi-sample frame (Renderer::render's sample loop,
+ * renderer.cpp:171-181): when the path of sample `sid` ended and its frame has
+ * samples left for the pixel, the pixel's next camera sample -- radiance slot
+ * sid + npx (the frame's samples occupy consecutive slots) -- drawn from the
+ * RNG state the ended path left.  False for a frame's last sample. */
+__device__ __forceinline__ bool chainNext(const DevCamera& cam, const StreamGeom& G, uint32_t spp, uint32_t sid, uint32_t slot,
+                                          uint32_t seed, float4& o4, float4& d4, float4& T4) {
+    if (spp <= 1u || slot % spp == spp - 1u) return false;
+    cameraSample(cam, G, sid - slot * G.npx, sid + G.npx, seed, o4, d4, T4);
+    return true;
 }
 
 /* Frame completion: one atomic per distinct frame slot in the wave (lanes of a
@@ -2153,7 +2208,7 @@ __global__ __launch_bounds__(kBlock, SURF_SHADE_WAVES) void k_shade(DevScene S, 
                                                   const uint32_t* __restrict__ hitInst, ShadowQ Q,
                                                   float4* __restrict__ rad, uint32_t* __restrict__ frameDone,
                                                   uint32_t npx, uint32_t window, Counters* C, int par,
-                                                  const uint32_t* __restrict__ order) {
+                                                  const uint32_t* __restrict__ order, DevCamera cam, StreamGeom G) {
     if (blockIdx.x * blockDim.x >= C->nIn[par]) return;     /* nothing to shade in this block */
     __shared__ DevInstance sInst[LDS_TABLES ? kLdsInst : 1];
     __shared__ DevMaterial sMat[LDS_TABLES ? kLdsMats : 1];
@@ -2168,14 +2223,14 @@ __global__ __launch_bounds__(kBlock, SURF_SHADE_WAVES) void k_shade(DevScene S, 
     __shared__ uint32_t sWave[2][kBlock / 64][2];
     __shared__ uint32_t sBase[2][2];
     const uint32_t n = C->nIn[par];
-    const uint32_t maxSeg = C->maxSeg, zeroCutoff = C->zeroCutoff;
+    const uint32_t maxSeg = C->maxSeg, zeroCutoff = C->zeroCutoff, spp = C->spp;
     const uint32_t wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
     uint32_t it = 0;
     unsigned long long cHit = 0, cCont = 0, cSh = 0, cAcc = 0, cCap = 0;
     for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x, it ^= 1u) {
         const uint32_t i = base + threadIdx.x;
         ShadeOut r;
-        r.cont = r.shadow = r.hitGeom = r.accd = r.capped = r.addRad = false;
+        r.cont = r.shadow = r.hitGeom = r.accd = r.capped = r.addRad = r.next = false;
         r.seg = 0;
         uint32_t slot = 0, sid = 0, hinst = kUnset;
         const bool active = i < n;
@@ -2187,8 +2242,14 @@ __global__ __launch_bounds__(kBlock, SURF_SHADE_WAVES) void k_shade(DevScene S, 
             hinst = ldSu(&hitInst[i]);
             shadePath(S, Tb, o4, ldS(&cur.od[2u * (j) + 1u]), ldS(&cur.T[j]), ldS(&hitTUV[i]), hinst, maxSeg, zeroCutoff, r);
             if (r.addRad) addRadiance(rad, sid, r.radd);
+            /* the sample ended: its frame's next sample of this pixel takes its
+             * place in the next pool (a camera ray, not a continuation) */
+            if (!r.cont && chainNext(cam, G, spp, sid, slot, r.seedOut, r.o, r.d, r.T)) {
+                r.next = true;
+                rad[sid + npx] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            }
         }
-        const unsigned long long mCont = __ballot(r.cont), mSh = __ballot(r.shadow);
+        const unsigned long long mCont = __ballot(r.cont || r.next), mSh = __ballot(r.shadow);
         if (laneId() == 0) { sWave[it][wv][0] = (uint32_t)__popcll(mCont); sWave[it][wv][1] = (uint32_t)__popcll(mSh); }
         __syncthreads();
         if (threadIdx.x == 0) {
@@ -2202,12 +2263,13 @@ __global__ __launch_bounds__(kBlock, SURF_SHADE_WAVES) void k_shade(DevScene S, 
         for (uint32_t k = 0; k < wv; ++k) { jc += sWave[it][k][0]; js += sWave[it][k][1]; }
         jc += rankBelow(mCont);
         js += rankBelow(mSh);
-        if (r.cont) {
+        if (r.cont || r.next) {
             stS(&nxt.od[2u * (jc)], r.o); stS(&nxt.od[2u * (jc) + 1u], r.d); stS(&nxt.T[jc], r.T);
-            nxt.key[jc] = poolKey(S, hinst, r.o, r.d);   /* starts on the instance it hit, from this quadrant */
+            /* starts on the instance it hit, from this quadrant; camera rays in their own bin */
+            nxt.key[jc] = r.next ? (uint8_t)(kBins - 1u) : poolKey(S, hinst, r.o, r.d);
         }
         if (r.shadow) {
-            stS(&Q.o[js], r.so); stS(&Q.d[js], r.sd); stS(&Q.c[js], r.sc);
+            stS(&Q.od[2u * js], r.so); stS(&Q.od[2u * js + 1u], r.sd); stS(&Q.c[js], r.sc);
             Q.key[js] = shadowKey(S, r.light, r.so);       /* toward the same light from the same octant of the scene */
         }
         /* a path that ends here may still have this phase's shadow ray pending:
@@ -2239,7 +2301,7 @@ __global__ __launch_bounds__(kBlock, SURF_TRACE_WAVES) void k_connect(DevScene S
         bool unocc = false;
         if (i0 < n) {
             const uint32_t i = order ? order[i0] : i0;
-            const float4 o = ldS(&Q.o[i]), d = ldS(&Q.d[i]);
+            const float4 o = ldS(&Q.od[2u * i]), d = ldS(&Q.od[2u * i + 1u]);
             float depth = o.w, u = 0.0f, v = 0.0f;
             uint32_t inst = kUnset, prim = kUnset;
             const bool occ = traceScene<true, LW>(S, Tt, xyz(o), xyz(d), depth, u, v, inst, prim, stk, stride);
@@ -2254,9 +2316,11 @@ __global__ __launch_bounds__(kBlock, SURF_TRACE_WAVES) void k_connect(DevScene S
     blockCount<2>(C, {5, 4}, {cUn, cUn});
 }
 
-/* Camera::getPrimaryRay + sampleDefocusDisk (camera.h:59-87), jitter of
- * renderer.cpp:173-177; draw order of g++ (last argument first).  Fills
- * pool[par^1] after the continuing paths, up to capacity and the issue limit. */
+/* Fills pool[par^1] after the continuing paths, up to capacity and the issue
+ * limit, with the first sample of the next (frame, pixel) chains in issue
+ * order: frame f's first sample is stream pass f * spp, seeded
+ * initSeed(p + 1799 * (baseFrame + f * spp)) (renderer.cpp:169; baseFrame =
+ * the sample count before the stream). */
 __global__ __launch_bounds__(kBlock) void k_regen(DevCamera cam, Pool nxt, float4* __restrict__ rad, Counters* C, int par,
                                                   uint32_t capacity, StreamGeom G) {
     const int nx = par ^ 1;
@@ -2264,11 +2328,12 @@ __global__ __launch_bounds__(kBlock) void k_regen(DevCamera cam, Pool nxt, float
     const unsigned long long iss = C->issued[par];
     const unsigned long long lim = C->limit;
     const unsigned long long base = C->baseFrame;
+    const uint32_t spp = C->spp;
     const uint32_t room = capacity - cont;
     const unsigned long long left = lim > iss ? lim - iss : 0ull;
     const uint32_t nnew = (unsigned long long)room < left ? room : (uint32_t)left;
     const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
-    /* frame / pixel of the first new sample, then step without 64-bit divisions */
+    /* frame / pixel of the first new chain, then step without 64-bit divisions */
     const unsigned long long f0 = iss / G.npx;
     const uint32_t lp0 = (uint32_t)(iss - f0 * G.npx);
     /* the permuted head of the stream (surf_hip.hip classifyPixels) */
@@ -2287,31 +2352,17 @@ __global__ __launch_bounds__(kBlock) void k_regen(DevCamera cam, Pool nxt, float
             lp -= df * G.npx;
             f = f0 + df;
         }
-        const uint32_t slot = (uint32_t)(f % G.window);
+        const unsigned long long pass = f * spp;
+        const uint32_t slot = (uint32_t)(pass % G.window);
         const uint32_t rowi = lp / G.width;
-        const uint32_t x = lp - rowi * G.width;
-        const uint32_t row = G.rows[rowi];
-        const uint32_t p = x + row * G.width;
+        const uint32_t p = (lp - rowi * G.width) + G.rows[rowi] * G.width;
         const uint32_t sid = slot * G.npx + lp;
-        uint32_t seed = initSeed(p + (uint32_t)(base + f) * 1799u);
-        const float jy = rndRange(seed, -0.5f, 0.5f);
-        const float jx = rndRange(seed, -0.5f, 0.5f);
-        const float u = ((float)x + jx) * cam.invW, v = ((float)row + jy) * cam.invH;
-        V3 origin = ld3(cam.pos);
-        if (cam.defocus) {
-            float sx, sy;
-            do {
-                sy = rndRange(seed, -1.0f, 1.0f);
-                sx = rndRange(seed, -1.0f, 1.0f);
-            } while (sx * sx + sy * sy > 1.0f);
-            origin = add(origin, add(lscl(sx, ld3(cam.diskU)), lscl(sy, ld3(cam.diskV))));
-        }
-        const V3 plane = add(add(ld3(cam.firstPixel), lscl(u, ld3(cam.uVec))), lscl(v, ld3(cam.vVec)));
-        const V3 dir = normalize(sub(plane, origin));
+        float4 o4, d4, T4;
+        cameraSample(cam, G, lp, sid, initSeed(p + (uint32_t)(base + pass) * 1799u), o4, d4, T4);
         const uint32_t slotIdx = cont + k;
-        stS(&nxt.od[2u * (slotIdx)], make_float4(origin.x, origin.y, origin.z, u2f(sid)));
-        stS(&nxt.od[2u * (slotIdx) + 1u], make_float4(dir.x, dir.y, dir.z, u2f(kFlagSpecular | (1u << 2))));
-        stS(&nxt.T[slotIdx], make_float4(1.0f, 1.0f, 1.0f, u2f(seed)));
+        stS(&nxt.od[2u * (slotIdx)], o4);
+        stS(&nxt.od[2u * (slotIdx) + 1u], d4);
+        stS(&nxt.T[slotIdx], T4);
         nxt.key[slotIdx] = (uint8_t)(kBins - 1u);                      /* camera rays */
         rad[sid] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     }
@@ -2339,10 +2390,12 @@ __global__ __launch_bounds__(kBlock) void k_regen(DevCamera cam, Pool nxt, float
 __device__ __forceinline__ bool runPath(const DevScene& S, const TraceTables& Tt, const ShadeTables& Tb, float4 o4, float4 d4,
                                         float4 T4, uint32_t budget, const Sink& sink, float4* __restrict__ rad,
                                         uint32_t* __restrict__ frameDone, uint32_t npx, uint32_t window, Counters* C,
-                                        uint32_t* stk, uint32_t stride, uint32_t firstCounted) {
-    const uint32_t maxSeg = C->maxSeg, zeroCutoff = C->zeroCutoff;
-    const uint32_t slot = f2u(o4.w) / npx;
-    uint32_t nExt = 0, nHit = 0, nCont = 0, nSh = 0, nAcc = 0, nUn = 0;   /* per path: 32 bits suffice */
+                                        uint32_t* stk, uint32_t stride, uint32_t firstCounted, const DevCamera& cam,
+                                        const StreamGeom& G) {
+    const uint32_t maxSeg = C->maxSeg, zeroCutoff = C->zeroCutoff, spp = C->spp;
+    const uint32_t st = blockIdx.x % kStripes;
+    uint32_t slot = f2u(o4.w) / npx;
+    uint32_t nExt = 0, nHit = 0, nCont = 0, nSh = 0, nAcc = 0, nUn = 0, nDone = 0;   /* per path: 32 bits suffice */
     bool done = true;
     for (;;) {
         float depth = kFarAway, u = 0.0f, v = 0.0f;
@@ -2365,7 +2418,15 @@ __device__ __forceinline__ bool runPath(const DevScene& S, const TraceTables& Tt
         if (r.capped) {
             noteCapped(C, f2u(o4.w));
         }
-        if (!r.cont) { atomicMax(&C->segMax, r.seg); break; }
+        if (!r.cont) {
+            atomicMax(&C->segMax, r.seg);
+            __threadfence();      /* radiance before completion: other streams' kernels read it */
+            atomicAdd(&frameDone[st * window + slot], 1u);
+            ++nDone;
+            /* the frame's next sample of this pixel continues on this lane */
+            if (chainNext(cam, G, spp, f2u(o4.w), slot, r.seedOut, o4, d4, T4)) { ++slot; continue; }
+            break;
+        }
         ++nCont;
         if (budget != 0u && nExt >= budget) {
             const uint32_t k = atomicAdd(sink.n, 1u);
@@ -2377,16 +2438,11 @@ __device__ __forceinline__ bool runPath(const DevScene& S, const TraceTables& Tt
         }
         o4 = r.o; d4 = r.d; T4 = r.T;
     }
-    const uint32_t st = blockIdx.x % kStripes;
     unsigned long long* ev = C->evS[st];
-    if (done) {
-        __threadfence();          /* radiance before completion: other streams' kernels read it */
-        atomicAdd(&frameDone[st * window + slot], 1u);
-    }
     atomicAdd(&ev[0], (unsigned long long)(nExt - firstCounted)); atomicAdd(&ev[1], (unsigned long long)nHit);
     atomicAdd(&ev[2], (unsigned long long)nCont); atomicAdd(&ev[3], (unsigned long long)nSh);
     atomicAdd(&ev[4], (unsigned long long)nAcc); atomicAdd(&ev[5], (unsigned long long)nUn);
-    if (done) atomicAdd(&ev[6], 1ull);
+    if (nDone) atomicAdd(&ev[6], (unsigned long long)nDone);
     return done;
 }
 
@@ -2399,7 +2455,8 @@ __device__ __forceinline__ bool runPath(const DevScene& S, const TraceTables& Tt
 template <bool LDS_TABLES>
 __global__ __launch_bounds__(64, SURF_TAIL_WAVES) void k_tail(DevScene S, Pool cur, uint32_t n, uint32_t lpw, float4* __restrict__ rad,
                                              uint32_t* __restrict__ frameDone, uint32_t npx, uint32_t window, Counters* C,
-                                             uint32_t stackWords, uint32_t firstCounted, uint32_t budget, Pool surv) {
+                                             uint32_t stackWords, uint32_t firstCounted, uint32_t budget, Pool surv,
+                                             DevCamera cam, StreamGeom G) {
     extern __shared__ uint32_t lds[];
     const TraceTables Tt = traceTables<LDS_TABLES>(S, lds, stackWords);
     __shared__ DevInstance sInst[LDS_TABLES ? kLdsInst : 1];
@@ -2414,7 +2471,7 @@ __global__ __launch_bounds__(64, SURF_TAIL_WAVES) void k_tail(DevScene S, Pool c
     const uint32_t i = blockIdx.x * lpw + lane;
     if (lane >= lpw || i >= n) return;
     runPath(S, Tt, Tb, cur.od[2u * (i)], cur.od[2u * (i) + 1u], cur.T[i], budget, Sink{surv, &C->survN, C->survCap}, rad, frameDone, npx, window, C,
-            lds + threadIdx.x, blockDim.x, firstCounted);
+            lds + threadIdx.x, blockDim.x, firstCounted, cam, G);
 }
 
 /* Cooperative tail: one path per 64-lane wave (block), for the long paths
@@ -2429,7 +2486,7 @@ __global__ __launch_bounds__(64, SURF_TAIL_WAVES) void k_tail(DevScene S, Pool c
 template <bool LDS, bool W2 = false>
 __global__ __launch_bounds__(64, SURF_COOP_WAVES) void k_tail_coop(DevScene S, Pool cur, uint32_t n, float4* __restrict__ rad,
                                                   uint32_t* __restrict__ frameDone, uint32_t npx, uint32_t window, Counters* C,
-                                                  uint32_t stackWords, uint32_t firstCounted) {
+                                                  uint32_t stackWords, uint32_t firstCounted, DevCamera cam, StreamGeom G) {
     extern __shared__ uint32_t lds[];
     const TraceTables Tt = coopTrace<LDS>(S, lds, stackWords + proWords(S));
     /* shading's instance / material / light tables in LDS too: a path's
@@ -2440,10 +2497,11 @@ __global__ __launch_bounds__(64, SURF_COOP_WAVES) void k_tail_coop(DevScene S, P
     const bool lead = threadIdx.x == 0;
     float* rstk = reinterpret_cast<float*>(lds);     /* the record stack (16 words per entry) */
     float4* pro = reinterpret_cast<float4*>(lds + stackWords);
-    const uint32_t maxSeg = C->maxSeg, zeroCutoff = C->zeroCutoff;
+    const uint32_t maxSeg = C->maxSeg, zeroCutoff = C->zeroCutoff, spp = C->spp;
+    const uint32_t st = blockIdx.x % kStripes;
     float4 o4 = cur.od[2u * (i)], d4 = cur.od[2u * (i) + 1u], T4 = cur.T[i];
-    const uint32_t slot = f2u(o4.w) / npx;
-    unsigned long long nExt = 0, nHit = 0, nCont = 0, nSh = 0, nAcc = 0, nUn = 0;
+    uint32_t slot = f2u(o4.w) / npx;
+    unsigned long long nExt = 0, nHit = 0, nCont = 0, nSh = 0, nAcc = 0, nUn = 0, nDone = 0;
 #if SURF_DRAIN_TRACE
     const unsigned long long tStart = wall_clock64();
     const uint32_t state0 = drainState(d4, T4);
@@ -2495,7 +2553,14 @@ __global__ __launch_bounds__(64, SURF_COOP_WAVES) void k_tail_coop(DevScene S, P
             noteCapped(C, f2u(o4.w));
         }
         if (!r.cont) {
-            if (lead) atomicMax(&C->segMax, r.seg);
+            if (lead) {
+                atomicMax(&C->segMax, r.seg);
+                __threadfence();      /* radiance before completion */
+                atomicAdd(&frameDone[st * window + slot], 1u);
+            }
+            ++nDone;
+            /* the frame's next sample of this pixel continues on this wave */
+            if (chainNext(cam, G, spp, f2u(o4.w), slot, r.seedOut, o4, d4, T4)) { ++slot; continue; }
             break;
         }
         ++nCont;
@@ -2505,13 +2570,10 @@ __global__ __launch_bounds__(64, SURF_COOP_WAVES) void k_tail_coop(DevScene S, P
 #if SURF_DRAIN_TRACE
         drainTraceEnd(tStart, (uint32_t)nExt, state0);
 #endif
-        const uint32_t st = blockIdx.x % kStripes;
         unsigned long long* ev = C->evS[st];
-        __threadfence();
-        atomicAdd(&frameDone[st * window + slot], 1u);
         atomicAdd(&ev[0], nExt - (unsigned long long)firstCounted); atomicAdd(&ev[1], nHit); atomicAdd(&ev[2], nCont);
         atomicAdd(&ev[3], nSh); atomicAdd(&ev[4], nAcc); atomicAdd(&ev[5], nUn);
-        atomicAdd(&ev[6], 1ull);
+        atomicAdd(&ev[6], nDone);
 #if SURF_SEG_TIMING
         atomicAdd(&C->dbg[0], cyc[0]); atomicAdd(&C->dbg[1], cyc[1]); atomicAdd(&C->dbg[2], cyc[2]);
         atomicAdd(&C->dbg[3], nExt); atomicAdd(&C->dbg[4], nSh);
@@ -2551,7 +2613,7 @@ __device__ __forceinline__ void ldsStoreRel(uint32_t* p, uint32_t v) {
 }
 
 /* Every wave counts its paths' events and adds them once at exit. */
-struct PairCounts { uint32_t ext, hit, cont, sh, acc, un, paths; };
+struct PairCounts { uint32_t ext, hit, cont, sh, acc, un, paths, samples; };   /* paths: taken from the queue; samples: finished */
 
 /* One path of the queue on the calling wave (w); its shadow rays go to the
  * sibling while box.help[w] is set. */
@@ -2559,9 +2621,9 @@ template <bool W2>
 __device__ __forceinline__ void pairPath(const DevScene& S, const TraceTables& Tt, const ShadeTables& Tb, PairBox& box, uint32_t w,
                                          float4 o4, float4 d4, float4 T4, float4* __restrict__ rad, uint32_t* __restrict__ frameDone,
                                          uint32_t npx, uint32_t window, Counters* C, float* rstk, float4* pro, bool lead,
-                                         uint32_t& posted, PairCounts& pc) {
-    const uint32_t maxSeg = C->maxSeg, zeroCutoff = C->zeroCutoff;
-    const uint32_t slot = f2u(o4.w) / npx;
+                                         uint32_t& posted, PairCounts& pc, const DevCamera& cam, const StreamGeom& G) {
+    const uint32_t maxSeg = C->maxSeg, zeroCutoff = C->zeroCutoff, spp = C->spp;
+    uint32_t slot = f2u(o4.w) / npx;
     bool pend = false;                     /* a posted shadow ray awaits its answer */
     for (;;) {
         float depth = kFarAway, u = 0.0f, v = 0.0f;
@@ -2601,29 +2663,33 @@ __device__ __forceinline__ void pairPath(const DevScene& S, const TraceTables& T
         if (lead && r.capped) noteCapped(C, f2u(o4.w));
         if (!r.cont) {
             if (lead) atomicMax(&C->segMax, r.seg);
+            if (pend) {                    /* the sample's last shadow ray */
+                while (ldsLoadAcq(&box.done[w]) != posted) __builtin_amdgcn_s_sleep(1);
+                if (!box.occ[w]) {
+                    if (lead) addRadiance(rad, f2u(box.sd[w].w), xyz(box.sc[w]));
+                    ++pc.un; ++pc.acc;
+                }
+                pend = false;
+            }
+            ++pc.samples;
+            if (lead) {
+                __threadfence();           /* radiance before completion */
+                atomicAdd(&frameDone[(blockIdx.x % kStripes) * window + slot], 1u);
+            }
+            /* the frame's next sample of this pixel continues on this wave */
+            if (chainNext(cam, G, spp, f2u(o4.w), slot, r.seedOut, o4, d4, T4)) { ++slot; continue; }
             break;
         }
         ++pc.cont;
         o4 = r.o; d4 = r.d; T4 = r.T;
     }
-    if (pend) {                            /* the last segment's shadow ray */
-        while (ldsLoadAcq(&box.done[w]) != posted) __builtin_amdgcn_s_sleep(1);
-        if (!box.occ[w]) {
-            if (lead) addRadiance(rad, f2u(box.sd[w].w), xyz(box.sc[w]));
-            ++pc.un; ++pc.acc;
-        }
-    }
     ++pc.paths;
-    if (lead) {
-        __threadfence();          /* radiance before completion */
-        atomicAdd(&frameDone[(blockIdx.x % kStripes) * window + slot], 1u);
-    }
 }
 
 template <bool LDS, bool W2 = false>
 __global__ __launch_bounds__(128, SURF_COOP_WAVES) void k_tail_pair(DevScene S, Pool cur, uint32_t n, float4* __restrict__ rad,
                                                    uint32_t* __restrict__ frameDone, uint32_t npx, uint32_t window, Counters* C,
-                                                   uint32_t stackWords, uint32_t firstCounted) {
+                                                   uint32_t stackWords, uint32_t firstCounted, DevCamera cam, StreamGeom G) {
     extern __shared__ uint32_t lds[];
     __shared__ PairBox box;
     /* LDS: [record stack | prologue table] per wave, then the trace tables and the shading tables */
@@ -2639,7 +2705,7 @@ __global__ __launch_bounds__(128, SURF_COOP_WAVES) void k_tail_pair(DevScene S, 
     const bool lead = (threadIdx.x & 63u) == 0u;
     float* rstk = reinterpret_cast<float*>(lds + w * per);
     float4* pro = reinterpret_cast<float4*>(lds + w * per + stackWords);
-    PairCounts pc{0, 0, 0, 0, 0, 0, 0};
+    PairCounts pc{0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t posted = 0u;                             /* == box.post[w] */
     for (;;) {
         uint32_t i = 0u;
@@ -2647,7 +2713,7 @@ __global__ __launch_bounds__(128, SURF_COOP_WAVES) void k_tail_pair(DevScene S, 
         i = __builtin_amdgcn_readfirstlane(i);
         if (i >= n) break;
         pairPath<W2>(S, Tt, Tb, box, w, cur.od[2u * i], cur.od[2u * i + 1u], cur.T[i], rad, frameDone, npx, window, C, rstk, pro,
-                 lead, posted, pc);
+                 lead, posted, pc, cam, G);
     }
     /* queue empty: leave the path loop, then serve the sibling's shadow rays
      * while it still runs a path (one of the two always sees the other's 0) */
@@ -2679,7 +2745,7 @@ __global__ __launch_bounds__(128, SURF_COOP_WAVES) void k_tail_pair(DevScene S, 
         atomicAdd(&ev[0], (unsigned long long)(pc.ext - pc.paths * firstCounted)); atomicAdd(&ev[1], (unsigned long long)pc.hit);
         atomicAdd(&ev[2], (unsigned long long)pc.cont); atomicAdd(&ev[3], (unsigned long long)pc.sh);
         atomicAdd(&ev[4], (unsigned long long)pc.acc); atomicAdd(&ev[5], (unsigned long long)pc.un);
-        atomicAdd(&ev[6], (unsigned long long)pc.paths);
+        atomicAdd(&ev[6], (unsigned long long)pc.samples);
     }
 }
 
@@ -2704,7 +2770,7 @@ __global__ __launch_bounds__(kBlock) void k_accumulate(const float4* __restrict_
 }
 
 /* wavefront_finalize.comp + RgbaToU32 (cvtps2dq round-to-even, packus saturation) */
-__device__ __forceinline__ uint32_t packChannel(float v) {
+SURF_HD uint32_t packChannel(float v) {
     if (!(v >= -2147483648.0f && v < 2147483648.0f)) return 0u;
     const float r = rintf(v);
     return r < 0.0f ? 0u : (r > 255.0f ? 255u : (uint32_t)r);
@@ -2722,7 +2788,7 @@ __global__ __launch_bounds__(kBlock) void k_finalize(const float4* __restrict__ 
  * (UNORM: c/255) and writes sqrt(c/255) to an 8-bit UNORM target; the target's
  * float->UNORM8 conversion is taken as round-to-nearest-even with saturation
  * (packChannel).  Fused with k_finalize's packing. */
-__device__ __forceinline__ uint32_t displayChannel(uint32_t c8) {
+SURF_HD uint32_t displayChannel(uint32_t c8) {
     return packChannel(sqrtf((float)c8 / 255.0f) * 255.0f);
 }
 __global__ __launch_bounds__(kBlock) void k_display(const float4* __restrict__ acc, uint32_t* __restrict__ out,

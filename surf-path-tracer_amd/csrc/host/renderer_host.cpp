@@ -1,8 +1,9 @@
 /*
  * renderer_host.cpp -- WaveFrontRenderer (headers/renderer.h:207-436) on top of
- * the C-ABI.  render() keeps the reference's frame semantics: every call adds
- * config().samplesPerFrame samples per pixel, each seeded from the running
- * sample count (renderer.cpp:169, 983), and camera state is re-read per frame
+ * the C-ABI.  render() keeps the reference's CPU frame semantics: every call
+ * adds config().samplesPerFrame samples per pixel, seeded once per frame from
+ * the running sample count (renderer.cpp:169) and run in sequence on that one
+ * RNG stream (renderer.cpp:171-181), and camera state is re-read per frame
  * (renderer.cpp:972-979).  render() returns once the frame's samples are
  * issued: consecutive frames form one sample stream on the device (no
  * per-frame drain); reads (accumulator, images, frameInfo() with lumenOutput)
@@ -53,8 +54,10 @@ void WaveFrontRenderer::render(F32 /*deltaTime*/) {
     }
     const CameraUBO ubo = m_camera.toUBO();
     check(surf_set_camera(m_ctx, &ubo), m_ctx, "surf_set_camera");
+    /* one frame of samplesPerFrame samples, seeded from the running sample
+     * count, its samples chaining their RNG state (renderer.cpp:160-188) */
     const U32 spp = m_config.samplesPerFrame ? m_config.samplesPerFrame : 1u;
-    check(surf_render(m_ctx, spp, m_totalSamples, m_config.maxSegments, 1), m_ctx, "surf_render");
+    check(surf_render(m_ctx, 1, m_totalSamples, m_config.maxSegments, spp), m_ctx, "surf_render");
     m_totalSamples += spp;
     m_frameInfo.totalSamples = m_totalSamples;
     m_energyStale = true;       /* render() itself never waits for the stream (no per-frame drain) */

@@ -118,13 +118,17 @@ struct surf_ctx {
     std::vector<void*> wfAllocs;
     uint64_t totalSamples = 0;     /* frames rendered since the last clear (samples per pixel) */
 
-    /* sample stream: frames [baseFrame, baseFrame + targetFrames) requested */
+    /* sample stream: targetFrames frames of spp samples per pixel requested,
+     * i.e. passes (samples per pixel) [0, targetFrames * spp) after the
+     * baseFrame samples rendered before the stream; pass q lives in radiance
+     * slot q % window (window a multiple of spp) */
     bool streamActive = false;
-    uint64_t baseFrame = 0;
-    uint64_t targetFrames = 0;     /* relative frames requested */
-    uint64_t accFrames = 0;        /* relative frames accumulated */
+    uint64_t baseFrame = 0;        /* sample count before the stream (the reference's totalSamples) */
+    uint64_t targetFrames = 0;     /* frames requested (chains per pixel) */
+    uint64_t accPasses = 0;        /* passes accumulated (in order) */
+    uint32_t spp = 1;              /* samples per frame of the stream (a frame's samples chain their RNG state) */
     uint32_t streamMaxSeg = 0;
-    bool zeroCutoff = true;        /* radiance-neutral early end of T == 0 paths */
+    int zeroCutoff = -1;           /* early end of paths with throughput < FLT_MIN: 1 on, 0 off, -1 automatic (on for 1-sample frames) */
     uint64_t pushedLimit = 0;
     uint32_t tailPaths = 0;        /* drain policy (surf_set_tail_policy), 0 = automatic */
     uint32_t tailBudget = 16;      /* per-stage segment budget of the drain tail (0 = one stage); 16: measured fastest */
@@ -342,8 +346,7 @@ int allocWavefront(surf_ctx* c) {
     }
     if ((rc = devAlloc(c, c->wfAllocs, &c->hitTUV, cap))) return rc;
     if ((rc = devAlloc(c, c->wfAllocs, &c->hitInst, cap))) return rc;
-    if ((rc = devAlloc(c, c->wfAllocs, &c->Q.o, cap))) return rc;
-    if ((rc = devAlloc(c, c->wfAllocs, &c->Q.d, cap))) return rc;
+    if ((rc = devAlloc(c, c->wfAllocs, &c->Q.od, 2 * cap))) return rc;
     if ((rc = devAlloc(c, c->wfAllocs, &c->Q.c, cap))) return rc;
     if ((rc = devAlloc(c, c->wfAllocs, &c->Q.key, cap))) return rc;
     if ((rc = devAlloc(c, c->wfAllocs, &c->ctr, 1))) return rc;
@@ -387,16 +390,25 @@ int allocWavefront(surf_ctx* c) {
  * min(32 GiB, a quarter of the free HBM) holds.  A later, longer stream grows
  * the ring; a window set by surf_set_frame_batch is kept as given. */
 constexpr uint64_t kWindowFloor = 256;
-int ensureWindow(surf_ctx* c, uint64_t frames) {
-    uint64_t want = c->windowFixed ? c->window : std::min<uint64_t>(4096, std::max<uint64_t>(frames, kWindowFloor));
+int ensureWindow(surf_ctx* c, uint64_t frames, uint32_t spp) {
+    const uint64_t passes = frames * spp;
+    uint64_t want = c->windowFixed ? c->window : std::min<uint64_t>(4096, std::max<uint64_t>(passes, kWindowFloor));
+    if (c->windowFixed && c->window % spp != 0)
+        return fail(c, SURF_ERR_INVALID, "frame window " + std::to_string(c->window) + " is not a multiple of samples_per_frame " +
+                                             std::to_string(spp));
     if (!c->windowFixed) {
         uint64_t budget = 32ull << 30;
         size_t freeB = 0, totalB = 0;
         if (hipMemGetInfo(&freeB, &totalB) == hipSuccess && freeB > 0)
             budget = std::min<uint64_t>(budget, (freeB + (c->rad ? (size_t)c->npx * c->window * sizeof(float4) : 0)) / 4);
         want = std::max<uint64_t>(1, std::min<uint64_t>(want, budget / ((uint64_t)c->npx * sizeof(float4))));
+        /* a frame's samples take consecutive slots of one window turn */
+        want = std::max<uint64_t>(spp, want / spp * spp);
+        if ((uint64_t)c->npx * want >= (1ull << 32))
+            return fail(c, SURF_ERR_OOM, "radiance ring of " + std::to_string(want) + " passes exceeds 32-bit sample ids");
+        if (c->rad && want <= c->window && c->window % spp == 0) return SURF_OK;
     }
-    if (c->rad && want <= c->window) return SURF_OK;
+    if (c->rad && want == c->window) return SURF_OK;
     if (c->rad) {
         SURF_CHECK(c, hipStreamSynchronize(c->stream));
         (void)hipFree(c->rad); (void)hipFree(c->frameDone); (void)hipHostFree(c->hFrameDone);
@@ -460,10 +472,12 @@ void launchPhase(surf_ctx* c, int ph, hipEvent_t* ev) {
     if (ovl && ph > 0) (void)hipStreamWaitEvent(s0, c->capEv[2 * (ph - 1) + 1], 0);   /* the previous phase's connect */
     if (c->ldsTables)
         hipLaunchKernelGGL(k_shade<true>, dim3(c->gridWork), dim3(kBlock), 0, s0, c->S, cur, c->pool[par ^ 1],
-                           c->hitTUV, (const uint32_t*)c->hitInst, c->Q, c->rad, c->frameDone, c->npx, c->window, c->ctr, par, order);
+                           c->hitTUV, (const uint32_t*)c->hitInst, c->Q, c->rad, c->frameDone, c->npx, c->window, c->ctr, par, order,
+                           c->cam, geom(c));
     else
         hipLaunchKernelGGL(k_shade<false>, dim3(c->gridWork), dim3(kBlock), 0, s0, c->S, cur, c->pool[par ^ 1],
-                           c->hitTUV, (const uint32_t*)c->hitInst, c->Q, c->rad, c->frameDone, c->npx, c->window, c->ctr, par, order);
+                           c->hitTUV, (const uint32_t*)c->hitInst, c->Q, c->rad, c->frameDone, c->npx, c->window, c->ctr, par, order,
+                           c->cam, geom(c));
     if (ev) (void)hipEventRecord(ev[3], s0);
     if (ovl) {
         (void)hipEventRecord(c->capEv[2 * ph], s0);
@@ -558,12 +572,12 @@ int classifyPixels(surf_ctx* c) {
 }
 
 /* ---- sample stream ------------------------------------------------------ */
-int startStream(surf_ctx* c, uint64_t baseFrame, uint32_t maxSeg, uint32_t frames) {
+int startStream(surf_ctx* c, uint64_t baseFrame, uint32_t maxSeg, uint32_t frames, uint32_t spp) {
     Counters h{};
     for (uint32_t& v : h.capped) v = kUnset;
     /* a multi-frame request that fits the window: its pixels in class order */
     c->permFrames = 0;
-    if (c->reorder && frames >= 2 && frames <= c->window && c->heavyInst.size()) {
+    if (c->reorder && frames >= 2 && (uint64_t)frames * spp <= c->window && c->heavyInst.size()) {
         int rc = classifyPixels(c);
         if (rc) return rc;
         if (c->permA > 0 && c->permA < c->npx) c->permFrames = frames;
@@ -571,7 +585,11 @@ int startStream(surf_ctx* c, uint64_t baseFrame, uint32_t maxSeg, uint32_t frame
     h.permFrames = c->permFrames;
     h.permA = c->permFrames ? c->permA : 0u;
     h.maxSeg = maxSeg;
-    h.zeroCutoff = c->zeroCutoff ? 1u : 0u;
+    /* automatic: on for 1-sample frames (radiance-neutral); off for
+     * multi-sample frames, whose next sample starts from the RNG state the
+     * reference's path ends with -- which an early end would change */
+    h.zeroCutoff = (c->zeroCutoff < 0 ? spp == 1 : c->zeroCutoff != 0) ? 1u : 0u;
+    h.spp = spp;
     h.baseFrame = baseFrame;
     h.survCap = c->survCap;
     *c->hctr = h;
@@ -580,15 +598,19 @@ int startStream(surf_ctx* c, uint64_t baseFrame, uint32_t maxSeg, uint32_t frame
     c->streamActive = true;
     c->baseFrame = baseFrame;
     c->targetFrames = 0;
-    c->accFrames = 0;
+    c->accPasses = 0;
+    c->spp = spp;
     c->streamMaxSeg = maxSeg;
     c->pushedLimit = 0;
     return SURF_OK;
 }
 
+/* Chains (first samples of (frame, pixel)) that may be issued: a frame is
+ * issued only when all its passes fit the window past the accumulated ones. */
 uint64_t issueLimit(const surf_ctx* c) {
-    return std::min<uint64_t>(c->targetFrames, c->accFrames + c->window) * (uint64_t)c->npx;
+    return std::min<uint64_t>(c->targetFrames, (c->accPasses + c->window) / c->spp) * (uint64_t)c->npx;
 }
+uint64_t targetPasses(const surf_ctx* c) { return c->targetFrames * c->spp; }
 
 int pushLimit(surf_ctx* c) {
     const uint64_t lim = issueLimit(c);
@@ -599,7 +621,7 @@ int pushLimit(surf_ctx* c) {
     return SURF_OK;
 }
 
-/* Frames whose every sample is issued after `iss` samples (k_regen's order:
+/* Frames whose every chain is issued after `iss` chains (k_regen's order:
  * the permuted head of permFrames frames, then frame-major). */
 uint64_t fullyIssuedFrames(const surf_ctx* c, uint64_t iss) {
     const uint64_t P = c->permFrames;
@@ -623,14 +645,15 @@ void streamEvents(const Counters& h, unsigned long long out[kEvents]) {
     }
 }
 
-/* Reads counters + per-frame completion (one sync) and accumulates, in frame
- * order, every leading frame whose samples have all finished. */
+/* Reads counters + per-pass completion (one sync) and accumulates, in pass
+ * order, every leading pass whose samples have all finished. */
 int syncAndAccumulate(surf_ctx* c) {
     SURF_CHECK(c, hipMemcpyAsync(c->hctr, c->ctr, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
-    /* completion counts of the open frames only ([accFrames, targetFrames),
+    /* completion counts of the open passes only ([accPasses, targetPasses),
      * at most a window): a strided copy of their slots in each stripe row */
-    const uint64_t open = std::min<uint64_t>(c->targetFrames - std::min(c->accFrames, c->targetFrames), c->window);
-    const uint32_t s0 = (uint32_t)(c->accFrames % c->window);
+    const uint64_t tp = targetPasses(c);
+    const uint64_t open = std::min<uint64_t>(tp - std::min(c->accPasses, tp), c->window);
+    const uint32_t s0 = (uint32_t)(c->accPasses % c->window);
     const uint32_t n0 = (uint32_t)std::min<uint64_t>(open, c->window - s0);
     const size_t pitch = (size_t)c->window * sizeof(uint32_t);
     if (n0)
@@ -640,19 +663,20 @@ int syncAndAccumulate(surf_ctx* c) {
         SURF_CHECK(c, hipMemcpy2DAsync(c->hFrameDone, pitch, c->frameDone, pitch, (open - n0) * sizeof(uint32_t), kStripes,
                                        hipMemcpyDeviceToHost, c->stream));
     SURF_CHECK(c, hipStreamSynchronize(c->stream));
-    /* a frame is complete when all its samples were issued and all finished; a
-     * slot is reused only after its frame is accumulated, so frames beyond the
-     * issued range must not be tested (their slot may still count an older frame) */
-    uint64_t f = c->accFrames;
-    const uint64_t issuedFrames = fullyIssuedFrames(c, c->hctr->issued[0]);
-    while (f < c->targetFrames && f < issuedFrames && framePaths(c, f % c->window) == c->npx) ++f;
-    if (f == c->accFrames) return SURF_OK;
-    const uint32_t count = (uint32_t)(f - c->accFrames);
+    /* a pass is complete when all its samples were issued and all finished; a
+     * slot is reused only after its pass is accumulated, so passes of frames
+     * not yet fully issued must not be tested (their slot may still count an
+     * older pass) */
+    uint64_t f = c->accPasses;
+    const uint64_t issuedPasses = fullyIssuedFrames(c, c->hctr->issued[0]) * c->spp;
+    while (f < tp && f < issuedPasses && framePaths(c, f % c->window) == c->npx) ++f;
+    if (f == c->accPasses) return SURF_OK;
+    const uint32_t count = (uint32_t)(f - c->accPasses);
     const uint32_t threads = std::max<uint32_t>(c->npx, count * kStripes);
     hipLaunchKernelGGL(k_accumulate, dim3((threads + kBlock - 1) / kBlock), dim3(kBlock), 0, c->stream, (const float4*)c->rad,
-                       c->acc, c->npx, (unsigned long long)c->accFrames, count, c->window, c->frameDone);
+                       c->acc, c->npx, (unsigned long long)c->accPasses, count, c->window, c->frameDone);
     SURF_CHECK(c, hipGetLastError());
-    c->accFrames = f;
+    c->accPasses = f;
     return pushLimit(c);
 }
 
@@ -689,10 +713,10 @@ void launchTail(surf_ctx* c, Pool in, uint32_t n, uint32_t lpw, uint32_t firstCo
     const size_t lds = traversalLds(c, 64);
     if (c->ldsTables)
         hipLaunchKernelGGL(k_tail<true>, dim3(blocks), dim3(64), lds, c->stream, c->S, in, n, lpw, c->rad, c->frameDone,
-                           c->npx, c->window, c->ctr, stackWords(c, 64), firstCounted, budget, out);
+                           c->npx, c->window, c->ctr, stackWords(c, 64), firstCounted, budget, out, c->cam, geom(c));
     else
         hipLaunchKernelGGL(k_tail<false>, dim3(blocks), dim3(64), lds, c->stream, c->S, in, n, lpw, c->rad, c->frameDone,
-                           c->npx, c->window, c->ctr, stackWords(c, 64), firstCounted, budget, out);
+                           c->npx, c->window, c->ctr, stackWords(c, 64), firstCounted, budget, out, c->cam, geom(c));
 }
 
 /* Finishes every path of pool 0 (counters at an even phase boundary: pool 0 is
@@ -709,7 +733,9 @@ void launchTail(surf_ctx* c, Pool in, uint32_t n, uint32_t lpw, uint32_t firstCo
 bool waveEligible(const surf_ctx* c) { return c->hasScene && c->stackDepth <= 64 && coopLdsOk(c); }
 /* The four-rows traversal: a single-leaf TLAS with at most one instance per lane of a row, LDS tables. */
 #if SURF_ROWS_ENGINE
-bool rowsEligible(const surf_ctx* c) { return waveEligible(c) && c->coopEligible && c->S.tlasLeafCount <= kRowInst; }
+bool rowsEligible(const surf_ctx* c) {
+    return waveEligible(c) && c->coopEligible && c->S.tlasLeafCount <= kRowInst && rowsLds(c) <= 65536;   /* four record stacks */
+}
 #else
 bool rowsEligible(const surf_ctx*) { return false; }
 #endif
@@ -732,7 +758,7 @@ int runTail(surf_ctx* c) {
             std::fprintf(stderr, "[surf tail] stage %d: %u paths at %.2f ms\n", stage, cnt, ms);
         }
 #if SURF_ROWS_ENGINE
-        if (c->tailRows && rowsEligible(c) && cnt <= c->coopAll) {
+        if (c->tailRows && rowsEligible(c) && c->spp == 1 && cnt <= c->coopAll) {   /* (the rows engine runs 1-sample frames) */
             /* every remaining path through the row queue: as many four-row
              * waves as are resident at once, each row taking the next path
              * when its own ends */
@@ -758,7 +784,7 @@ int runTail(surf_ctx* c) {
             const uint32_t blocks = std::max<uint32_t>(1u, std::min<uint32_t>((cnt + 1u) / 2u, c->cus * (uint32_t)per));
             SURF_CHECK(c, hipMemsetAsync(&c->ctr->rowNext, 0, sizeof(uint32_t), c->stream));
             hipLaunchKernelGGL(kern, dim3(blocks), dim3(128), pairTailLds(c), c->stream, c->S, in, cnt, c->rad, c->frameDone,
-                               c->npx, c->window, c->ctr, recStackWords(c), firstCounted);
+                               c->npx, c->window, c->ctr, recStackWords(c), firstCounted, c->cam, geom(c));
             SURF_CHECK(c, hipGetLastError());
             c->stats.tail_survivors += cnt;
             break;
@@ -769,7 +795,7 @@ int runTail(surf_ctx* c) {
                                             : (w2 ? k_tail_coop<false, true> : k_tail_coop<false, false>),
                                dim3(cnt), dim3(64), coopTailLds(c), c->stream,
                                c->S, in, cnt, c->rad, c->frameDone,
-                               c->npx, c->window, c->ctr, recStackWords(c), firstCounted);
+                               c->npx, c->window, c->ctr, recStackWords(c), firstCounted, c->cam, geom(c));
             SURF_CHECK(c, hipGetLastError());
             c->stats.tail_survivors += cnt;
             break;
@@ -861,15 +887,15 @@ int pump(surf_ctx* c, bool drain) {
         /* in flight at a replay boundary: the pool the next phase extends */
         const uint32_t inflight = c->hctr->nIn[0];
         if (!drain && issued >= target) return SURF_OK;
-        if (drain && c->accFrames >= c->targetFrames) return SURF_OK;
+        if (drain && c->accPasses >= targetPasses(c)) return SURF_OK;
         const bool starved = issued >= c->pushedLimit;     /* nothing more may be issued right now */
-        const uint64_t accBefore = c->accFrames;
+        const uint64_t accBefore = c->accPasses;
         static const bool dbgDrain = std::getenv("SURF_DEBUG_DRAIN") != nullptr;   /* diagnostics: drain timeline */
         if (dbgDrain && starved) {
             static auto tS = std::chrono::steady_clock::now();
-            std::fprintf(stderr, "[surf drain] iteration %llu: %u paths in flight, %llu/%llu frames at %.3f ms\n",
-                         (unsigned long long)c->stats.iterations, inflight, (unsigned long long)c->accFrames,
-                         (unsigned long long)c->targetFrames,
+            std::fprintf(stderr, "[surf drain] iteration %llu: %u paths in flight, %llu/%llu passes at %.3f ms\n",
+                         (unsigned long long)c->stats.iterations, inflight, (unsigned long long)c->accPasses,
+                         (unsigned long long)targetPasses(c),
                          std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tS).count());
         }
         if (starved && inflight > 0 && inflight <= tailThreshold(c)) {
@@ -886,13 +912,13 @@ int pump(surf_ctx* c, bool drain) {
                 if ((rc = advance(c, shortRun))) return rc;
         }
         if ((rc = syncAndAccumulate(c))) return rc;
-        if (starved && inflight == 0 && c->accFrames == accBefore)
+        if (starved && inflight == 0 && c->accPasses == accBefore)
             return fail(c, SURF_ERR_HIP, "sample stream stalled: pool empty but frames incomplete");
     }
 }
 
 int ensureDrained(surf_ctx* c) {
-    if (!c->streamActive || c->accFrames >= c->targetFrames) return SURF_OK;
+    if (!c->streamActive || c->accPasses >= targetPasses(c)) return SURF_OK;
     SURF_CHECK(c, hipSetDevice(c->device));
     if (!c->profiling) {
         int rc = buildGraph(c);
@@ -1059,6 +1085,14 @@ int surf_shard_rows(const surf_ctx* c, uint32_t* rows, uint32_t* count) {
     return SURF_OK;
 }
 
+int surf_shard_row_list(uint32_t height, uint32_t shard, uint32_t shards, uint32_t block, uint32_t* rows, uint32_t* count) {
+    if (!count || shards == 0 || shard >= shards) return fail(nullptr, SURF_ERR_INVALID, "bad shard index");
+    const std::vector<uint32_t> r = shardRows(height, shard, shards, block);
+    if (rows && !r.empty()) std::memcpy(rows, r.data(), r.size() * sizeof(uint32_t));
+    *count = (uint32_t)r.size();
+    return SURF_OK;
+}
+
 int surf_set_pool_capacity(surf_ctx* c, uint32_t paths) {
     if (!c || paths < 64) return SURF_ERR_INVALID;
     if (c->allocated) return fail(c, SURF_ERR_INVALID, "pool capacity is fixed after the first render");
@@ -1134,7 +1168,7 @@ int surf_set_zero_cutoff(surf_ctx* c, int enabled) {
     if (!c) return SURF_ERR_INVALID;
     int rc = endStream(c);
     if (rc) return rc;
-    c->zeroCutoff = enabled != 0;
+    c->zeroCutoff = enabled < 0 ? -1 : (enabled != 0 ? 1 : 0);
     return SURF_OK;
 }
 
@@ -1403,7 +1437,7 @@ int surf_upload_scene(surf_ctx* c, const surf_scene_desc* d) {
      * and of its two children, each in the lanes-as-planes order (lane l of a
      * row = dword planeDword(l) of the 64-B record), 48 floats; a leaf's W holds
      * its own record.  192-B offsets are 32-bit buffer offsets: at most 22.3 M nodes. */
-    static const bool walk2 = !(std::getenv("SURF_WALK2") && std::getenv("SURF_WALK2")[0] == '0');   /* A/B: 0 = one-level walk */
+    const bool walk2 = !(std::getenv("SURF_WALK2") && std::getenv("SURF_WALK2")[0] == '0');   /* A/B: 0 = one-level walk (read per upload) */
     if (walk2 && (uint64_t)d->blas_node_count * 192u < (1ull << 32)) {
         std::vector<float> W((size_t)d->blas_node_count * 48, 0.0f);
         /* lanes 14 / 15 of a row (unused by the wave walk): the row node's two
@@ -1569,9 +1603,9 @@ int surf_set_camera(surf_ctx* c, const surf_camera_ubo* u) {
     return SURF_OK;
 }
 
-int surf_render(surf_ctx* c, uint32_t frames, uint32_t firstFrame, uint32_t maxSeg, uint32_t spp) {
+int surf_render(surf_ctx* c, uint32_t frames, uint32_t firstSample, uint32_t maxSeg, uint32_t spp) {
     if (!c) return SURF_ERR_INVALID;
-    if (spp != 1) return fail(c, SURF_ERR_INVALID, "samples_per_frame must be 1 (render consecutive frames instead)");
+    if (spp == 0 || spp > 4096) return fail(c, SURF_ERR_INVALID, "samples_per_frame must be 1..4096");
     if (!c->hasScene) return fail(c, SURF_ERR_NO_SCENE, "no scene uploaded");
     if (!c->hasCamera) return fail(c, SURF_ERR_NO_SCENE, "no camera set");
     if (frames == 0) return SURF_OK;
@@ -1579,11 +1613,11 @@ int surf_render(surf_ctx* c, uint32_t frames, uint32_t firstFrame, uint32_t maxS
     int rc = allocWavefront(c);
     if (rc) return rc;
     /* continue the open stream only for the next consecutive frames of the same kind */
-    if (c->streamActive && (firstFrame != c->baseFrame + c->targetFrames || maxSeg != c->streamMaxSeg))
+    if (c->streamActive && ((uint64_t)firstSample != c->baseFrame + targetPasses(c) || maxSeg != c->streamMaxSeg || spp != c->spp))
         if ((rc = endStream(c))) return rc;
     if (!c->streamActive) {
-        if ((rc = ensureWindow(c, frames))) return rc;
-        if ((rc = startStream(c, firstFrame, maxSeg, frames))) return rc;
+        if ((rc = ensureWindow(c, frames, spp))) return rc;
+        if ((rc = startStream(c, firstSample, maxSeg, frames, spp))) return rc;
     }
     if (!c->profiling && (rc = buildGraph(c))) return rc;         /* (re)captured if the ring moved */
     SURF_CHECK(c, hipEventRecord(c->ev0, c->stream));
@@ -1594,8 +1628,8 @@ int surf_render(surf_ctx* c, uint32_t frames, uint32_t firstFrame, uint32_t maxS
     float ms = 0;
     (void)hipEventElapsedTime(&ms, c->ev0, c->ev1);
     c->stats.ms_total += ms;
-    c->totalSamples += frames;
-    c->stats.samples += (uint64_t)frames * c->npx;
+    c->totalSamples += (uint64_t)frames * spp;
+    c->stats.samples += (uint64_t)frames * spp * c->npx;
     return SURF_OK;
 }
 
@@ -1810,6 +1844,19 @@ int surf_debug_segment_cycles(surf_ctx* c, const float* path12, uint32_t reps, u
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     (void)hipFree(d);
     if (e != hipSuccess) return fail(c, SURF_ERR_HIP, std::string("segment cycles: ") + hipGetErrorString(e));
+    return SURF_OK;
+}
+
+int surf_pack_rgba8(const float* acc, uint32_t n, float inv, int display, uint32_t* out) {
+    if ((n && (!acc || !out))) return fail(nullptr, SURF_ERR_INVALID, "bad arguments");
+    for (uint32_t p = 0; p < n; ++p) {
+        uint32_t w = 0;
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t c8 = packChannel((acc[4 * (size_t)p + k] * inv) * 255.0f);
+            w |= (display ? displayChannel(c8) : c8) << (8 * k);
+        }
+        out[p] = w;
+    }
     return SURF_OK;
 }
 

@@ -6,7 +6,9 @@
  * application builds them, with RenderContext holding a HIP device instead of
  * a Vulkan context and no UIManager.
  *
- * usage: render_indoor ASSETS_DIR WIDTH HEIGHT FRAMES OUT.(ppm|png) [--lumen]
+ * usage: render_indoor ASSETS_DIR WIDTH HEIGHT FRAMES OUT.(ppm|png) [--lumen] [--spp N]
+ * (--spp: config().samplesPerFrame, the UI's 1..24 slider, ui_manager.cpp:103 /
+ * main.cpp:415; a frame's samples continue one RNG stream, renderer.cpp:169-181)
  * Prints the reference's per-frame line (ms, Mrays/s, samples, Lumen; the
  * energy only with --lumen, the reference's WF_LUMEN_OUTPUT, which drains the
  * stream every frame), then one JSON line with the loop's wall time including
@@ -15,10 +17,12 @@
  * channel (displayRGBA8), as PPM or PNG by extension.
  */
 #include "surf/surf_host.hpp"
+#include "indoor_scene.hpp"
 
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <algorithm>
 #include <cstdlib>
 #include <memory>
 #include <string>
@@ -28,51 +32,28 @@ using namespace surf;
 
 int main(int argc, char** argv) {
     if (argc < 6) {
-        std::fprintf(stderr, "usage: %s ASSETS_DIR WIDTH HEIGHT FRAMES OUT.(ppm|png)\n", argv[0]);
+        std::fprintf(stderr, "usage: %s ASSETS_DIR WIDTH HEIGHT FRAMES OUT.(ppm|png) [--lumen] [--spp N]\n", argv[0]);
         return 2;
     }
     const std::string dir = argv[1];
     const U32 W = (U32)std::atoi(argv[2]), H = (U32)std::atoi(argv[3]), frames = (U32)std::atoi(argv[4]);
+    bool lumen = false;
+    U32 spp = 1;
+    for (int a = 6; a < argc; ++a) {
+        const std::string opt = argv[a];
+        if (opt == "--lumen") lumen = true;
+        else if (opt == "--spp" && a + 1 < argc) spp = (U32)std::max(1, std::atoi(argv[++a]));
+        else { std::fprintf(stderr, "unknown option %s\n", opt.c_str()); return 2; }
+    }
     try {
         RenderContext context;            /* HIP device 0 */
-        Camera worldCam(Float3(0.0f, 0.0f, -7.0f), Float3(0.0f, 0.0f, 0.0f), W, H, 70.0f, 7.0f, 0.5f);
+        Camera worldCam = indoorCamera(W, H);
+        IndoorScene indoor(&context, dir);          /* main.cpp:161-346 */
+        GPUScene& scene = *indoor.scene;
 
-        /* main.cpp:161-346 */
-        Mesh susanneMesh(dir + "/susanne.obj"), cubeMesh(dir + "/cube.obj"), lensMesh(dir + "/lens.obj"), planeMesh(dir + "/plane.obj");
-        BvhBLAS susanneBlas(&susanneMesh), cubeBlas(&cubeMesh), lensBlas(&lensMesh), planeBlas(&planeMesh);
-
-        Material floorMat; floorMat.albedo = Float3(0.8f); floorMat.reflectivity = 0.01f;
-        Material wallRed; wallRed.albedo = Float3(1.0f, 0.0f, 0.0f);
-        Material wallGreen; wallGreen.albedo = Float3(0.0f, 1.0f, 0.0f);
-        Material diffuseMat; diffuseMat.albedo = Float3(1.0f, 0.0f, 0.0f);
-        Material dielectricMat; dielectricMat.albedo = Float3(0.7f, 0.7f, 0.2f); dielectricMat.absorption = Float3(0.03f, 0.04f, 0.03f);
-        dielectricMat.refractivity = 1.0f; dielectricMat.indexOfRefraction = 1.42f;
-        Material specularMat; specularMat.albedo = Float3(0.2f, 0.9f, 1.0f); specularMat.reflectivity = 0.8f;
-        Material softLight; softLight.emissionColor = Float3(1.0f, 0.8f, 0.6f); softLight.emissionStrength = 5.0f;
-        Material redLight; redLight.emissionColor = Float3(1.0f, 0.5f, 0.2f); redLight.emissionStrength = 5.0f;
-
-        const Mat4 I(1.0f);
-        std::vector<Instance> instances;
-        instances.emplace_back(&planeBlas, &floorMat, scale(translate(I, Float3(0.0f, -1.0f, 0.0f)), Float3(10.0f, 10.0f, 10.0f)));
-        instances.emplace_back(&cubeBlas, &softLight, scale(translate(I, Float3(-8.0f, 7.0f, 5.0f)), Float3(0.5f, 0.5f, 0.5f)));
-        instances.emplace_back(&cubeBlas, &redLight, scale(translate(I, Float3(9.0f, 5.0f, -5.0f)), Float3(1.0f, 1.0f, 1.0f)));
-        instances.emplace_back(&susanneBlas, &diffuseMat, translate(I, Float3(0.0f, 0.0f, -1.0f)));
-        instances.emplace_back(&susanneBlas, &specularMat, translate(I, Float3(3.0f, 0.0f, -1.0f)));
-        instances.emplace_back(&lensBlas, &dielectricMat, translate(I, Float3(-3.0f, 0.0f, -1.0f)));
-        instances.emplace_back(&planeBlas, &wallRed, scale(rotate(translate(I, Float3(-10.0f, 4.0f, 0.0f)), radians(90.0f), WORLD_FORWARD), Float3(5.0f, 10.0f, 10.0f)));
-        instances.emplace_back(&planeBlas, &wallGreen, scale(rotate(translate(I, Float3(10.0f, 4.0f, 0.0f)), radians(90.0f), WORLD_FORWARD), Float3(5.0f, 10.0f, 10.0f)));
-        instances.emplace_back(&planeBlas, &floorMat, scale(translate(I, Float3(0.0f, 9.0f, 0.0f)), Float3(10.0f, 10.0f, 10.0f)));
-        instances.emplace_back(&planeBlas, &floorMat, scale(rotate(translate(I, Float3(0.0f, 4.0f, -10.0f)), radians(90.0f), WORLD_RIGHT), Float3(10.0f, 10.0f, 5.0f)));
-        instances.emplace_back(&planeBlas, &floorMat, scale(rotate(translate(I, Float3(0.0f, 4.0f, 10.0f)), radians(90.0f), WORLD_RIGHT), Float3(10.0f, 10.0f, 5.0f)));
-
-        SceneBackground background;
-        background.type = BackgroundType::ColorGradient;
-        background.gradient.colorA = Float3(0.8f, 0.8f, 0.8f);
-        background.gradient.colorB = Float3(0.1f, 0.4f, 0.6f);
-        GPUScene scene(&context, background, instances);
-
-        RendererConfig config;            /* samplesPerFrame 1 (ui_manager.h:26), unbounded + RR */
-        config.lumenOutput = argc > 6 && std::string(argv[6]) == "--lumen";
+        RendererConfig config;            /* samplesPerFrame 1 (ui_manager.h:26) unless --spp, unbounded + RR */
+        config.samplesPerFrame = spp;
+        config.lumenOutput = lumen;
         WaveFrontRenderer renderer(&context, nullptr, config, FramebufferSize{W, H}, worldCam, scene);
 
         const auto tLoop = std::chrono::steady_clock::now();
@@ -96,8 +77,9 @@ int main(int argc, char** argv) {
 
         renderer.synchronize();           /* every frame accumulated */
         const double loopMs = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tLoop).count();
-        std::printf("{\"frames\": %u, \"width\": %u, \"height\": %u, \"loop_ms\": %.3f, \"mrays_per_s\": %.3f, \"lumen_output\": %s}\n",
-                    frames, W, H, loopMs, (double)W * H * frames / loopMs / 1000.0, config.lumenOutput ? "true" : "false");
+        std::printf("{\"frames\": %u, \"samples_per_frame\": %u, \"width\": %u, \"height\": %u, \"loop_ms\": %.3f, \"mrays_per_s\": %.3f, "
+                    "\"lumen_output\": %s}\n",
+                    frames, spp, W, H, loopMs, (double)W * H * frames * spp / loopMs / 1000.0, config.lumenOutput ? "true" : "false");
         const std::vector<U32> img = renderer.displayRGBA8();
         const std::string path = argv[5];
         const bool png = path.size() > 4 && path.compare(path.size() - 4, 4, ".png") == 0;

@@ -7,7 +7,7 @@ to anything: if the library is missing, `load()` raises.
 Mirrors the reference interface for the hot path:
   Scene.indoor(...)            main.cpp:161-346 scene (Mesh/BvhBLAS/Instance/GPUScene)
   Renderer(...)                WaveFrontRenderer (renderer.h:207-436)
-    .render(frames, first)     render loop, one sample per pixel per frame
+    .render(frames, first, spp=) render loop: frames of spp samples per pixel (Renderer::render)
     .clear_accumulator()       IRenderer::clearAccumulator
     .accumulator()             float RGBA accumulator (rows of this shard)
     .finalize_rgba8()          wavefront_finalize.comp + RgbaToU32
@@ -23,6 +23,7 @@ import numpy as np
 
 _PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(_PKG, "lib", "libsurf_hip.so")
+MGPU_LIB_PATH = os.path.join(_PKG, "lib", "libsurf_mgpu.so")
 REPO_ROOT = os.path.dirname(_PKG)
 ASSETS_DIR = os.path.join(REPO_ROOT, "assets")
 
@@ -95,6 +96,8 @@ def load() -> C.CDLL:
         "surf_create_sharded": ([I32, U32, U32, U32, U32, U32, C.POINTER(P)], I32),
         "surf_destroy": ([P], None), "surf_last_error": ([P], C.c_char_p),
         "surf_shard_rows": ([P, P, C.POINTER(U32)], I32),
+        "surf_shard_row_list": ([U32, U32, U32, U32, P, C.POINTER(U32)], I32),
+        "surf_pack_rgba8": ([P, U32, F, I32, P], I32),
         "surf_set_pool_capacity": ([P, U32], I32), "surf_set_frame_batch": ([P, U32], I32),
         "surf_set_profiling": ([P, I32], I32), "surf_set_zero_cutoff": ([P, I32], I32), "surf_set_trace_mode": ([P, I32], I32), "surf_set_tail_policy": ([P, U32, U32, U32], I32), "surf_set_tail_coop": ([P, U32], I32),
         "surf_debug_capped": ([P, P, U32, C.POINTER(C.c_uint64)], I32),
@@ -128,6 +131,59 @@ def load() -> C.CDLL:
         fn.restype = res
     _lib = lib
     return lib
+
+
+_mgpu = None
+
+
+def load_mgpu() -> C.CDLL:
+    """Loads libsurf_mgpu.so (include/surf_mgpu.h: the RCCL gather and the row
+    un-permute of a multi-GPU render); raises if it has not been built."""
+    global _mgpu
+    if _mgpu is not None:
+        return _mgpu
+    load()
+    if not os.path.exists(MGPU_LIB_PATH):
+        raise FileNotFoundError(f"{MGPU_LIB_PATH} not built: run `make -C surf-path-tracer_amd`")
+    lib = C.CDLL(MGPU_LIB_PATH)
+    P, U32, I32 = C.c_void_p, C.c_uint32, C.c_int
+    sig = {
+        "surf_mgpu_unique_id": ([P], I32),
+        "surf_mgpu_create": ([P, U32, U32, U32, U32, U32, P, C.POINTER(P)], I32),
+        "surf_mgpu_create_all": ([P, U32, U32, U32, U32, P], I32),
+        "surf_mgpu_gather": ([P, P], I32), "surf_mgpu_gather_all": ([P, U32, P], I32),
+        "surf_mgpu_destroy": ([P], None), "surf_mgpu_last_error": ([], C.c_char_p),
+        "surf_mgpu_assemble": ([U32, U32, U32, U32, P, U32, P], I32),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    _mgpu = lib
+    return lib
+
+
+def assemble_slabs(width: int, height: int, shards: int, row_block: int, gathered: np.ndarray) -> np.ndarray:
+    """The root's row un-permute of a multi-GPU gather, by libsurf_mgpu's native
+    code (surf_mgpu_assemble): gathered is (shards, rows_per_slab, W, 4) float32,
+    slab k holding shard k's rows in shard order (padding rows ignored)."""
+    g = np.ascontiguousarray(gathered, dtype=np.float32)
+    if g.ndim != 4 or g.shape[0] != shards or g.shape[2] != width or g.shape[3] != 4:
+        raise ValueError(f"gathered shape {g.shape} is not ({shards}, rows, {width}, 4)")
+    out = np.zeros((height, width, 4), np.float32)
+    rc = load_mgpu().surf_mgpu_assemble(width, height, shards, row_block, g.ctypes.data, g.shape[1], out.ctypes.data)
+    if rc != SURF_OK:
+        raise SurfError(rc, "surf_mgpu_assemble", load_mgpu().surf_mgpu_last_error().decode())
+    return out
+
+
+def pack_rgba8(acc: np.ndarray, samples: int, display: bool = False) -> np.ndarray:
+    """surf_finalize_rgba8 / surf_display_rgba8 of a host accumulator (surf_pack_rgba8)."""
+    a = np.ascontiguousarray(acc, dtype=np.float32).reshape(-1, 4)
+    out = np.zeros(len(a), np.uint32)
+    _check(load().surf_pack_rgba8(a.ctypes.data, len(a), np.float32(1.0) / np.float32(samples), 1 if display else 0,
+                                  out.ctypes.data), "surf_pack_rgba8")
+    return out
 
 
 def _check(rc: int, what: str, ctx=None):
@@ -335,8 +391,9 @@ class Renderer:
                  "leaf_cycles", "walks", "leaves", "triangles", "visits2", "prologue_cycles", "instance_loop_cycles")
         return {k: float(out[i]) / reps for i, k in enumerate(names) if k != "checksum"}
 
-    def set_zero_cutoff(self, on: bool):
-        _check(load().surf_set_zero_cutoff(self._h, 1 if on else 0), "surf_set_zero_cutoff", self._h)
+    def set_zero_cutoff(self, on):
+        """True / False, or None for the automatic default (on for 1-sample frames, off for multi-sample frames)."""
+        _check(load().surf_set_zero_cutoff(self._h, -1 if on is None else (1 if on else 0)), "surf_set_zero_cutoff", self._h)
 
     def update_instances(self, scene: Scene):
         """Re-uploads the scene's instance records, TLAS and lights (after Scene.update)."""
@@ -362,8 +419,13 @@ class Renderer:
     def set_profiling(self, on: bool):
         _check(load().surf_set_profiling(self._h, 1 if on else 0), "surf_set_profiling", self._h)
 
-    def render(self, frames: int, first_frame: int = 0, max_segments: int = 0):
-        _check(load().surf_render(self._h, frames, first_frame, max_segments, 1), "surf_render", self._h)
+    def render(self, frames: int, first_frame: int = 0, max_segments: int = 0, spp: int = 1):
+        """`frames` frames of `spp` samples per pixel (Renderer::render with
+        samplesPerFrame = spp, renderer.cpp:160-188): first_frame is the sample
+        count before the call (the reference's totalSamples; the frame index for
+        spp 1); frame k is seeded from first_frame + k * spp and its samples
+        chain their RNG state."""
+        _check(load().surf_render(self._h, frames, first_frame, max_segments, spp), "surf_render", self._h)
 
     def synchronize(self):
         _check(load().surf_synchronize(self._h), "surf_synchronize", self._h)

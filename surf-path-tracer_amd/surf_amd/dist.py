@@ -11,7 +11,7 @@ from __future__ import annotations
 
 import numpy as np
 
-from . import ShardSpec, shard_rows
+from . import ShardSpec, assemble_slabs, shard_rows
 
 
 class RowGather:
@@ -20,6 +20,7 @@ class RowGather:
     def __init__(self, width: int, height: int, world: int, rank: int, row_block: int, device, dst: int = 0):
         import torch
         self.width, self.height, self.world, self.rank, self.dst = width, height, world, rank, dst
+        self.row_block = row_block
         self.specs = [ShardSpec(r, world, row_block) for r in range(world)]
         self.rows = [len(shard_rows(height, s)) for s in self.specs]
         self.max_rows = max(self.rows)
@@ -36,10 +37,11 @@ class RowGather:
         dist.gather(self.send, self.recv, dst=self.dst)
 
     def assemble(self) -> np.ndarray:
-        """Full (H, W, 4) frame on the destination rank (rows un-permuted)."""
+        """Full (H, W, 4) frame on the destination rank: the gathered slabs
+        un-permuted by libsurf_mgpu's native code (surf_mgpu_assemble, the same
+        un-permute a C++ application's surf_mgpu_gather runs)."""
         if self.recv is None:
             raise RuntimeError("assemble() is only valid on the destination rank")
-        full = np.zeros((self.height, self.width, 4), dtype=np.float32)
-        for r, spec in enumerate(self.specs):
-            full[shard_rows(self.height, spec)] = self.recv[r][: self.rows[r]].cpu().numpy()
-        return full
+        import torch
+        slabs = torch.stack([r.cpu() for r in self.recv]).numpy()
+        return assemble_slabs(self.width, self.height, self.world, self.row_block, slabs)

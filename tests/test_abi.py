@@ -1,4 +1,5 @@
-"""The C-ABI library loads and exports every symbol include/surf_hip.h declares
+"""The C-ABI libraries load and export every symbol their headers declare:
+include/surf_hip.h (libsurf_hip.so) and include/surf_mgpu.h (libsurf_mgpu.so)
 (no compute calls: this runs without a GPU)."""
 import os
 import re
@@ -7,10 +8,11 @@ import subprocess
 import surf_amd
 
 HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "surf_hip.h")
+MGPU_HEADER = os.path.join(os.path.dirname(HEADER), "surf_mgpu.h")
 
 
-def declared_functions():
-    text = open(HEADER).read()
+def declared_functions(header=HEADER):
+    text = open(header).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     return sorted(set(re.findall(r"\b(surf_[a-z0-9_]+)\s*\(", text)))
 
@@ -52,3 +54,18 @@ def test_errors_are_returned_not_raised():
     assert lib.surf_create(0, 0, 0, 0, 0, C.byref(h)) == -1
     assert lib.surf_render(None, 1, 0, 0, 1) == -1
     assert lib.surf_scene_build_indoor(b"/nonexistent", 0, C.byref(h)) == -6
+
+
+def test_mgpu_library_exports_every_declared_symbol():
+    lib = surf_amd.load_mgpu()
+    fns = declared_functions(MGPU_HEADER)
+    assert "surf_mgpu_gather" in fns and "surf_mgpu_create_all" in fns
+    missing = [f for f in fns if not hasattr(lib, f)]
+    assert not missing, missing
+    out = subprocess.run(["nm", "-D", "--defined-only", surf_amd.MGPU_LIB_PATH], capture_output=True, text=True, check=True).stdout
+    syms = {line.split()[-1] for line in out.splitlines() if line.strip()}
+    assert all(f in syms for f in fns)
+    # the gather is RCCL's (rccl.h:745); the render library itself stays RCCL-free
+    deps = subprocess.run(["ldd", surf_amd.MGPU_LIB_PATH], capture_output=True, text=True).stdout
+    assert "librccl" in deps
+    assert "librccl" not in subprocess.run(["ldd", surf_amd.LIB_PATH], capture_output=True, text=True).stdout

@@ -257,6 +257,80 @@ def test_issue_order_keys_overlap_bitexact(oracle_scene, product_scene, reorder,
     r.close()
 
 
+@pytest.mark.parametrize("cutoff", [None, True], ids=["reference-no-cutoff", "cutoff-on-both"])
+def test_render_spp4_per_frame_bitexact(oracle_scene, product_scene, cutoff):
+    """Multi-sample frames (config().samplesPerFrame = 4; renderer.cpp:160-188):
+    frame f is seeded once per pixel from the running sample count 4f, and its
+    four samples run in sequence, each drawing jitter, lens sample and path from
+    the RNG state the previous sample's path left.  96x64, 3 frames: the GPU
+    (sample chains continued by k_shade and the drain) equals the oracle bit for
+    bit with equal event counts -- in reference semantics (the automatic
+    default: no throughput cutoff for multi-sample frames) and with the cutoff
+    on both sides."""
+    W, H, F, K = 96, 64, 3, 4
+    r = surf_amd.Renderer(product_scene, W, H)
+    if cutoff is not None:
+        r.set_zero_cutoff(cutoff)
+    r.render(F, 0, 0, spp=K)
+    g = r.accumulator()
+    st = r.stats()
+    r.close()
+    assert np.all(g[..., 3] == F * K) and st["samples"] == W * H * F * K
+    oracle.set_zero_cutoff(bool(cutoff))
+    try:
+        c, cnt, _ = oracle_scene.render(W, H, F, spp=K)
+        one, _, _ = oracle_scene.render(W, H, F * K)
+    finally:
+        oracle.set_zero_cutoff(False)
+    _assert_bitexact(g, c, f"{F} frames x {K} samples, cutoff {cutoff}")
+    _assert_counts(st, cnt)
+    assert not np.array_equal(c.view(np.uint32), one.view(np.uint32)), "chained samples must differ from 1-spp frames"
+
+
+@pytest.mark.parametrize("policy,coop,engine", [((1 << 30, 0, 8), 1 << 30, "pair"), ((1 << 30, 0, 8), 1 << 30, "coop"),
+                                                ((0, 8, 4), 0, "lanes"), ((1, 0, 0), 0, "lanes")],
+                         ids=["pair-from-start", "coop-from-start", "8-lanes-staged", "wavefront-to-end"])
+def test_spp_chains_through_drain_bitexact(oracle_scene, product_scene, policy, coop, engine, monkeypatch):
+    """A frame's sample chain continued inside every drain engine (the next
+    camera sample drawn on the lane or wave that ended the previous one), and
+    the drop-in loop (one frame of 3 samples per render() call, each call's
+    first sample index the running count): equal to the oracle bit for bit."""
+    monkeypatch.setenv("SURF_TAIL_PAIR", "0" if engine == "coop" else "1")
+    W, H, F, K = 64, 48, 4, 3
+    r = surf_amd.Renderer(product_scene, W, H, pool_capacity=4096)
+    r.set_tail_policy(*policy)
+    r.set_tail_coop(coop)
+    r.render(F, 0, 0, spp=K)
+    g = r.accumulator()
+    st = r.stats()
+    r.clear_accumulator()
+    for f in range(F):                    # main.cpp's loop: render() per frame
+        r.render(1, f * K, 0, spp=K)
+    g2 = r.accumulator()
+    r.close()
+    c, cnt, _ = oracle_scene.render(W, H, F, spp=K)
+    _assert_bitexact(g, c, f"spp {K} drain {engine} {policy}")
+    _assert_counts(st, cnt)
+    _assert_bitexact(g2, c, f"spp {K} one frame per call, drain {engine}")
+
+
+def test_spp_window_and_offset_bitexact(oracle_scene, product_scene):
+    """Multi-sample frames through a radiance window of two frames (6 passes,
+    frame_batch a multiple of spp) and from a sample offset (first sample index
+    7, as after 7 earlier samples): the window's slot reuse and the seeds."""
+    W, H, K = 48, 40, 3
+    r = surf_amd.Renderer(product_scene, W, H, pool_capacity=2048, frame_batch=2 * K)
+    r.render(5, 7, 0, spp=K)
+    g = r.accumulator()
+    r.close()
+    c, _, _ = oracle_scene.render(W, H, 5, first_frame=7, spp=K)
+    _assert_bitexact(g, c, "5 frames x 3 samples from sample 7 through a 6-pass window")
+    bad = surf_amd.Renderer(product_scene, W, H, frame_batch=4)
+    with pytest.raises(surf_amd.SurfError):
+        bad.render(2, 0, 0, spp=3)        # a window of 4 passes cannot hold whole 3-sample frames
+    bad.close()
+
+
 def test_render_c1_256x256x16_bitexact(oracle_scene, product_scene):
     g, c, stats, cnt, _ = _render_both(oracle_scene, product_scene, 256, 256, 16)
     _assert_bitexact(g, c, "C1 256x256x16")
