@@ -332,16 +332,31 @@ def main():
         r.set_profiling(False)
         launches = max(pe["launches_extend"], 1)
         rays_per_launch = pe["n_ext_wavefront"] / launches
+        avg_ms = pe["ms_extend"] / launches
+        per_rank = None
+        if dist_on:
+            # every rank profiles its own shard; the line reports the slowest
+            # rank's k_extend (the one the max-over-ranks clock waits for)
+            t = torch.zeros((world, 3), dtype=torch.float64, device=coll_dev)
+            t[rank] = torch.tensor([avg_ms, rays_per_launch, launches], dtype=torch.float64)
+            dist.all_reduce(t)
+            per_rank = t.cpu().tolist()
+            slow = max(range(world), key=lambda k: per_rank[k][0])
+            avg_ms, rays_per_launch, launches = per_rank[slow][0], per_rank[slow][1], per_rank[slow][2]
         bytes_per_ray = EXTEND_BYTES_PER_RAY + (C5_SCENE_BYTES_PER_RAY if wl["scene"] == "c5" else 0.0)
         bytes_per_launch = bytes_per_ray * rays_per_launch
-        avg_ms = pe["ms_extend"] / launches
         achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
         roof = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
-                "kernel": "k_extend", "avg_launch_ms": round(avg_ms, 5), "launches": int(pe["launches_extend"]),
+                "kernel": "k_extend", "avg_launch_ms": round(avg_ms, 5), "launches": int(launches),
                 "rays_per_launch": round(rays_per_launch, 1), "bytes_per_ray": round(bytes_per_ray, 1),
                 "algorithmic_bytes_per_launch": round(bytes_per_launch, 1)}
-        rp = rocprof_summary(args.workload)
+        if per_rank:
+            roof["rank"] = slow
+            roof["per_rank_avg_launch_ms"] = [round(x[0], 5) for x in per_rank]
+        # the committed rocprof/PMC summary is of the one-GPU command: an N > 1
+        # line carries no traffic of its own (its ranks' kernels are not profiled)
+        rp = rocprof_summary(args.workload) if not dist_on else None
         if rp:
             roof["traffic"] = round(rp["traffic"]) if rp["traffic"] else None
             roof["rocprof"] = {"source": rp["source"], "avg_launch_ms": rp["avg_launch_ms"],

@@ -1912,6 +1912,21 @@ __device__ __forceinline__ void addRadiance(float4* rad, uint32_t sid, V3 c) {
     r.x = r.x + c.x; r.y = r.y + c.y; r.z = r.z + c.z;
     rad[sid] = r;
 }
+/* The drain kernels keep the radiance of the sample they run in registers:
+ * loaded once when the path is taken (what the wavefront phases added before
+ * the hand-over), each contribution added in the reference's order
+ * (renderer.cpp:415-444, the same float adds addRadiance makes), stored once
+ * when the sample ends or leaves the kernel -- instead of a dependent global
+ * read-modify-write on the path's chain every segment. */
+__device__ __forceinline__ V3 loadRadiance(const float4* rad, uint32_t sid) { return xyz(rad[sid]); }
+__device__ __forceinline__ void storeRadiance(float4* rad, uint32_t sid, V3 e) { rad[sid] = make_float4(e.x, e.y, e.z, 0.0f); }
+/* One-path-per-wave kernels: the running sum is wave-uniform; kept in SGPRs
+ * (readfirstlane after each add) so it costs no VGPRs across the walks. */
+__device__ __forceinline__ float sgprF(float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); }
+__device__ __forceinline__ V3 addU(V3 e, V3 c) {
+    const V3 t = add(e, c);
+    return mk3(sgprF(t.x), sgprF(t.y), sgprF(t.z));
+}
 
 /* Result of shading one hit: what the path does next. */
 struct ShadeOut {
@@ -2397,6 +2412,7 @@ __device__ __forceinline__ bool runPath(const DevScene& S, const TraceTables& Tt
     uint32_t slot = f2u(o4.w) / npx;
     uint32_t nExt = 0, nHit = 0, nCont = 0, nSh = 0, nAcc = 0, nUn = 0, nDone = 0;   /* per path: 32 bits suffice */
     bool done = true;
+    V3 E = loadRadiance(rad, f2u(o4.w));
     for (;;) {
         float depth = kFarAway, u = 0.0f, v = 0.0f;
         uint32_t inst = kUnset, prim = kUnset;
@@ -2404,14 +2420,14 @@ __device__ __forceinline__ bool runPath(const DevScene& S, const TraceTables& Tt
         ++nExt;
         ShadeOut r;
         shadePath(S, Tb, o4, d4, T4, make_float4(depth, u, v, u2f(prim)), hit ? inst : kUnset, maxSeg, zeroCutoff, r);
-        if (r.addRad) addRadiance(rad, f2u(o4.w), r.radd);
+        if (r.addRad) E = add(E, r.radd);
         nHit += r.hitGeom; nAcc += r.accd;
         if (r.shadow) {
             ++nSh;
             float sdep = r.so.w, su = 0.0f, sv = 0.0f;
             uint32_t si = kUnset, sp = kUnset;
             if (!traceScene<true>(S, Tt, xyz(r.so), xyz(r.sd), sdep, su, sv, si, sp, stk, stride)) {
-                addRadiance(rad, f2u(r.sd.w), xyz(r.sc));
+                E = add(E, xyz(r.sc));
                 ++nUn; ++nAcc;
             }
         }
@@ -2420,17 +2436,19 @@ __device__ __forceinline__ bool runPath(const DevScene& S, const TraceTables& Tt
         }
         if (!r.cont) {
             atomicMax(&C->segMax, r.seg);
+            storeRadiance(rad, f2u(o4.w), E);
             __threadfence();      /* radiance before completion: other streams' kernels read it */
             atomicAdd(&frameDone[st * window + slot], 1u);
             ++nDone;
             /* the frame's next sample of this pixel continues on this lane */
-            if (chainNext(cam, G, spp, f2u(o4.w), slot, r.seedOut, o4, d4, T4)) { ++slot; continue; }
+            if (chainNext(cam, G, spp, f2u(o4.w), slot, r.seedOut, o4, d4, T4)) { ++slot; E = mk3(0.0f, 0.0f, 0.0f); continue; }
             break;
         }
         ++nCont;
         if (budget != 0u && nExt >= budget) {
             const uint32_t k = atomicAdd(sink.n, 1u);
             if (k < sink.cap) {
+                storeRadiance(rad, f2u(o4.w), E);          /* the next stage reloads it */
                 sink.q.od[2u * (k)] = r.o; sink.q.od[2u * (k) + 1u] = r.d; sink.q.T[k] = r.T;
                 done = false;
                 break;
@@ -2501,6 +2519,7 @@ __global__ __launch_bounds__(64, SURF_COOP_WAVES) void k_tail_coop(DevScene S, P
     const uint32_t st = blockIdx.x % kStripes;
     float4 o4 = cur.od[2u * (i)], d4 = cur.od[2u * (i) + 1u], T4 = cur.T[i];
     uint32_t slot = f2u(o4.w) / npx;
+    V3 E = loadRadiance(rad, __builtin_amdgcn_readfirstlane(f2u(o4.w)));            /* the running sample's radiance */
     unsigned long long nExt = 0, nHit = 0, nCont = 0, nSh = 0, nAcc = 0, nUn = 0, nDone = 0;
 #if SURF_DRAIN_TRACE
     const unsigned long long tStart = wall_clock64();
@@ -2528,7 +2547,7 @@ __global__ __launch_bounds__(64, SURF_COOP_WAVES) void k_tail_coop(DevScene S, P
         const unsigned long long c1 = segClock();
 #endif
         shadePath<true>(S, Tb, o4, d4, T4, make_float4(depth, u, v, u2f(prim)), hit ? inst : kUnset, maxSeg, zeroCutoff, r);
-        if (lead && r.addRad) addRadiance(rad, f2u(o4.w), r.radd);
+        if (r.addRad) E = addU(E, r.radd);
 #if SURF_SEG_TIMING
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         const unsigned long long c2 = segClock();
@@ -2540,7 +2559,7 @@ __global__ __launch_bounds__(64, SURF_COOP_WAVES) void k_tail_coop(DevScene S, P
             uint32_t si = kUnset, sp = kUnset;
             const bool occ = traceWave<true, W2>(S, Tt, xyz(r.so), xyz(r.sd), sdep, su, sv, si, sp, rstk, pro);
             if (!occ) {
-                if (lead) addRadiance(rad, f2u(r.sd.w), xyz(r.sc));
+                E = addU(E, xyz(r.sc));
                 ++nUn; ++nAcc;
             }
         }
@@ -2555,12 +2574,13 @@ __global__ __launch_bounds__(64, SURF_COOP_WAVES) void k_tail_coop(DevScene S, P
         if (!r.cont) {
             if (lead) {
                 atomicMax(&C->segMax, r.seg);
+                storeRadiance(rad, __builtin_amdgcn_readfirstlane(f2u(o4.w)), E);   /* (uniform: an SGPR address) */
                 __threadfence();      /* radiance before completion */
                 atomicAdd(&frameDone[st * window + slot], 1u);
             }
             ++nDone;
             /* the frame's next sample of this pixel continues on this wave */
-            if (chainNext(cam, G, spp, f2u(o4.w), slot, r.seedOut, o4, d4, T4)) { ++slot; continue; }
+            if (chainNext(cam, G, spp, f2u(o4.w), slot, r.seedOut, o4, d4, T4)) { ++slot; E = mk3(0.0f, 0.0f, 0.0f); continue; }
             break;
         }
         ++nCont;
@@ -2625,6 +2645,7 @@ __device__ __forceinline__ void pairPath(const DevScene& S, const TraceTables& T
     const uint32_t maxSeg = C->maxSeg, zeroCutoff = C->zeroCutoff, spp = C->spp;
     uint32_t slot = f2u(o4.w) / npx;
     bool pend = false;                     /* a posted shadow ray awaits its answer */
+    V3 E = loadRadiance(rad, __builtin_amdgcn_readfirstlane(f2u(o4.w)));   /* the running sample's radiance */
     for (;;) {
         float depth = kFarAway, u = 0.0f, v = 0.0f;
         uint32_t inst = kUnset, prim = kUnset;
@@ -2633,14 +2654,14 @@ __device__ __forceinline__ void pairPath(const DevScene& S, const TraceTables& T
         if (pend) {
             while (ldsLoadAcq(&box.done[w]) != posted) __builtin_amdgcn_s_sleep(1);
             if (!box.occ[w]) {
-                if (lead) addRadiance(rad, f2u(box.sd[w].w), xyz(box.sc[w]));
+                E = addU(E, xyz(box.sc[w]));
                 ++pc.un; ++pc.acc;
             }
             pend = false;
         }
         ShadeOut r;
         shadePath<true>(S, Tb, o4, d4, T4, make_float4(depth, u, v, u2f(prim)), hit ? inst : kUnset, maxSeg, zeroCutoff, r);
-        if (lead && r.addRad) addRadiance(rad, f2u(o4.w), r.radd);
+        if (r.addRad) E = addU(E, r.radd);
         pc.hit += r.hitGeom; pc.acc += r.accd;
         if (r.shadow) {
             ++pc.sh;
@@ -2655,7 +2676,7 @@ __device__ __forceinline__ void pairPath(const DevScene& S, const TraceTables& T
                 float sdep = r.so.w, su = 0.0f, sv = 0.0f;
                 uint32_t si = kUnset, sp = kUnset;
                 if (!traceWave<true, W2>(S, Tt, xyz(r.so), xyz(r.sd), sdep, su, sv, si, sp, rstk, pro)) {
-                    if (lead) addRadiance(rad, f2u(r.sd.w), xyz(r.sc));
+                    E = addU(E, xyz(r.sc));
                     ++pc.un; ++pc.acc;
                 }
             }
@@ -2666,18 +2687,19 @@ __device__ __forceinline__ void pairPath(const DevScene& S, const TraceTables& T
             if (pend) {                    /* the sample's last shadow ray */
                 while (ldsLoadAcq(&box.done[w]) != posted) __builtin_amdgcn_s_sleep(1);
                 if (!box.occ[w]) {
-                    if (lead) addRadiance(rad, f2u(box.sd[w].w), xyz(box.sc[w]));
+                    E = addU(E, xyz(box.sc[w]));
                     ++pc.un; ++pc.acc;
                 }
                 pend = false;
             }
             ++pc.samples;
             if (lead) {
+                storeRadiance(rad, __builtin_amdgcn_readfirstlane(f2u(o4.w)), E);   /* (uniform: an SGPR address) */
                 __threadfence();           /* radiance before completion */
                 atomicAdd(&frameDone[(blockIdx.x % kStripes) * window + slot], 1u);
             }
             /* the frame's next sample of this pixel continues on this wave */
-            if (chainNext(cam, G, spp, f2u(o4.w), slot, r.seedOut, o4, d4, T4)) { ++slot; continue; }
+            if (chainNext(cam, G, spp, f2u(o4.w), slot, r.seedOut, o4, d4, T4)) { ++slot; E = mk3(0.0f, 0.0f, 0.0f); continue; }
             break;
         }
         ++pc.cont;
