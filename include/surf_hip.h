@@ -207,12 +207,15 @@ int surf_set_zero_cutoff(surf_ctx* ctx, int enabled);
  * Drains the context first. */
 int surf_set_tail_policy(surf_ctx* ctx, uint32_t threshold_paths, uint32_t lanes_per_wave, uint32_t stage_segments);
 /* Drain paths handed to the cooperative tail (default 150000, 0 = never): one
- * path per 64-lane wave with the lanes-as-planes traversal (single-leaf TLAS of
- * <= 64 instances), in two-wave workgroups whose idle wave traces its
- * sibling's shadow rays once the path queue is empty (SURF_TAIL_PAIR=0 in the
- * environment: one-wave workgroups); with SURF_TAIL_ROWS=1 at surf_create,
- * four paths per wave (one per 16-lane row, a path queue; <= 16 instances).
- * Identical results. */
+ * path per 64-lane wave with the lanes-as-planes traversal (any TLAS -- a
+ * single-leaf TLAS walks its instances in a wave-uniform loop, any other the
+ * TLAS DFS on the wave -- with a BVH stack of <= 64 entries; past 64
+ * instances, materials or lights the tables are read from global memory), in
+ * two-wave workgroups whose idle wave traces its sibling's shadow rays once
+ * the path queue is empty (SURF_TAIL_PAIR=0 in the environment: one-wave
+ * workgroups); with a ROWS=1 build and SURF_TAIL_ROWS=1 at surf_create, four
+ * paths per wave (one per 16-lane row, a path queue; single-leaf TLAS of <= 16
+ * instances, 1-sample frames).  Identical results. */
 int surf_set_tail_coop(surf_ctx* ctx, uint32_t max_paths);
 /* Diagnostics: how many paths the segment cap ended in the current sample
  * stream, and the sample ids (frame slot * shard pixels + pixel) of up to
@@ -264,7 +267,8 @@ int surf_set_camera(surf_ctx* ctx, const surf_camera_ubo* camera);
  * starts a stream issues every frame's samples of the pixels whose centre
  * camera ray first hits one of the largest BLASes first (SURF_REORDER=0:
  * frame-major); continuations are traced in the order of the large BLASes
- * they can reach (SURF_KEY=0: by start instance); each phase's shadow rays are
+ * they can reach, those reaching the most first (SURF_KEY=1: ascending,
+ * 0: by start instance); each phase's shadow rays are
  * traced beside the next phase's extension (SURF_OVERLAP=0: serialized). */
 int surf_render(surf_ctx* ctx, uint32_t frames, uint32_t first_sample_index,
                 uint32_t max_segments, uint32_t samples_per_frame);
@@ -295,8 +299,8 @@ int surf_trace_closest(surf_ctx* ctx, uint32_t n, const float* o, const float* d
 int surf_trace_any(surf_ctx* ctx, uint32_t n, const float* o, const float* d, const float* tmax,
                    uint8_t* occluded);
 /* 0: one ray per lane (the wavefront kernels' traversal); 1: one ray per
- * 64-lane wave, lanes as the node record's planes (needs a single-leaf TLAS of
- * <= 64 instances and a BVH stack of <= 64 entries); 2: one ray per 16-lane
+ * 64-lane wave, lanes as the node record's planes (any TLAS; needs a BVH stack
+ * of <= 64 entries); 2: one ray per 16-lane
  * row, four per wave (the drain's traversal; single-leaf TLAS of <= 16
  * instances, stack <= 64).  Results are identical; selects what surf_trace_* run. */
 int surf_set_trace_mode(surf_ctx* ctx, int mode);

@@ -1717,13 +1717,23 @@ __device__ __forceinline__ uint32_t heavyMask(const DevScene& S, float4 o, float
  * a wave's lanes enter the same expensive BVHs -- the wave-uniform instance
  * loop pays, per instance, its slowest lane in it (recorded C3 extension rays,
  * lock-step visit steps per 64 rays, tools/lockstep_sim.cpp: 53.8 by start
- * instance x quadrant, 37.7 by heavy-instance mask).  Otherwise the instance
- * the path starts on (<= 14; camera rays: kBins - 1) x the quadrant: 1 M
- * recorded extension rays (tools/order_probe.py, order_probe2.py): 634 us
- * shuffled, 345 by start instance, 334 by start x quadrant. */
+ * instance x quadrant, 37.7 by heavy-instance mask).  keyMode 2 (default)
+ * orders the masks descending: the rays that reach the most heavy BLASes --
+ * the costliest -- come first in the order, so k_extend's first-dispatched
+ * workgroups take them and its last-dispatched ones the cheap ones (longest
+ * jobs first).  In ascending order (keyMode 1) the costly bins sat at the end
+ * of the grid's first pass, on the last-dispatched workgroups, unless enough
+ * of them spilled into the grid-stride second pass (which the first workgroups
+ * run): k_extend 119 -> 166 ms per C3 render between a 5- and a 4.5-frame pool
+ * at the same grid, 117 -> 150 ms at 56 workgroups per CU; heavy-first: 119
+ * and 117 (profiles/r4_experiments/cliff).  Otherwise the instance the path
+ * starts on (<= 14; camera rays: kBins - 1) x the quadrant: 1 M recorded
+ * extension rays (round 2, DESIGN 4 "Ray order"): 634 us shuffled, 345 by
+ * start instance, 334 by start x quadrant. */
 __device__ __forceinline__ uint8_t poolKey(const DevScene& S, uint32_t inst, float4 o, float4 d) {
     const uint32_t cx = (o.x - S.cellLo[0]) * S.cellScale[0] >= 1.0f ? 1u : 0u;
     const uint32_t cz = (o.z - S.cellLo[2]) * S.cellScale[2] >= 1.0f ? 1u : 0u;
+    if (S.keyMode == 2u) return (uint8_t)((7u - heavyMask(S, o, d, kFarAway)) * 4u + cx + 2u * cz);
     if (S.keyMode) return (uint8_t)(heavyMask(S, o, d, kFarAway) * 4u + cx + 2u * cz);
     return (uint8_t)((inst < 14u ? inst : 14u) * 4u + cx + 2u * cz);
 }

@@ -95,7 +95,11 @@ struct surf_ctx {
     uint32_t* dPerm = nullptr;
     uint32_t permA = 0, permFrames = 0;
     std::vector<uint32_t> heavyInst;
-    uint32_t keyMode = 1;          /* pool ray-order key (SURF_KEY): 1 heavy-instance mask x quadrant, 0 start instance x quadrant */
+    /* pool ray-order key (SURF_KEY): 2 heavy-instance mask x quadrant, most
+     * heavy instances first (the default: the costliest rays are dealt to the
+     * first-dispatched workgroups, DESIGN 4 "Pool sizing"), 1 the same key
+     * ascending, 0 start instance x quadrant */
+    uint32_t keyMode = 2;
     /* camera */
     bool hasCamera = false;
     DevCamera cam{};
@@ -368,9 +372,10 @@ int allocWavefront(surf_ctx* c) {
     if (c->extBlock == 128) extPerCu *= 2;                 /* the same threads per CU in half-size workgroups */
     c->gridExtend = (uint32_t)std::min<uint64_t>((cap + c->extBlock - 1) / c->extBlock, (uint64_t)cus * extPerCu);
     /* k_extend: ~1.5 rays per thread at a full pool (grid-stride).  Measured
-     * (DESIGN §4 "Pool sizing"): the launch is fast at 1.3-1.6 rays per thread
-     * and 15-30 % slower at 1.1-1.2 or >= 1.7 (C3: 48 workgroups per CU = 1.4
-     * -> 120 ms, 56 = 1.2 -> 151 ms; C4: 1.56 -> 1094 ms, 3.1 -> 1170 ms) */
+     * (DESIGN §4 "Pool sizing"): with the heavy-first ray order the launch
+     * time is flat from 1.2 to 1.5 rays per thread (C3 117-118 ms per render at
+     * 48-56 workgroups per CU), slower at one ray per thread (131 ms) and at
+     * >= 1.7 (C3 127 ms at 36; C4: 1.56 -> 1094 ms, 3.1 -> 1170 ms) */
     if (!eExt) c->gridExtend = (uint32_t)std::max<uint64_t>(c->gridExtend, (cap * 2 / 3 + c->extBlock - 1) / c->extBlock);
     c->gridConnect = (uint32_t)std::min<uint64_t>(maxBlocks, (uint64_t)cus * conPerCu);
     c->coopMax = (uint32_t)cus * 4 * SURF_TAIL_WAVES;
@@ -989,7 +994,7 @@ int createCtx(int dev, uint32_t w, uint32_t h, std::vector<uint32_t> rows, surf_
         c->sortShadow = e[0] != '2';
     }
     if (const char* e = std::getenv("SURF_CONNECT_GLOBAL")) c->connectGlobal = e[0] != '0';
-    if (const char* e = std::getenv("SURF_KEY")) c->keyMode = e[0] == '0' ? 0u : 1u;
+    if (const char* e = std::getenv("SURF_KEY")) c->keyMode = e[0] == '0' ? 0u : (e[0] == '1' ? 1u : 2u);
     if (const char* e = std::getenv("SURF_OVERLAP")) c->overlap = e[0] != '0';
     if (const char* e = std::getenv("SURF_REORDER")) c->reorder = e[0] != '0';
     if (const char* e = std::getenv("SURF_TAIL_ROWS")) c->tailRows = e[0] == '1';

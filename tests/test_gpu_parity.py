@@ -231,13 +231,15 @@ def test_ray_order_and_launch_shapes_bitexact(oracle_scene, product_scene, sort,
     r.close()
 
 
-@pytest.mark.parametrize("reorder,key,overlap", [("1", "1", "1"), ("0", "1", "1"), ("1", "0", "1"), ("1", "1", "0")],
-                         ids=["default", "frame-major-issue", "start-instance-key", "connect-serialized"])
+@pytest.mark.parametrize("reorder,key,overlap", [("1", "2", "1"), ("0", "2", "1"), ("1", "1", "1"), ("1", "0", "1"),
+                                                 ("1", "2", "0")],
+                         ids=["default", "frame-major-issue", "ascending-mask-key", "start-instance-key", "connect-serialized"])
 def test_issue_order_keys_overlap_bitexact(oracle_scene, product_scene, reorder, key, overlap, monkeypatch):
     """Scheduling only: the class-ordered issue of a multi-frame stream (pixels
     whose centre ray first hits a heavy instance, all frames first;
-    SURF_REORDER), the pool's ray-order key (heavy-BLAS mask or start
-    instance; SURF_KEY) and k_connect on its own graph stream (SURF_OVERLAP)
+    SURF_REORDER), the pool's ray-order key (heavy-BLAS mask, most heavy
+    first or ascending, or start instance; SURF_KEY) and k_connect on its own
+    graph stream (SURF_OVERLAP)
     change no sample: radiance and event counts equal the oracle's."""
     W, H, F = 96, 64, 6
     monkeypatch.setenv("SURF_REORDER", reorder)
