@@ -60,7 +60,7 @@ B_EVENT = {"n_ext": 52, "n_hit": 68, "n_cont": 48, "n_shadow": 88, "n_acc": 24}
 # rocprofv3 summary of this bench command per workload (tools/profile_round.sh + tools/summarize_profile.py):
 # k_extend's average duration (--kernel-trace --stats) and HBM bytes per launch (FETCH_SIZE x2 +
 # WRITE_SIZE, separate PMC passes, MI355X_MICROARCH.md HBM/rocprofv3 section).
-PMC_SUMMARY = os.path.join(REPO, "profiles", "r3_{}", "summary.json")
+PMC_SUMMARY = os.path.join(REPO, "profiles", "r4_{}", "summary.json")
 
 WORKLOADS = {
     "C3": dict(scene="indoor", width=1280, height=720, spp=256, max_segments=0, cpu_row_step=5),
