@@ -169,7 +169,8 @@ int surf_set_pool_capacity(surf_ctx* ctx, uint32_t paths);
  * consecutive passes) whose samples may be in flight at once -- a multiple of
  * the stream's samples_per_frame.  Default: the passes the stream being
  * started requests (one render call's frames x spp, rounded to a multiple of spp),
- * at least 256 (a drop-in loop extends its stream one frame per call), at most
+ * at least 256 -- 1024 for a stream opened by a one-frame request (a drop-in
+ * loop extends its stream one frame per call) -- at most
  * 4096 and at most what min(32 GiB, a quarter of the free HBM) holds; a later
  * stream that requests more frames grows the ring (C3 at 1280x720: 256 frames
  * = 3.8 GB; C4 at 1920x1080: 1024 frames = 34 GB, within the 1035 that 32 GiB hold).
@@ -232,6 +233,11 @@ int surf_debug_capped(surf_ctx* ctx, uint32_t* sample_ids, uint32_t max, uint64_
  * cycles, leaf cycles, walks, leaves, triangles, two-level visits, prologue
  * cycles, instance-loop cycles (else 0).  No reference counterpart. */
 int surf_debug_segment_cycles(surf_ctx* ctx, const float* path12, uint32_t reps, uint64_t* cycles15);
+/* Diagnostics: the current sample stream's issue order.  permuted_frames is
+ * the number of leading frames whose chain heads are issued heavy pixels
+ * first (0: frame-major order throughout); heavy_pixels the size of that
+ * heavy class (0 when permuted_frames is 0).  No reference counterpart. */
+int surf_debug_issue_order(surf_ctx* ctx, uint32_t* heavy_pixels, uint32_t* permuted_frames);
 /* When enabled, per-kernel device times are measured with HIP events on the
  * render stream (slower: disables the graph replay). */
 int surf_set_profiling(surf_ctx* ctx, int enabled);

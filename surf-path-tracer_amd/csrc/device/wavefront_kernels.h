@@ -1679,8 +1679,9 @@ __device__ __forceinline__ void blockCount(Counters* C, const int (&idx)[N], con
  * ray starts on (the one its path just hit; camera rays have their own bin).
  * Rays that start on the same surface enter the same BVHs, so a wave's
  * wave-uniform instance loop walks fewer instances: 1 M recorded extension
- * rays take 635 us shuffled, 355 us grouped by start instance
- * (tools/order_probe.py).  A counting sort of 4-byte indices per phase
+ * rays take 635 us shuffled, 355 us grouped by start instance (round 1;
+ * DESIGN.md 4 "Ray order"; the probe script, tools/order_probe.py, was retired
+ * in round 3 -- commit 5a920ae still holds it).  A counting sort of 4-byte indices per phase
  * (count, scan, scatter; ~2 us of kernels per 100 k paths) feeds k_extend and
  * k_shade through order[]; hit records stay in order i, so the paths, their
  * results and the append order of the next pool are unchanged in content --
@@ -1739,7 +1740,8 @@ __device__ __forceinline__ uint8_t poolKey(const DevScene& S, uint32_t inst, flo
 }
 
 /* Shadow-ray order key: light slot (mod 2) x the octant cell of the scene box
- * holding the ray's origin.  1 M recorded shadow rays (tools/order_probe2.py):
+ * holding the ray's origin.  1 M recorded shadow rays (round 2; the retired
+ * tools/order_probe2.py, last in commit 5a920ae):
  * 340 us shuffled, 277 sorted by light, 238 by light x octant cell, 286 by
  * light x 4x4x4 cells (too fine: the bins stop sharing paths through the BVH).
  * The pool's heavy-instance mask (of the segment [0, tmax)) x light x x/z

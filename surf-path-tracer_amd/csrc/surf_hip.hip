@@ -93,6 +93,9 @@ struct surf_ctx {
     bool reorder = true;
     bool permValid = false;
     uint32_t* dPerm = nullptr;
+    /* one-frame render calls may leave up to a pool of their stream unissued
+     * (SURF_LOOP_LAG=0: issue each call's frame before returning) */
+    bool loopLag = true;
     uint32_t permA = 0, permFrames = 0;
     std::vector<uint32_t> heavyInst;
     /* pool ray-order key (SURF_KEY): 2 heavy-instance mask x quadrant, most
@@ -389,15 +392,19 @@ int allocWavefront(surf_ctx* c) {
 /* The radiance ring (float4 per frame slot x pixel) and the per-slot
  * completion counters, sized for the stream about to start (no stream active):
  * as many slots as the stream requests frames -- so no frame waits for an old
- * frame's long Russian-roulette paths to free a slot -- at least kWindowFloor
- * (a drop-in loop extends its stream one frame per call, so its first request
- * says nothing about its length), at most 4096 and at most what
- * min(32 GiB, a quarter of the free HBM) holds.  A later, longer stream grows
- * the ring; a window set by surf_set_frame_batch is kept as given. */
-constexpr uint64_t kWindowFloor = 256;
+ * frame's long Russian-roulette paths to free a slot -- at least kWindowFloor,
+ * and at least kLoopFloor for a stream opened by a one-frame request (a
+ * drop-in loop extends its stream one frame per call, so its first request
+ * says nothing about its length; 4096 one-frame calls at 1280x720 run at
+ * 365 / 443 / 472 Mrays/s with 256 / 1024 / 4096 slots), at most
+ * 4096 and at most what min(32 GiB, a quarter of the free HBM) holds.  A
+ * later, longer stream grows the ring; a window set by surf_set_frame_batch
+ * is kept as given. */
+constexpr uint64_t kWindowFloor = 256, kLoopFloor = 1024;
 int ensureWindow(surf_ctx* c, uint64_t frames, uint32_t spp) {
     const uint64_t passes = frames * spp;
-    uint64_t want = c->windowFixed ? c->window : std::min<uint64_t>(4096, std::max<uint64_t>(passes, kWindowFloor));
+    const uint64_t floor = frames == 1 ? kLoopFloor : kWindowFloor;
+    uint64_t want = c->windowFixed ? c->window : std::min<uint64_t>(4096, std::max<uint64_t>(passes, floor));
     if (c->windowFixed && c->window % spp != 0)
         return fail(c, SURF_ERR_INVALID, "frame window " + std::to_string(c->window) + " is not a multiple of samples_per_frame " +
                                              std::to_string(spp));
@@ -883,7 +890,7 @@ uint32_t tailThreshold(const surf_ctx* c) {
 
 /* Runs until every requested sample is issued (drain = false) or until every
  * requested frame is accumulated (drain = true). */
-int pump(surf_ctx* c, bool drain) {
+int pump(surf_ctx* c, bool drain, uint64_t lag) {
     int rc;
     if ((rc = pushLimit(c))) return rc;
     const uint64_t target = c->targetFrames * (uint64_t)c->npx;
@@ -891,7 +898,7 @@ int pump(surf_ctx* c, bool drain) {
         const uint64_t issued = c->hctr->issued[0];
         /* in flight at a replay boundary: the pool the next phase extends */
         const uint32_t inflight = c->hctr->nIn[0];
-        if (!drain && issued >= target) return SURF_OK;
+        if (!drain && issued + lag >= target) return SURF_OK;
         if (drain && c->accPasses >= targetPasses(c)) return SURF_OK;
         const bool starved = issued >= c->pushedLimit;     /* nothing more may be issued right now */
         const uint64_t accBefore = c->accPasses;
@@ -911,8 +918,9 @@ int pump(surf_ctx* c, bool drain) {
             /* draining (nothing left to issue): several replays per host poll --
              * the per-replay poll, not the kernels, is what a small pool pays */
             const int reps = starved ? c->drainReplays : 1;
-            /* at most one frame left to issue (a per-frame render call): short replays */
-            const bool shortRun = !drain && target - issued <= c->npx;
+            /* a per-frame render call (lagged, or at most one frame left to
+             * issue): short replays */
+            const bool shortRun = !drain && (lag > 0 || target - issued <= c->npx);
             for (int k = 0; k < reps; ++k)
                 if ((rc = advance(c, shortRun))) return rc;
         }
@@ -930,7 +938,7 @@ int ensureDrained(surf_ctx* c) {
         if (rc) return rc;
     }
     SURF_CHECK(c, hipEventRecord(c->ev0, c->stream));
-    int rc = pump(c, true);
+    int rc = pump(c, true, 0);
     if (rc) return rc;
     SURF_CHECK(c, hipEventRecord(c->ev1, c->stream));
     SURF_CHECK(c, hipEventSynchronize(c->ev1));
@@ -996,6 +1004,7 @@ int createCtx(int dev, uint32_t w, uint32_t h, std::vector<uint32_t> rows, surf_
     if (const char* e = std::getenv("SURF_CONNECT_GLOBAL")) c->connectGlobal = e[0] != '0';
     if (const char* e = std::getenv("SURF_KEY")) c->keyMode = e[0] == '0' ? 0u : (e[0] == '1' ? 1u : 2u);
     if (const char* e = std::getenv("SURF_OVERLAP")) c->overlap = e[0] != '0';
+    if (const char* e = std::getenv("SURF_LOOP_LAG")) c->loopLag = e[0] != '0';
     if (const char* e = std::getenv("SURF_REORDER")) c->reorder = e[0] != '0';
     if (const char* e = std::getenv("SURF_TAIL_ROWS")) c->tailRows = e[0] == '1';
     if (const char* e = std::getenv("SURF_TAIL_PAIR")) c->tailPair = e[0] != '0';
@@ -1132,6 +1141,13 @@ int surf_debug_capped(surf_ctx* c, uint32_t* sids, uint32_t max, uint64_t* count
             if (c->hctr->capped[k] != kUnset) { if (sids) sids[n] = c->hctr->capped[k]; ++n; }
     if (sids)
         for (uint32_t k = n; k < std::min<uint32_t>(max, 64u); ++k) sids[k] = kUnset;
+    return SURF_OK;
+}
+
+int surf_debug_issue_order(surf_ctx* c, uint32_t* heavy_pixels, uint32_t* permuted_frames) {
+    if (!c || !heavy_pixels || !permuted_frames) return SURF_ERR_INVALID;
+    *heavy_pixels = c->permFrames ? c->permA : 0u;
+    *permuted_frames = c->permFrames;
     return SURF_OK;
 }
 
@@ -1627,7 +1643,14 @@ int surf_render(surf_ctx* c, uint32_t frames, uint32_t firstSample, uint32_t max
     if (!c->profiling && (rc = buildGraph(c))) return rc;         /* (re)captured if the ring moved */
     SURF_CHECK(c, hipEventRecord(c->ev0, c->stream));
     c->targetFrames += frames;
-    if ((rc = pump(c, false))) return rc;
+    /* A one-frame call (the drop-in loop, main.cpp:381-446) may return with up
+     * to a pool's worth of its stream not yet issued: the next calls, or the
+     * drain a read of the accumulator starts, issue it.  Issuing each call's
+     * frame at once would run 2 phases per frame on a pool a third full
+     * (DESIGN 4 "Pool sizing"); with the lag the pool stays full and the
+     * calls replay only as many phases as the stream retires. */
+    const uint64_t lag = frames == 1 && c->loopLag ? c->capacity : 0;
+    if ((rc = pump(c, false, lag))) return rc;
     SURF_CHECK(c, hipEventRecord(c->ev1, c->stream));
     SURF_CHECK(c, hipEventSynchronize(c->ev1));
     float ms = 0;

@@ -101,6 +101,7 @@ def load() -> C.CDLL:
         "surf_set_pool_capacity": ([P, U32], I32), "surf_set_frame_batch": ([P, U32], I32),
         "surf_set_profiling": ([P, I32], I32), "surf_set_zero_cutoff": ([P, I32], I32), "surf_set_trace_mode": ([P, I32], I32), "surf_set_tail_policy": ([P, U32, U32, U32], I32), "surf_set_tail_coop": ([P, U32], I32),
         "surf_debug_capped": ([P, P, U32, C.POINTER(C.c_uint64)], I32),
+        "surf_debug_issue_order": ([P, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)], I32),
         "surf_debug_segment_cycles": ([P, P, U32, P], I32),
         "surf_upload_scene": ([P, C.POINTER(SceneDesc)], I32),
         "surf_set_camera": ([P, P], I32),
@@ -372,6 +373,13 @@ class Renderer:
         n = C.c_uint64()
         _check(load().surf_debug_capped(self._h, _ptr(ids), 64, C.byref(n)), "surf_debug_capped", self._h)
         return int(n.value), ids[ids != 0xFFFFFFFF]
+
+    def debug_issue_order(self):
+        """(heavy pixels, permuted frames) of the current stream's issue order
+        (surf_debug_issue_order); (0, 0) when it is frame-major throughout."""
+        a, f = C.c_uint32(), C.c_uint32()
+        _check(load().surf_debug_issue_order(self._h, C.byref(a), C.byref(f)), "surf_debug_issue_order", self._h)
+        return int(a.value), int(f.value)
 
     def debug_segment_cycles(self, origin, direction, throughput, seed: int, segment: int = 1, reps: int = 64):
         """Diagnostics: mean shader-clock cycles of one drain segment's pieces on

@@ -247,6 +247,11 @@ def test_issue_order_keys_overlap_bitexact(oracle_scene, product_scene, reorder,
     monkeypatch.setenv("SURF_OVERLAP", overlap)
     r = surf_amd.Renderer(product_scene, W, H, pool_capacity=4096)
     r.render(F, 0, 0)
+    heavy, permuted = r.debug_issue_order()
+    if reorder == "1":      # the class-ordered issue must be engaged, not trivially skipped
+        assert 0 < heavy < W * H and permuted == F, (heavy, permuted)
+    else:
+        assert (heavy, permuted) == (0, 0)
     g = r.accumulator()
     st = r.stats()
     oracle.set_zero_cutoff(True)
@@ -257,6 +262,32 @@ def test_issue_order_keys_overlap_bitexact(oracle_scene, product_scene, reorder,
     _assert_bitexact(g, c2, f"reorder={reorder} key={key} overlap={overlap}")
     _assert_counts(st, cnt)
     r.close()
+
+
+def test_permuted_stream_continued_bitexact(oracle_scene, product_scene, monkeypatch):
+    """A class-ordered (permuted) stream continued by a second call: render(6)
+    issues its six frames heavy pixels first; render(6, first=6) continues the
+    same sample stream (no restart), so frames 6..11 follow the permuted head
+    frame-major.  The 12 frames equal the oracle's bit for bit."""
+    W, H, F = 96, 64, 6
+    monkeypatch.setenv("SURF_REORDER", "1")
+    r = surf_amd.Renderer(product_scene, W, H, pool_capacity=4096)
+    r.render(F, 0, 0)
+    heavy, permuted = r.debug_issue_order()
+    assert 0 < heavy < W * H and permuted == F, (heavy, permuted)
+    r.render(F, F, 0)
+    assert r.debug_issue_order() == (heavy, permuted), "the second call must continue, not restart, the stream"
+    g = r.accumulator()
+    st = r.stats()
+    r.close()
+    oracle.set_zero_cutoff(True)
+    try:
+        c2, cnt, _ = oracle_scene.render(W, H, 2 * F)
+    finally:
+        oracle.set_zero_cutoff(False)
+    assert np.all(g[..., 3] == 2 * F)
+    _assert_bitexact(g, c2, "permuted stream continued across calls")
+    _assert_counts(st, cnt)
 
 
 @pytest.mark.parametrize("cutoff", [None, True], ids=["reference-no-cutoff", "cutoff-on-both"])
