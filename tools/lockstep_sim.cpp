@@ -44,6 +44,7 @@ int main(int argc, char** argv) {
     double iters = 0, active = 0, distinct = 0, uniform = 0, leafIters = 0, triDistinct = 0, triLoads = 0, nodeLoads = 0;
     double uniAct = 0;
     std::map<int,double> hist;
+    std::map<uint32_t, double> instIters, instLanes, instTri;   /* per TLAS instance: wave steps, lane-steps, triangle tests */
     for (uint32_t g = 0; g + 64 <= n; g += 64) {
         V3 o[64], d[64]; float depth[64];
         bool occ[64];
@@ -82,6 +83,7 @@ int main(int argc, char** argv) {
                 for (int l = 0; l < 64; ++l) if (act[l]) { ++na; ns.insert(node[l]); }
                 if (!na) break;
                 iters++; active += na; distinct += ns.size(); nodeLoads += na; if (ns.size() == 1) { uniform++; uniAct += na; }
+                instIters[T.idx[root.lf + k]] += 1; instLanes[T.idx[root.lf + k]] += na;
                 hist[std::min<int>(ns.size(), 64)]++;
                 for (int l = 0; l < 64; ++l) if (act[l]) {
                     const Node& nd = b.nodes[node[l]];
@@ -89,7 +91,7 @@ int main(int argc, char** argv) {
                     if (nd.cnt) {
                         anyLeaf = true;
                         bool h = false;
-                        for (uint32_t i = 0; i < nd.cnt; ++i) { ts.insert(nd.lf + i); triLoads++; float u, v; if (hitTri(in.blas->mesh->tris[b.idx[nd.lf + i]], oo[l], dd[l], depth[l], u, v) && ANY) { h = true; break; } }
+                        for (uint32_t i = 0; i < nd.cnt; ++i) { ts.insert(nd.lf + i); triLoads++; instTri[T.idx[root.lf + k]] += 1; float u, v; if (hitTri(in.blas->mesh->tris[b.idx[nd.lf + i]], oo[l], dd[l], depth[l], u, v) && ANY) { h = true; break; } }
                         if (h) { occ[l] = true; act[l] = false; continue; }
                         pop = true;
                     } else {
@@ -170,6 +172,9 @@ int main(int argc, char** argv) {
         }
         printf("per-instance passes: iterations %.0f (%.1f per 64 rays) active/iter %.1f\n", it2, it2 / (n / 64), act2 / it2);
     }
+    for (auto& [ii, v] : instIters)
+        printf("  instance %u (blas %zu nodes): wave steps per 64 rays %.2f, lanes per step %.1f, triangle tests per ray %.2f\n", ii,
+               S.inst[ii].blas->bvh.nodes.size(), v / (n / 64), instLanes[ii] / v, instTri[ii] / n);
     printf("groups %u iters/group %.1f active/iter %.1f distinct nodes/iter %.2f uniform iters %.3f (lanes in uniform iters %.3f of node loads)\n",
            n / 64, iters / (n / 64), active / iters, distinct / iters, uniform / iters, uniAct / nodeLoads);
     printf("leaf iters %.3f tri loads/iter-with-leaf %.1f distinct tris %.1f\n", leafIters / iters, triLoads / leafIters, triDistinct / leafIters);
