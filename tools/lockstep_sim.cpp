@@ -13,7 +13,7 @@
 #include <map>
 struct Lane { V3 oo, dd; uint32_t node; std::vector<uint32_t> st; bool act; };
 int main(int argc, char** argv) {
-    orc_scene* h = orc_scene_create(getenv("SURF_ASSETS") ? getenv("SURF_ASSETS") : "assets", 0);
+    orc_scene* h = orc_scene_create(getenv("SURF_ASSETS") ? getenv("SURF_ASSETS") : "assets", getenv("SCENE_VARIANT") ? atoi(getenv("SCENE_VARIANT")) : 0);
     Scene& S = *h->s;
     FILE* f = fopen(argv[1], "rb"); uint32_t n = 0;
     if (!f || fread(&n, 4, 1, f) != 1) return 1;
