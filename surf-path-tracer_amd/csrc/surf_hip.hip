@@ -96,6 +96,8 @@ struct surf_ctx {
     /* one-frame render calls may leave up to a pool of their stream unissued
      * (SURF_LOOP_LAG=0: issue each call's frame before returning) */
     bool loopLag = true;
+    /* occupancy probes: extra dynamic LDS per k_extend / k_connect workgroup (SURF_EXT_LDS_PAD / SURF_CON_LDS_PAD bytes) */
+    size_t extLdsPad = 0, conLdsPad = 0;
     uint32_t permA = 0, permFrames = 0;
     std::vector<uint32_t> heavyInst;
     /* pool ray-order key (SURF_KEY): 2 heavy-instance mask x quadrant, most
@@ -478,7 +480,7 @@ void launchPhase(surf_ctx* c, int ph, hipEvent_t* ev) {
     /* LW: the two-level records in the lane traversal (HBM-resident BVHs, S.laneW) */
     auto extendK = c->S.laneW ? (c->ldsTables ? k_extend<true, true> : k_extend<false, true>)
                               : (c->ldsTables ? k_extend<true, false> : k_extend<false, false>);
-    hipLaunchKernelGGL(extendK, dim3(c->gridExtend), dim3(c->extBlock), traversalLds(c, c->extBlock), s0, c->S,
+    hipLaunchKernelGGL(extendK, dim3(c->gridExtend), dim3(c->extBlock), traversalLds(c, c->extBlock) + c->extLdsPad, s0, c->S,
                        cur, c->hitTUV, c->hitInst, (const Counters*)c->ctr, par, stackWords(c, c->extBlock), order);
     if (ev) (void)hipEventRecord(ev[2], s0);
     if (ovl && ph > 0) (void)hipStreamWaitEvent(s0, c->capEv[2 * (ph - 1) + 1], 0);   /* the previous phase's connect */
@@ -505,8 +507,9 @@ void launchPhase(surf_ctx* c, int ph, hipEvent_t* ev) {
     const bool ldsC = c->ldsTables && !c->connectGlobal;   /* else global tables: LDS holds only the traversal stack */
     auto connectK = c->S.laneW ? (ldsC ? k_connect<true, true> : k_connect<false, true>)
                                : (ldsC ? k_connect<true, false> : k_connect<false, false>);
-    hipLaunchKernelGGL(connectK, dim3(c->gridConnect), dim3(kBlock), ldsC ? traversalLds(c, kBlock) : (size_t)sw * sizeof(uint32_t),
-                       s1, c->S, c->Q, c->rad, c->ctr, par, sw, qorder);
+    hipLaunchKernelGGL(connectK, dim3(c->gridConnect), dim3(kBlock),
+                       (ldsC ? traversalLds(c, kBlock) : (size_t)sw * sizeof(uint32_t)) + c->conLdsPad, s1, c->S, c->Q, c->rad, c->ctr,
+                       par, sw, qorder);
     if (ovl) (void)hipEventRecord(c->capEv[2 * ph + 1], s1);
     if (ev) (void)hipEventRecord(ev[5], s0);
     hipLaunchKernelGGL(k_regen, dim3(c->gridRegen), dim3(kBlock), 0, s0, c->cam, c->pool[par ^ 1], c->rad, c->ctr, par,
@@ -1005,6 +1008,8 @@ int createCtx(int dev, uint32_t w, uint32_t h, std::vector<uint32_t> rows, surf_
     if (const char* e = std::getenv("SURF_KEY")) c->keyMode = e[0] == '0' ? 0u : (e[0] == '1' ? 1u : 2u);
     if (const char* e = std::getenv("SURF_OVERLAP")) c->overlap = e[0] != '0';
     if (const char* e = std::getenv("SURF_LOOP_LAG")) c->loopLag = e[0] != '0';
+    if (const char* e = std::getenv("SURF_EXT_LDS_PAD")) c->extLdsPad = (size_t)std::max(0, std::atoi(e));
+    if (const char* e = std::getenv("SURF_CON_LDS_PAD")) c->conLdsPad = (size_t)std::max(0, std::atoi(e));
     if (const char* e = std::getenv("SURF_REORDER")) c->reorder = e[0] != '0';
     if (const char* e = std::getenv("SURF_TAIL_ROWS")) c->tailRows = e[0] == '1';
     if (const char* e = std::getenv("SURF_TAIL_PAIR")) c->tailPair = e[0] != '0';

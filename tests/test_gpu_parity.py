@@ -560,6 +560,42 @@ def test_animation_update_render_bitexact():
         p.close()
 
 
+def test_dropin_loop_lag_across_reads_and_updates():
+    """The interactive loop (main.cpp:381-446) on the lagged stream: one-frame
+    render() calls return with up to a pool of their samples unissued; a read
+    in the middle (stats) drains exactly the frames requested so far; an
+    animation update drains the pending samples under the old transforms
+    before re-uploading; after the clear the loop goes on.  Every observed
+    accumulator equals the oracle's, bit for bit."""
+    W, H = 48, 32
+    o = oracle.OracleScene()
+    p = surf_amd.Scene.indoor()
+    try:
+        r = surf_amd.Renderer(p, W, H)
+        r.set_zero_cutoff(False)
+        for f in range(3):
+            r.render(1, first_frame=f)
+        assert r.stats()["samples"] == W * H * 3
+        c, _, _ = o.render(W, H, 3)
+        _assert_bitexact(r.accumulator(), c, "3 lagged one-frame calls")
+        for f in range(3, 6):
+            r.render(1, first_frame=f)
+        p.update(0.7)
+        r.update_instances(p)                 # the pending frames 3..5 run under the old transforms
+        c, _, _ = o.render(W, H, 6)
+        _assert_bitexact(r.accumulator(), c, "6 one-frame calls, drained by the update")
+        o.update(0.7)
+        r.clear_accumulator()
+        for f in range(4):
+            r.render(1, first_frame=6 + f)
+        c, _, _ = o.render(W, H, 4, first_frame=6)
+        _assert_bitexact(r.accumulator(), c, "4 one-frame calls after the update")
+        r.close()
+    finally:
+        o.close()
+        p.close()
+
+
 def test_c5_deep_bvh_bitexact():
     """C5: 10.2M-triangle lattice BLAS (HBM-resident, depth 36,
     built by the parallel builder) -- hit records, a small render and three row
