@@ -29,6 +29,7 @@
  */
 #pragma once
 #include <hip/hip_runtime.h>
+#include <type_traits>
 #include "surf_math.h"
 
 namespace surfdev {
@@ -92,6 +93,9 @@ struct DevScene {
     const DevMaterial* mats;
     const uint2* lights;      /* (instance, primitive count) */
     uint32_t nLights;
+    /* the emitters' BLAS whose node records [sbNode0, sbNode0 + sbNodeN)
+     * k_connect stages in LDS (sbNodeN = 0: none) */
+    uint32_t sbNode0, sbNodeN;
     uint32_t nInst, nMats;
     uint32_t tlasLeafCount;   /* TLAS root is a leaf with this many instances (0: general TLAS) */
     uint32_t finiteBoxes;     /* every BLAS node box is finite: slabFinite is exact */
@@ -288,10 +292,13 @@ __device__ __forceinline__ float boxDist(float4 lo, float4 hi, V3 o, V3 rd, floa
 
 /* FIN: o, rd and every box finite (slabFinite is exact); else the reference's
  * ternary slab with its NaN behaviour. */
-template <bool ANY, bool FIN>
+/* STG: the BLAS is the one whose node records are staged in LDS (S.sbNode0,
+ * sN) -- the same records, so the same decisions and results.  SK: the stack
+ * entry type (16-bit when every node index fits). */
+template <bool ANY, bool FIN, bool STG = false, typename SK = uint32_t>
 __device__ __forceinline__ bool blasTrace(const DevScene& S, const TraceInst& I, V3 o, V3 d, V3 rd, float& depth,
                                           float& hu, float& hv, uint32_t& hprim,
-                                          uint32_t* stk, uint32_t stride, uint32_t base) {
+                                          SK* stk, uint32_t stride, uint32_t base, const float4* sN = nullptr) {
     const uint32_t nodeOff = I.meta.x;
     const float4* tri = S.tris + 3u * I.meta.y;
     /* root: never box-tested (bvh.cpp:131), only its children are */
@@ -299,8 +306,8 @@ __device__ __forceinline__ bool blasTrace(const DevScene& S, const TraceInst& I,
     const uint32_t rlf = f2u(r0.w), rcnt = f2u(r1.w);
     if (rcnt != 0u) return leafTestUniform<ANY>(tri, rlf, rcnt, o, d, depth, hu, hv, hprim);
     /* stack pointer walks in steps of `stride` words (lane-interleaved LDS) */
-    uint32_t* const bottom = stk + base * stride;
-    uint32_t* sp = bottom;
+    SK* const bottom = stk + base * stride;
+    SK* sp = bottom;
     uint32_t node;
     bool any = false;
     {
@@ -322,7 +329,7 @@ __device__ __forceinline__ bool blasTrace(const DevScene& S, const TraceInst& I,
         }
     }
     for (;;) {
-        const float4* nd = S.nodes + 4u * node;
+        const float4* nd = STG ? sN + 4u * (node - S.sbNode0) : S.nodes + 4u * node;
         float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
         pin(q0); pin(q1); pin(q2); pin(q3);
         const uint32_t lf = f2u(q0.w), cnt = f2u(q1.w);
@@ -476,9 +483,10 @@ __device__ __forceinline__ float rowDot(float4 r, float x, float y, float z, flo
     return a + b;
 }
 
-template <bool ANY, bool LW = false>
+template <bool ANY, bool LW = false, bool STG = false, typename SK = uint32_t>
 __device__ __forceinline__ bool instanceTrace(const DevScene& S, const TraceInst& I, V3 o, V3 d, float& depth, float& hu,
-                                              float& hv, uint32_t& hprim, uint32_t* stk, uint32_t stride, uint32_t base) {
+                                              float& hv, uint32_t& hprim, SK* stk, uint32_t stride, uint32_t base,
+                                              const float4* sN = nullptr) {
     V3 oo = mk3(rowDot(I.m0, o.x, o.y, o.z, 1.0f), rowDot(I.m1, o.x, o.y, o.z, 1.0f), rowDot(I.m2, o.x, o.y, o.z, 1.0f));
     if (!I.meta.z) oo = divs(oo, rowDot(I.m3, o.x, o.y, o.z, 1.0f));
     const V3 dd = mk3(rowDot(I.m0, d.x, d.y, d.z, 0.0f), rowDot(I.m1, d.x, d.y, d.z, 0.0f), rowDot(I.m2, d.x, d.y, d.z, 0.0f));
@@ -488,11 +496,11 @@ __device__ __forceinline__ bool instanceTrace(const DevScene& S, const TraceInst
     const V3 rd = mk3(1.0f / dd.x, 1.0f / dd.y, 1.0f / dd.z);
     /* S.finiteBoxes: every BLAS box is finite (checked at upload) */
     const bool fin = S.finiteBoxes && finite3(oo) && finite3(rd);
-    if (LW)
+    if constexpr (LW)
         return fin ? blasTraceW<ANY, true>(S, I, oo, dd, rd, depth, hu, hv, hprim, stk, stride, base)
                    : blasTraceW<ANY, false>(S, I, oo, dd, rd, depth, hu, hv, hprim, stk, stride, base);
-    if (fin) return blasTrace<ANY, true>(S, I, oo, dd, rd, depth, hu, hv, hprim, stk, stride, base);
-    return blasTrace<ANY, false>(S, I, oo, dd, rd, depth, hu, hv, hprim, stk, stride, base);
+    if (fin) return blasTrace<ANY, true, STG, SK>(S, I, oo, dd, rd, depth, hu, hv, hprim, stk, stride, base, sN);
+    return blasTrace<ANY, false, STG, SK>(S, I, oo, dd, rd, depth, hu, hv, hprim, stk, stride, base, sN);
 }
 
 /* Instance tables a traversal reads: LDS copies (stageTrace) or global. */
@@ -520,9 +528,9 @@ __device__ __forceinline__ TraceTables traceTables(const DevScene& S, uint32_t* 
 }
 
 /* BvhTLAS::intersect / intersectAny (bvh.cpp:654-778). */
-template <bool ANY, bool LW = false>
+template <bool ANY, bool LW = false, bool STG = false, typename SK = uint32_t>
 __device__ __forceinline__ bool traceScene(const DevScene& S, const TraceTables& Tt, V3 o, V3 d, float& depth, float& hu, float& hv,
-                                           uint32_t& hinst, uint32_t& hprim, uint32_t* stk, uint32_t stride) {
+                                           uint32_t& hinst, uint32_t& hprim, SK* stk, uint32_t stride, const float4* sN = nullptr) {
     bool any = false;
     if (S.tlasLeafCount) {
         /* single-leaf TLAS (the bundled scene): every lane visits the same
@@ -546,7 +554,11 @@ __device__ __forceinline__ bool traceScene(const DevScene& S, const TraceTables&
                 const float t1 = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
                 if (t1 < t0 || t1 < 0.0f || t0 >= depth) continue;
             }
-            if (instanceTrace<ANY, LW>(S, I, o, d, depth, hu, hv, hprim, stk, stride, 0u)) {
+            /* (wave-uniform: the staged BLAS's instances walk it in LDS) */
+            const bool hitI = (STG && !LW && I.meta.x == S.sbNode0)
+                                  ? instanceTrace<ANY, false, true, SK>(S, I, o, d, depth, hu, hv, hprim, stk, stride, 0u, sN)
+                                  : instanceTrace<ANY, LW, false, SK>(S, I, o, d, depth, hu, hv, hprim, stk, stride, 0u);
+            if (hitI) {
                 if (ANY) return true;
                 any = true;
                 hinst = ii;
@@ -564,7 +576,7 @@ __device__ __forceinline__ bool traceScene(const DevScene& S, const TraceTables&
         if (cnt != 0u) {
             for (uint32_t k = 0; k < cnt; ++k) {
                 const uint32_t ii = Tt.order[lf + k];
-                if (instanceTrace<ANY, LW>(S, Tt.inst[ii], o, d, depth, hu, hv, hprim, stk, stride, sp)) {
+                if (instanceTrace<ANY, LW, false, SK>(S, Tt.inst[ii], o, d, depth, hu, hv, hprim, stk, stride, sp)) {
                     if (ANY) return true;
                     any = true;
                     hinst = ii;
@@ -1656,10 +1668,10 @@ __device__ __forceinline__ void waveCount(unsigned long long* ctr, unsigned long
 /* Block-level event counts: one atomic per counter per workgroup (the counters
  * are hot addresses shared by every wave of the launch).  vals are wave-uniform;
  * every thread of the block must call this. */
-template <int N>
+template <int N, int BLK = kBlock>   /* BLK: the largest workgroup the caller runs */
 __device__ __forceinline__ void blockCount(Counters* C, const int (&idx)[N], const unsigned long long (&vals)[N]) {
     unsigned long long* ev = C->evS[blockIdx.x % kStripes];
-    __shared__ unsigned long long sEv[N][kBlock / 64];
+    __shared__ unsigned long long sEv[N][BLK / 64];
     const uint32_t w = threadIdx.x >> 6, nw = blockDim.x >> 6;
     if (laneId() == 0)
         for (int k = 0; k < N; ++k) sEv[k][w] = vals[k];
@@ -2313,15 +2325,26 @@ __global__ __launch_bounds__(kBlock, SURF_SHADE_WAVES) void k_shade(DevScene S, 
     blockCount<5>(C, {1, 2, 3, 4, 7}, {cHit, cCont, cSh, cAcc, cCap});
 }
 
-template <bool LDS, bool LW = false>
-__global__ __launch_bounds__(kBlock, SURF_TRACE_WAVES) void k_connect(DevScene S, ShadowQ Q, float4* __restrict__ rad, Counters* C, int par,
+template <bool LDS, bool LW = false, bool STG = false>
+__global__ __launch_bounds__(kBlock, STG ? 5 : SURF_TRACE_WAVES) void k_connect(DevScene S, ShadowQ Q, float4* __restrict__ rad, Counters* C, int par,
                                                     uint32_t stackWords, const uint32_t* __restrict__ order) {
     extern __shared__ uint32_t lds[];
     const uint32_t n = (uint32_t)(C->app[par] >> 32);
     if (blockIdx.x * blockDim.x >= n) return;               /* no shadow rays for this block */
-    const TraceTables Tt = traceTables<LDS>(S, lds, stackWords);
+    /* STG: the emitters' BLAS node records (every unoccluded shadow ray walks
+     * that BLAS down to its sampled triangle) staged after a stack of 16-bit
+     * entries (every node index < 65536) and the trace tables; stageTrace's
+     * barrier publishes them */
+    const uint32_t stackWordsUsed = STG ? stackWords / 2u : stackWords;
+    float4* sN = nullptr;
+    if (STG) {
+        sN = reinterpret_cast<float4*>(lds + ((stackWordsUsed + S.nInst * (uint32_t)((sizeof(TraceInst) + 4u) / 4u) + 3u) & ~3u));
+        for (uint32_t k = threadIdx.x; k < 4u * S.sbNodeN; k += blockDim.x) sN[k] = S.nodes[4u * S.sbNode0 + k];
+    }
+    const TraceTables Tt = traceTables<LDS>(S, lds, stackWordsUsed);
     const uint32_t stride = blockDim.x;
-    uint32_t* stk = lds + threadIdx.x;
+    using SK = typename std::conditional<STG, uint16_t, uint32_t>::type;
+    SK* stk = reinterpret_cast<SK*>(lds) + threadIdx.x;
     unsigned long long cUn = 0;
     for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
         const uint32_t i0 = base + threadIdx.x;
@@ -2331,7 +2354,7 @@ __global__ __launch_bounds__(kBlock, SURF_TRACE_WAVES) void k_connect(DevScene S
             const float4 o = ldS(&Q.od[2u * i]), d = ldS(&Q.od[2u * i + 1u]);
             float depth = o.w, u = 0.0f, v = 0.0f;
             uint32_t inst = kUnset, prim = kUnset;
-            const bool occ = traceScene<true, LW>(S, Tt, xyz(o), xyz(d), depth, u, v, inst, prim, stk, stride);
+            const bool occ = traceScene<true, LW, STG, SK>(S, Tt, xyz(o), xyz(d), depth, u, v, inst, prim, stk, stride, sN);
             if (!occ) {
                 const float4 c = ldS(&Q.c[i]);
                 addRadiance(rad, f2u(d.w), xyz(c));

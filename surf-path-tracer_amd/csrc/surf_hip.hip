@@ -81,7 +81,7 @@ struct surf_ctx {
     DevScene S{};
     std::vector<void*> sceneAllocs;
     uint32_t stackDepth = 0;
-    uint32_t nInstances = 0, nTriangles = 0;
+    uint32_t nInstances = 0, nTriangles = 0, nBlasNodes = 0;
     /* what surf_update_instances may change: instance records, TLAS, lights */
     uint32_t nMaterials = 0, nLightsUp = 0, tlasNodeCount = 0, maxBlasDepth = 0;
     std::map<std::tuple<uint32_t, uint32_t, uint32_t>, std::array<float4, 4>> blasRoots;  /* (node, idx, tri offset) -> root record */
@@ -98,6 +98,10 @@ struct surf_ctx {
     bool loopLag = true;
     /* occupancy probes: extra dynamic LDS per k_extend / k_connect workgroup (SURF_EXT_LDS_PAD / SURF_CON_LDS_PAD bytes) */
     size_t extLdsPad = 0, conLdsPad = 0;
+    /* k_connect stages the emitters' BLAS node records in LDS when they are
+     * few and every BLAS node index fits 16 bits (SURF_LDS_LIGHTBLAS=0: never) */
+    bool ldsLightBlas = true;
+    std::map<uint32_t, std::array<uint32_t, 2>> blasNodeRange;   /* BLAS node offset -> [first, last] reachable node */
     uint32_t permA = 0, permFrames = 0;
     std::vector<uint32_t> heavyInst;
     /* pool ray-order key (SURF_KEY): 2 heavy-instance mask x quadrant, most
@@ -403,6 +407,7 @@ int allocWavefront(surf_ctx* c) {
  * later, longer stream grows the ring; a window set by surf_set_frame_batch
  * is kept as given. */
 constexpr uint64_t kWindowFloor = 256, kLoopFloor = 1024;
+constexpr uint64_t kLdsLightBlas = 20480;     /* k_connect's staged emitter BLAS node records, bytes at most */
 int ensureWindow(surf_ctx* c, uint64_t frames, uint32_t spp) {
     const uint64_t passes = frames * spp;
     const uint64_t floor = frames == 1 ? kLoopFloor : kWindowFloor;
@@ -505,11 +510,17 @@ void launchPhase(surf_ctx* c, int ph, hipEvent_t* ev) {
     }
     if (ev) (void)hipEventRecord(ev[4], s0);
     const bool ldsC = c->ldsTables && !c->connectGlobal;   /* else global tables: LDS holds only the traversal stack */
+    /* the emitters' BLAS in LDS (S.sbNodeN > 0): after the stack and the tables, 16-B aligned */
+    const size_t stgLds = ((((size_t)sw * sizeof(uint16_t) + (size_t)c->nInstances * (sizeof(TraceInst) + sizeof(uint32_t))) + 15) & ~(size_t)15) +
+                          (size_t)c->S.sbNodeN * 64;
+    /* staged only where the copy still leaves 5 workgroups of 256 per CU (k_connect's residency) */
+    const bool stg = ldsC && !c->S.laneW && c->S.sbNodeN > 0u && stgLds * 5 <= 163840;
     auto connectK = c->S.laneW ? (ldsC ? k_connect<true, true> : k_connect<false, true>)
-                               : (ldsC ? k_connect<true, false> : k_connect<false, false>);
-    hipLaunchKernelGGL(connectK, dim3(c->gridConnect), dim3(kBlock),
-                       (ldsC ? traversalLds(c, kBlock) : (size_t)sw * sizeof(uint32_t)) + c->conLdsPad, s1, c->S, c->Q, c->rad, c->ctr,
-                       par, sw, qorder);
+                               : (ldsC ? (stg ? k_connect<true, false, true> : k_connect<true, false>) : k_connect<false, false>);
+    /* staged: 16-bit stack entries (half the stack's LDS) leave room for the
+     * copy beside 5 workgroups of 256 per CU, the residency k_connect runs at */
+    const size_t connectLds = (!ldsC ? (size_t)sw * sizeof(uint32_t) : stg ? stgLds : traversalLds(c, kBlock)) + c->conLdsPad;
+    hipLaunchKernelGGL(connectK, dim3(c->gridConnect), dim3(kBlock), connectLds, s1, c->S, c->Q, c->rad, c->ctr, par, sw, qorder);
     if (ovl) (void)hipEventRecord(c->capEv[2 * ph + 1], s1);
     if (ev) (void)hipEventRecord(ev[5], s0);
     hipLaunchKernelGGL(k_regen, dim3(c->gridRegen), dim3(kBlock), 0, s0, c->cam, c->pool[par ^ 1], c->rad, c->ctr, par,
@@ -1010,6 +1021,7 @@ int createCtx(int dev, uint32_t w, uint32_t h, std::vector<uint32_t> rows, surf_
     if (const char* e = std::getenv("SURF_LOOP_LAG")) c->loopLag = e[0] != '0';
     if (const char* e = std::getenv("SURF_EXT_LDS_PAD")) c->extLdsPad = (size_t)std::max(0, std::atoi(e));
     if (const char* e = std::getenv("SURF_CON_LDS_PAD")) c->conLdsPad = (size_t)std::max(0, std::atoi(e));
+    if (const char* e = std::getenv("SURF_LDS_LIGHTBLAS")) c->ldsLightBlas = e[0] != '0';
     if (const char* e = std::getenv("SURF_REORDER")) c->reorder = e[0] != '0';
     if (const char* e = std::getenv("SURF_TAIL_ROWS")) c->tailRows = e[0] == '1';
     if (const char* e = std::getenv("SURF_TAIL_PAIR")) c->tailPair = e[0] != '0';
@@ -1231,6 +1243,23 @@ void setKeys(surf_ctx* c, DevScene& S, const InstanceTables& T) {
         S.hvHi[h] = h < T.nHeavy ? T.hvHi[h] : make_float4(0, 0, 0, 0);
     }
     S.keyMode = T.nHeavy ? c->keyMode : 0u;
+    /* the emitters' BLAS, when every light instance uses one BLAS and its
+     * node records fit kLdsLightBlas bytes: k_connect stages them */
+    S.sbNode0 = S.sbNodeN = 0u;
+    if (c->ldsLightBlas && !T.lights.empty()) {
+        bool one = true;
+        const DevInstance* L0 = T.lights[0].x < T.inst.size() ? &T.inst[T.lights[0].x] : nullptr;
+        for (const uint2& L : T.lights)
+            one = one && L0 && L.x < T.inst.size() && T.inst[L.x].nodeOffset == L0->nodeOffset &&
+                  T.inst[L.x].idxOffset == L0->idxOffset && T.inst[L.x].triOffset == L0->triOffset;
+        const auto nr = one ? c->blasNodeRange.find(L0->nodeOffset) : c->blasNodeRange.end();
+        /* 16-bit stack entries: every BLAS and TLAS node index below 65536 */
+        const bool small = c->nBlasNodes < 65536u && T.tnodes.size() / 4 < 65536u;
+        if (small && nr != c->blasNodeRange.end() && nr->second[0] == L0->nodeOffset) {
+            const uint64_t nN = (uint64_t)nr->second[1] - nr->second[0] + 1;
+            if (nN * 64 <= kLdsLightBlas) { S.sbNode0 = nr->second[0]; S.sbNodeN = (uint32_t)nN; }
+        }
+    }
 }
 
 int buildInstanceTables(surf_ctx* c, const surf_gpu_instance* instances, uint32_t n, const uint32_t* tlasIdx,
@@ -1401,6 +1430,13 @@ int surf_upload_scene(surf_ctx* c, const surf_scene_desc* d) {
                 }
         }
     }
+    c->nBlasNodes = d->blas_node_count;
+    c->blasNodeRange.clear();
+    for (uint32_t k = 0; k < d->blas_node_count; ++k)
+        if (owner[k] != kUnset) {
+            auto it = c->blasNodeRange.emplace(owner[k], std::array<uint32_t, 2>{k, k}).first;
+            it->second[0] = std::min(it->second[0], k); it->second[1] = std::max(it->second[1], k);
+        }
     c->blasRoots.clear();
     for (uint32_t i = 0; i < d->instance_count; ++i) {
         const surf_gpu_instance& g = d->instances[i];

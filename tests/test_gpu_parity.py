@@ -290,6 +290,28 @@ def test_permuted_stream_continued_bitexact(oracle_scene, product_scene, monkeyp
     _assert_counts(st, cnt)
 
 
+@pytest.mark.parametrize("staged", ["1", "0"], ids=["light-blas-in-lds", "light-blas-global"])
+def test_connect_light_blas_staging_bitexact(oracle_scene, product_scene, staged, monkeypatch):
+    """k_connect with the emitters' BLAS node records staged in LDS (the lights'
+    instances walk them there, beside a 16-bit traversal stack; the default
+    for the bundled scene) and without (SURF_LDS_LIGHTBLAS=0): the same node
+    records and decisions, so radiance and event counts equal the oracle's."""
+    monkeypatch.setenv("SURF_LDS_LIGHTBLAS", staged)
+    W, H, F = 96, 64, 4
+    r = surf_amd.Renderer(product_scene, W, H)
+    r.render(F, 0, 0)
+    g = r.accumulator()
+    st = r.stats()
+    r.close()
+    oracle.set_zero_cutoff(True)
+    try:
+        c, cnt, _ = oracle_scene.render(W, H, F)
+    finally:
+        oracle.set_zero_cutoff(False)
+    _assert_bitexact(g, c, f"light BLAS staged={staged}")
+    _assert_counts(st, cnt)
+
+
 @pytest.mark.parametrize("cutoff", [None, True], ids=["reference-no-cutoff", "cutoff-on-both"])
 def test_render_spp4_per_frame_bitexact(oracle_scene, product_scene, cutoff):
     """Multi-sample frames (config().samplesPerFrame = 4; renderer.cpp:160-188):
