@@ -45,6 +45,22 @@ int main(int argc, char** argv) {
     double uniAct = 0;
     std::map<int,double> hist;
     std::map<uint32_t, double> instIters, instLanes, instTri;   /* per TLAS instance: wave steps, lane-steps, triangle tests */
+    /* node loads by breadth-first rank of the node in its BLAS (LOCKSTEP_BFS=1): how many a staged top-K prefix would serve */
+    std::map<const Bvh*, std::vector<uint32_t>> bfsRank;
+    std::vector<double> rankLoads(1 << 16, 0.0);
+    double allLoads = 0;
+    auto rankOf = [&](const Bvh& b) -> const std::vector<uint32_t>& {
+        auto it = bfsRank.find(&b);
+        if (it != bfsRank.end()) return it->second;
+        std::vector<uint32_t> r(b.nodes.size(), 0xffffffffu);
+        std::vector<uint32_t> q{0u}; r[0] = 0; uint32_t next = 1;
+        for (size_t h = 0; h < q.size(); ++h) {
+            const Node& nd = b.nodes[q[h]];
+            if (nd.cnt) continue;
+            for (uint32_t c = nd.lf; c <= nd.lf + 1; ++c) { r[c] = next++; q.push_back(c); }
+        }
+        return bfsRank.emplace(&b, std::move(r)).first->second;
+    };
     for (uint32_t g = 0; g + 64 <= n; g += 64) {
         V3 o[64], d[64]; float depth[64];
         bool occ[64];
@@ -87,6 +103,7 @@ int main(int argc, char** argv) {
                 hist[std::min<int>(ns.size(), 64)]++;
                 for (int l = 0; l < 64; ++l) if (act[l]) {
                     const Node& nd = b.nodes[node[l]];
+                    { const uint32_t rk = rankOf(b)[node[l]]; allLoads += 1; if (rk < rankLoads.size()) rankLoads[rk] += 1; }
                     bool pop = false;
                     if (nd.cnt) {
                         anyLeaf = true;
@@ -175,6 +192,13 @@ int main(int argc, char** argv) {
     for (auto& [ii, v] : instIters)
         printf("  instance %u (blas %zu nodes): wave steps per 64 rays %.2f, lanes per step %.1f, triangle tests per ray %.2f\n", ii,
                S.inst[ii].blas->bvh.nodes.size(), v / (n / 64), instLanes[ii] / v, instTri[ii] / n);
+    if (getenv("LOCKSTEP_BFS")) {
+        double cum = 0; size_t k = 0;
+        for (size_t K : {15, 31, 63, 127, 255, 511, 1023}) {
+            for (; k < K && k < rankLoads.size(); ++k) cum += rankLoads[k];
+            printf("  node loads at BFS rank < %zu: %.3f\n", K, cum / allLoads);
+        }
+    }
     printf("groups %u iters/group %.1f active/iter %.1f distinct nodes/iter %.2f uniform iters %.3f (lanes in uniform iters %.3f of node loads)\n",
            n / 64, iters / (n / 64), active / iters, distinct / iters, uniform / iters, uniAct / nodeLoads);
     printf("leaf iters %.3f tri loads/iter-with-leaf %.1f distinct tris %.1f\n", leafIters / iters, triLoads / leafIters, triDistinct / leafIters);
