@@ -294,7 +294,9 @@ public:
 /* ------------------------------------------------------------ renderer */
 struct RendererConfig {
     U32 maxBounces = 5;          /* unused by the reference's iterative path; kept */
-    U32 samplesPerFrame = 1;
+    U32 samplesPerFrame = 1;     /* > 1: the throughput cutoff is off (surf_set_zero_cutoff's automatic default), so a
+                                    lens TIR orbit runs to its end as in the reference -- up to millions of segments
+                                    (seconds) for the frame holding it; maxSegments bounds it (surf_hip.h) */
     U32 maxSegments = 0;         /* 0: unbounded + Russian roulette (reference); N: cap (config C2) */
     bool lumenOutput = false;    /* WF_LUMEN_OUTPUT (renderer.cpp:31, default 0): frameInfo().energy from the
                                     accumulator; reading it drains the sample stream, so it is computed only

@@ -157,6 +157,9 @@ void surf_destroy(surf_ctx* ctx);
 const char* surf_last_error(const surf_ctx* ctx);   /* ctx may be NULL: last global error */
 /* Rows of this shard in shard order (row_count from surf_shard_rows(ctx, NULL, &n)). */
 int surf_shard_rows(const surf_ctx* ctx, uint32_t* rows, uint32_t* row_count);
+/* The HIP device the context was created on (the multi-GPU gather allocates
+ * its buffers and streams there, whatever device the calling thread has set). */
+int surf_get_device(const surf_ctx* ctx, int* hip_device);
 /* The rows shard shard_index of shard_count owns under surf_create_sharded's
  * rule, in shard order (rows may be NULL to get the count).  Host only. */
 int surf_shard_row_list(uint32_t height, uint32_t shard_index, uint32_t shard_count, uint32_t row_block, uint32_t* rows,
@@ -196,7 +199,14 @@ int surf_set_frame_batch(surf_ctx* ctx, uint32_t frames);
  * parity tests compare the GPU with the cutoff against the oracle without it,
  * bit for bit, on every tested image); n_ext/n_cont/... shrink.  It ends the
  * total-internal-reflection orbits in the glass lens that the reference traces
- * for up to millions of segments at a denormal throughput. */
+ * for up to millions of segments at a denormal throughput.
+ * Stall risk with the cutoff off -- the automatic default for multi-sample
+ * frames, e.g. a drop-in Renderer whose samplesPerFrame is above 1: such an
+ * orbit runs to its end as in the reference (13,104,648 segments for one C3
+ * path, frame 143, pixel 205912 at 1280x720 -- seconds of drain for the frame
+ * holding it).  Bound it with max_segments (surf_render; a deviation, the
+ * capped paths are counted and listed by surf_debug_capped) or enable the
+ * cutoff (a deviation for multi-sample frames, see above). */
 int surf_set_zero_cutoff(surf_ctx* ctx, int enabled);
 /* Drain policy: when no new sample may be issued and at most `threshold_paths`
  * paths are in flight, the tail kernel finishes them in stages: each stage

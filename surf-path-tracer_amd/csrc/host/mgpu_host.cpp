@@ -66,7 +66,10 @@ int setupRank(surf_ctx* shard, uint32_t width, uint32_t height, uint32_t index, 
         m->maxRows = std::max(m->maxRows, n);
     }
     m->rows = mine;
-    hipError_t e = hipGetDevice(&m->device);
+    /* the shard's own device, not the calling thread's current one: a single
+     * thread sets up every rank of surf_mgpu_create_all */
+    if ((rc = surf_get_device(shard, &m->device))) { delete m; return rc; }
+    hipError_t e = hipSetDevice(m->device);
     const size_t slab = (size_t)m->maxRows * width * 4;
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipMalloc(&m->dSend, slab * sizeof(float));
@@ -83,10 +86,14 @@ int stage(surf_mgpu* m) {
     return surf_copy_accumulator_device(m->shard, m->dSend);
 }
 
+/* Every rank waits for its gather before returning, the root too when it
+ * passes no frame: the next gather's stage() rewrites dSend through the shard's
+ * stream, which does not order against m->stream. */
 int finishRoot(surf_mgpu* root, float* frame) {
-    if (!frame) return SURF_OK;
     hipError_t e = hipSetDevice(root->device);
     if (e == hipSuccess) e = hipStreamSynchronize(root->stream);
+    if (e != hipSuccess) return hipFail("gather", e);
+    if (!frame) return SURF_OK;
     std::vector<float> gathered((size_t)root->count * root->maxRows * root->width * 4);
     if (e == hipSuccess)
         e = hipMemcpy(gathered.data(), root->dRecv, gathered.size() * sizeof(float), hipMemcpyDeviceToHost);
@@ -136,9 +143,16 @@ int surf_mgpu_create_all(surf_ctx* const* shards, uint32_t count, uint32_t width
     std::vector<int> devs(count);
     for (uint32_t k = 0; k < count; ++k) {
         out[k] = nullptr;
+        int rc = surf_get_device(shards[k], &devs[k]);
+        if (rc) return fail(rc, "shard " + std::to_string(k) + ": no context");
+        for (uint32_t j = 0; j < k; ++j)   /* one rank per GPU (RCCL refuses duplicate devices in one communicator) */
+            if (devs[j] == devs[k])
+                return fail(SURF_ERR_INVALID, "shards " + std::to_string(j) + " and " + std::to_string(k) + " share HIP device " +
+                                                  std::to_string(devs[k]));
+    }
+    for (uint32_t k = 0; k < count; ++k) {
         int rc = setupRank(shards[k], width, height, k, count, rowBlock, &out[k]);
         if (rc) { for (uint32_t j = 0; j < k; ++j) { surf_mgpu_destroy(out[j]); out[j] = nullptr; } return rc; }
-        devs[k] = out[k]->device;
     }
     std::vector<ncclComm_t> comms(count);
     const ncclResult_t r = ncclCommInitAll(comms.data(), (int)count, devs.data());
@@ -157,11 +171,7 @@ int surf_mgpu_gather(surf_mgpu* m, float* frame) {
     const size_t slab = (size_t)m->maxRows * m->width * 4;
     const ncclResult_t r = ncclGather(m->dSend, m->dRecv, slab, ncclFloat32, 0, m->comm, m->stream);
     if (r != ncclSuccess) return rcclFail("ncclGather", r);
-    if (m->index != 0) {
-        const hipError_t e = hipStreamSynchronize(m->stream);
-        return e == hipSuccess ? SURF_OK : hipFail("gather", e);
-    }
-    return finishRoot(m, frame);
+    return finishRoot(m, m->index == 0 ? frame : nullptr);
 }
 
 int surf_mgpu_gather_all(surf_mgpu* const* ms, uint32_t count, float* frame) {
@@ -172,12 +182,15 @@ int surf_mgpu_gather_all(surf_mgpu* const* ms, uint32_t count, float* frame) {
         if (rc) return rc;
     }
     ncclResult_t r = ncclGroupStart();
+    bool devOk = true;
     for (uint32_t k = 0; k < count && r == ncclSuccess; ++k) {
-        if (hipSetDevice(ms[k]->device) != hipSuccess) return fail(SURF_ERR_HIP, "hipSetDevice");
+        /* never leave the group open: a failed device switch stops issuing, the group still ends */
+        if (hipSetDevice(ms[k]->device) != hipSuccess) { devOk = false; break; }
         const size_t slab = (size_t)ms[k]->maxRows * ms[k]->width * 4;
         r = ncclGather(ms[k]->dSend, ms[k]->dRecv, slab, ncclFloat32, 0, ms[k]->comm, ms[k]->stream);
     }
     const ncclResult_t e = ncclGroupEnd();
+    if (!devOk) return fail(SURF_ERR_HIP, "hipSetDevice");
     if (r != ncclSuccess) return rcclFail("ncclGather", r);
     if (e != ncclSuccess) return rcclFail("ncclGroupEnd", e);
     for (uint32_t k = 1; k < count; ++k) {

@@ -1118,6 +1118,12 @@ int surf_shard_rows(const surf_ctx* c, uint32_t* rows, uint32_t* count) {
     return SURF_OK;
 }
 
+int surf_get_device(const surf_ctx* c, int* dev) {
+    if (!c || !dev) return SURF_ERR_INVALID;
+    *dev = c->device;
+    return SURF_OK;
+}
+
 int surf_shard_row_list(uint32_t height, uint32_t shard, uint32_t shards, uint32_t block, uint32_t* rows, uint32_t* count) {
     if (!count || shards == 0 || shard >= shards) return fail(nullptr, SURF_ERR_INVALID, "bad shard index");
     const std::vector<uint32_t> r = shardRows(height, shard, shards, block);

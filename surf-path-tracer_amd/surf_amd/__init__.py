@@ -95,7 +95,7 @@ def load() -> C.CDLL:
         "surf_create": ([I32, U32, U32, U32, U32, C.POINTER(P)], I32),
         "surf_create_sharded": ([I32, U32, U32, U32, U32, U32, C.POINTER(P)], I32),
         "surf_destroy": ([P], None), "surf_last_error": ([P], C.c_char_p),
-        "surf_shard_rows": ([P, P, C.POINTER(U32)], I32),
+        "surf_shard_rows": ([P, P, C.POINTER(U32)], I32), "surf_get_device": ([P, C.POINTER(I32)], I32),
         "surf_shard_row_list": ([U32, U32, U32, U32, P, C.POINTER(U32)], I32),
         "surf_pack_rgba8": ([P, U32, F, I32, P], I32),
         "surf_set_pool_capacity": ([P, U32], I32), "surf_set_frame_batch": ([P, U32], I32),
@@ -172,9 +172,20 @@ def assemble_slabs(width: int, height: int, shards: int, row_block: int, gathere
     if g.ndim != 4 or g.shape[0] != shards or g.shape[2] != width or g.shape[3] != 4:
         raise ValueError(f"gathered shape {g.shape} is not ({shards}, rows, {width}, 4)")
     out = np.zeros((height, width, 4), np.float32)
-    rc = load_mgpu().surf_mgpu_assemble(width, height, shards, row_block, g.ctypes.data, g.shape[1], out.ctypes.data)
+    try:
+        mg = load_mgpu()
+    except OSError:
+        # libsurf_mgpu.so (it links RCCL) not built or not loadable: the same
+        # un-permute on the host in numpy -- a torch.distributed gather does not need RCCL's library
+        for k in range(shards):
+            rows = shard_rows(height, ShardSpec(k, shards, row_block))
+            if len(rows) > g.shape[1]:
+                raise ValueError(f"slab smaller than shard {k}")
+            out[rows] = g[k, :len(rows)]
+        return out
+    rc = mg.surf_mgpu_assemble(width, height, shards, row_block, g.ctypes.data, g.shape[1], out.ctypes.data)
     if rc != SURF_OK:
-        raise SurfError(rc, "surf_mgpu_assemble", load_mgpu().surf_mgpu_last_error().decode())
+        raise SurfError(rc, "surf_mgpu_assemble", mg.surf_mgpu_last_error().decode())
     return out
 
 

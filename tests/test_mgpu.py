@@ -44,6 +44,31 @@ def test_native_assemble_matches_python(height, shards, block):
         surf_amd.assemble_slabs(W, height, shards, block, slabs[:, :0] if maxr else slabs)
 
 
+def test_assemble_without_mgpu_library(monkeypatch):
+    """A torch.distributed gather needs no RCCL library of ours: without
+    libsurf_mgpu.so the un-permute runs in numpy, with the same result."""
+    W, height, shards, block = 9, 37, 3, 4
+    rng = np.random.default_rng(5)
+    slabs = rng.standard_normal((shards, 13, W, 4)).astype(np.float32)
+    want = surf_amd.assemble_slabs(W, height, shards, block, slabs)
+
+    def missing():
+        raise OSError("libsurf_mgpu.so not built")
+    monkeypatch.setattr(surf_amd, "load_mgpu", missing)
+    got = surf_amd.assemble_slabs(W, height, shards, block, slabs)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+    with pytest.raises(ValueError):
+        surf_amd.assemble_slabs(W, height, shards, block, slabs[:, :5])
+
+
+def test_ctx_device_getter_is_exported():
+    import ctypes as C
+    lib = surf_amd.load()
+    dev = C.c_int(-7)
+    assert lib.surf_get_device(None, C.byref(dev)) == -1   # SURF_ERR_INVALID
+    assert dev.value == -7
+
+
 def test_host_pack_rgba8_matches_oracle():
     rng = np.random.default_rng(3)
     acc = (rng.standard_normal((4096, 4)) * 3.0).astype(np.float32)
