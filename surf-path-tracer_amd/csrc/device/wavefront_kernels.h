@@ -93,9 +93,13 @@ struct DevScene {
     const DevMaterial* mats;
     const uint2* lights;      /* (instance, primitive count) */
     uint32_t nLights;
-    /* the emitters' BLAS whose node records [sbNode0, sbNode0 + sbNodeN)
-     * k_connect stages in LDS (sbNodeN = 0: none) */
-    uint32_t sbNode0, sbNodeN;
+    /* the emitters' BLAS k_connect stages in LDS (sbRecN = 0: none): the
+     * instances whose BLAS root is node sbNode0 walk its sbRecN interior records
+     * in compact form (sbRec: the children's boxes, each child an interior
+     * record index or a leaf's triangle range -- no leaf records) and its sbTriN
+     * triangle slots (S.tris + 3 * sbTri0) from LDS */
+    uint32_t sbNode0, sbRecN, sbTri0, sbTriN;
+    const float4* sbRec;
     uint32_t nInst, nMats;
     uint32_t tlasLeafCount;   /* TLAS root is a leaf with this many instances (0: general TLAS) */
     uint32_t finiteBoxes;     /* every BLAS node box is finite: slabFinite is exact */
@@ -126,10 +130,14 @@ struct Pool { float4* od; float4* T; uint8_t* key; };
 /* Where a path that used up its segment budget goes. */
 struct Sink { Pool q; uint32_t* n; uint32_t cap; };
 /* Shadow queue: od[2i] = (origin, tmax), od[2i + 1] = (direction, sample id)
- * -- the ray k_connect traverses is one 32-B piece of one cache line, also
- * when gathered through the shadow order -- c[i] = (T * Ld, 0), read only for
- * an unoccluded ray; key[i] = ray-order bin. */
-struct ShadowQ { float4* od; float4* c; uint8_t* key; };
+ * -- the ray k_connect traverses is one 32-B piece of one cache line --
+ * c[i] = (T * Ld, 0), read only for an unoccluded ray.  k_shade appends each
+ * shadow ray straight into the region of its order bin (shadowKey: kShBins
+ * regions of `region` slots, then an overflow region of the pool's capacity
+ * for a bin that outgrows its region), so k_connect reads the rays in bin
+ * order sequentially: no sort pass and no gather through an order array. */
+constexpr uint32_t kShBins = 16;     /* shadow-ray order bins: light slot (mod 2) x octant cell */
+struct ShadowQ { float4* od; float4* c; uint32_t region; uint32_t bins; };
 
 /* Device counters of the sample stream.  Double-buffered by phase parity so no
  * kernel writes a word another block of the same launch still reads. */
@@ -162,6 +170,10 @@ struct Counters {
      * atomics (~12 ns each, measured); totals = ev + sum over stripes */
     unsigned long long evS[32][16];
     unsigned long long dbg[8];       /* SURF_SEG_TIMING builds: k_tail_coop cycles (extend, shade, connect, segments) */
+    /* shadow-queue cursors by phase parity: bins 0..kShBins-1 (may count past
+     * their region: the excess went to the overflow region), then the overflow
+     * region's; one 128-B line each (same-line atomics serialize) */
+    uint32_t shCur[2][kShBins + 1][32];
 };
 constexpr uint32_t kStripes = 32;    /* frameDone and event-count stripes */
 constexpr int kEvents = 9;           /* event kinds counted (ev / evS index) */
@@ -290,11 +302,65 @@ __device__ __forceinline__ float boxDist(float4 lo, float4 hi, V3 o, V3 rd, floa
                : slab(lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, o, rd, depth);
 }
 
+/* Any-hit walk of the emitters' BLAS staged in LDS (k_connect, S.sbRecN):
+ * record r = (L.min, refL), (L.max, refR), (R.min, -), (R.max, -) of interior
+ * node r (root 0); a child reference is an interior record index or, for a
+ * leaf, kLeafTag | count << 16 | leftFirst into the staged triangles (v0, e1,
+ * e2 per BVH slot, after the records).  The reference's box tests at the
+ * fixed shadow-ray depth decide which leaves are tested (a leaf is box-tested
+ * at its parent and never again, bvh.cpp:193-253); the answer is an OR over
+ * them, so testing a hit leaf's triangles as soon as its parent is visited --
+ * no leaf record, no stack entry -- returns what blasTrace<true> does. */
+constexpr uint32_t kLeafTagC = 0x80000000u;
+__device__ __forceinline__ bool leafAnyStaged(const float4* sT, uint32_t ref, V3 o, V3 d, float depth) {
+    const uint32_t cnt = (ref >> 16) & 0x7fffu, lf = ref & 0xffffu;
+    for (uint32_t k = 0; k < cnt; ++k) {
+        const float4* tp = sT + 3u * (lf + k);
+        const float4 a = tp[0], b = tp[1], c = tp[2];
+        float dd = depth, u, v;
+        if (triHit(xyz(a), xyz(b), xyz(c), o, d, dd, u, v)) return true;
+    }
+    return false;
+}
+template <bool FIN, typename SK>
+__device__ __forceinline__ bool blasAnyStaged(uint32_t recN, const float4* sR, V3 o, V3 d, V3 rd, float depth, SK* stk,
+                                              uint32_t stride, uint32_t base) {
+    const float4* sT = sR + 4u * recN;
+    SK* const bottom = stk + base * stride;
+    SK* sp = bottom;
+    uint32_t node = 0u;
+    for (;;) {
+        const float4* nd = sR + 4u * node;
+        const float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
+        const uint32_t rl = f2u(q0.w), rr = f2u(q1.w);
+        bool hl = boxDist<FIN>(q0, q1, o, rd, depth) != kFarAway;
+        bool hr = boxDist<FIN>(q2, q3, o, rd, depth) != kFarAway;
+        if (hl && (rl & kLeafTagC)) {
+            if (leafAnyStaged(sT, rl, o, d, depth)) return true;
+            hl = false;
+        }
+        if (hr && (rr & kLeafTagC)) {
+            if (leafAnyStaged(sT, rr, o, d, depth)) return true;
+            hr = false;
+        }
+        if (hl) {
+            node = rl;
+            if (hr) { *sp = (SK)rr; sp += stride; }
+        } else if (hr) {
+            node = rr;
+        } else {
+            if (sp == bottom) return false;
+            sp -= stride;
+            node = *sp;
+        }
+    }
+}
+
 /* FIN: o, rd and every box finite (slabFinite is exact); else the reference's
  * ternary slab with its NaN behaviour. */
-/* STG: the BLAS is the one whose node records are staged in LDS (S.sbNode0,
- * sN) -- the same records, so the same decisions and results.  SK: the stack
- * entry type (16-bit when every node index fits). */
+/* STG: the BLAS is the emitters' one staged in LDS (S.sbNode0, sN; any-hit
+ * only: blasAnyStaged).  SK: the stack entry type (16-bit when every node
+ * index fits). */
 template <bool ANY, bool FIN, bool STG = false, typename SK = uint32_t>
 __device__ __forceinline__ bool blasTrace(const DevScene& S, const TraceInst& I, V3 o, V3 d, V3 rd, float& depth,
                                           float& hu, float& hv, uint32_t& hprim,
@@ -305,6 +371,7 @@ __device__ __forceinline__ bool blasTrace(const DevScene& S, const TraceInst& I,
     const float4 r0 = I.r0, r1 = I.r1;
     const uint32_t rlf = f2u(r0.w), rcnt = f2u(r1.w);
     if (rcnt != 0u) return leafTestUniform<ANY>(tri, rlf, rcnt, o, d, depth, hu, hv, hprim);
+    if constexpr (STG && ANY) return blasAnyStaged<FIN, SK>(S.sbRecN, sN, o, d, rd, depth, stk, stride, base);
     /* stack pointer walks in steps of `stride` words (lane-interleaved LDS) */
     SK* const bottom = stk + base * stride;
     SK* sp = bottom;
@@ -329,7 +396,7 @@ __device__ __forceinline__ bool blasTrace(const DevScene& S, const TraceInst& I,
         }
     }
     for (;;) {
-        const float4* nd = STG ? sN + 4u * (node - S.sbNode0) : S.nodes + 4u * node;
+        const float4* nd = S.nodes + 4u * node;
         float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
         pin(q0); pin(q1); pin(q2); pin(q3);
         const uint32_t lf = f2u(q0.w), cnt = f2u(q1.w);
@@ -2261,6 +2328,13 @@ __global__ __launch_bounds__(kBlock, SURF_SHADE_WAVES) void k_shade(DevScene S, 
      * block's continuation and shadow slots (LDS double-buffered by iteration) */
     __shared__ uint32_t sWave[2][kBlock / 64][2];
     __shared__ uint32_t sBase[2][2];
+    /* shadow rays per bin of the iteration (a lane's LDS atomic returns its rank
+     * in its bin) and each bin's reservation: region base, the part that fits
+     * the region, the overflow base of the rest */
+    __shared__ uint32_t sShCnt[2][kShBins];
+    __shared__ uint32_t sShBase[2][kShBins], sShOk[2][kShBins], sShOv[2][kShBins];
+    if (threadIdx.x < 2u * kShBins) (&sShCnt[0][0])[threadIdx.x] = 0u;
+    __syncthreads();
     const uint32_t n = C->nIn[par];
     const uint32_t maxSeg = C->maxSeg, zeroCutoff = C->zeroCutoff, spp = C->spp;
     const uint32_t wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
@@ -2290,6 +2364,11 @@ __global__ __launch_bounds__(kBlock, SURF_SHADE_WAVES) void k_shade(DevScene S, 
         }
         const unsigned long long mCont = __ballot(r.cont || r.next), mSh = __ballot(r.shadow);
         if (laneId() == 0) { sWave[it][wv][0] = (uint32_t)__popcll(mCont); sWave[it][wv][1] = (uint32_t)__popcll(mSh); }
+        /* the shadow ray's bin -- toward the same light from the same octant of
+         * the scene -- and its rank among the iteration's rays of that bin */
+        const uint32_t kb = r.shadow ? (Q.bins > 1u ? shadowKey(S, r.light, r.so) : 0u) : kShBins;
+        uint32_t rk = 0;
+        if (r.shadow) rk = atomicAdd(&sShCnt[it][kb], 1u);
         __syncthreads();
         if (threadIdx.x == 0) {
             unsigned long long tc = 0, ts = 0;
@@ -2297,19 +2376,32 @@ __global__ __launch_bounds__(kBlock, SURF_SHADE_WAVES) void k_shade(DevScene S, 
             const unsigned long long old = (tc | ts) ? atomicAdd(&C->app[par], (ts << 32) | tc) : 0ull;
             sBase[it][0] = (uint32_t)old; sBase[it][1] = (uint32_t)(old >> 32);
         }
+        if (threadIdx.x < kShBins) {
+            /* one reservation per (iteration, non-empty bin); what does not fit
+             * the bin's region goes to the overflow region */
+            const uint32_t tot = sShCnt[it][threadIdx.x];
+            sShCnt[it ^ 1u][threadIdx.x] = 0u;     /* the next iteration's counts (last read an iteration ago) */
+            uint32_t b0 = 0, ok = 0, ov = 0;
+            if (tot) {
+                b0 = atomicAdd(&C->shCur[par][threadIdx.x][0], tot);
+                ok = b0 >= Q.region ? 0u : min(tot, Q.region - b0);
+                if (ok < tot) ov = atomicAdd(&C->shCur[par][kShBins][0], tot - ok);
+            }
+            sShBase[it][threadIdx.x] = b0; sShOk[it][threadIdx.x] = ok; sShOv[it][threadIdx.x] = ov;
+        }
         __syncthreads();
-        uint32_t jc = sBase[it][0], js = sBase[it][1];
-        for (uint32_t k = 0; k < wv; ++k) { jc += sWave[it][k][0]; js += sWave[it][k][1]; }
+        uint32_t jc = sBase[it][0];
+        for (uint32_t k = 0; k < wv; ++k) jc += sWave[it][k][0];
         jc += rankBelow(mCont);
-        js += rankBelow(mSh);
         if (r.cont || r.next) {
             stS(&nxt.od[2u * (jc)], r.o); stS(&nxt.od[2u * (jc) + 1u], r.d); stS(&nxt.T[jc], r.T);
             /* starts on the instance it hit, from this quadrant; camera rays in their own bin */
             nxt.key[jc] = r.next ? (uint8_t)(kBins - 1u) : poolKey(S, hinst, r.o, r.d);
         }
         if (r.shadow) {
+            const uint32_t ok = sShOk[it][kb];
+            const uint32_t js = rk < ok ? kb * Q.region + sShBase[it][kb] + rk : kShBins * Q.region + sShOv[it][kb] + (rk - ok);
             stS(&Q.od[2u * js], r.so); stS(&Q.od[2u * js + 1u], r.sd); stS(&Q.c[js], r.sc);
-            Q.key[js] = shadowKey(S, r.light, r.so);       /* toward the same light from the same octant of the scene */
         }
         /* a path that ends here may still have this phase's shadow ray pending:
          * connect runs before the host reads frameDone (end of the phase). */
@@ -2325,12 +2417,31 @@ __global__ __launch_bounds__(kBlock, SURF_SHADE_WAVES) void k_shade(DevScene S, 
     blockCount<5>(C, {1, 2, 3, 4, 7}, {cHit, cCont, cSh, cAcc, cCap});
 }
 
+/* Where shadow ray i of the bin order lives: the bins' regions in bin order,
+ * then the overflow region (pre: the first ray index of each, kShBins + 2
+ * entries, the last = the count). */
+__device__ __forceinline__ uint32_t shadowSlot(const ShadowQ& Q, const uint32_t* pre, uint32_t i) {
+    uint32_t b = 0;
+    while (b < kShBins && i >= pre[b + 1]) ++b;
+    return b * Q.region + (i - pre[b]);
+}
+
 template <bool LDS, bool LW = false, bool STG = false>
 __global__ __launch_bounds__(kBlock, STG ? 5 : SURF_TRACE_WAVES) void k_connect(DevScene S, ShadowQ Q, float4* __restrict__ rad, Counters* C, int par,
-                                                    uint32_t stackWords, const uint32_t* __restrict__ order) {
+                                                    uint32_t stackWords) {
     extern __shared__ uint32_t lds[];
     const uint32_t n = (uint32_t)(C->app[par] >> 32);
     if (blockIdx.x * blockDim.x >= n) return;               /* no shadow rays for this block */
+    __shared__ uint32_t sPre[kShBins + 2];
+    if (threadIdx.x == 0) {
+        uint32_t run = 0;
+        for (uint32_t b = 0; b <= kShBins; ++b) {
+            sPre[b] = run;
+            run += min(C->shCur[par][b][0], b < kShBins ? Q.region : 0xffffffffu);
+        }
+        sPre[kShBins + 1] = run;     /* == n */
+    }
+    __syncthreads();
     /* STG: the emitters' BLAS node records (every unoccluded shadow ray walks
      * that BLAS down to its sampled triangle) staged after a stack of 16-bit
      * entries (every node index < 65536) and the trace tables; stageTrace's
@@ -2339,7 +2450,9 @@ __global__ __launch_bounds__(kBlock, STG ? 5 : SURF_TRACE_WAVES) void k_connect(
     float4* sN = nullptr;
     if (STG) {
         sN = reinterpret_cast<float4*>(lds + ((stackWordsUsed + S.nInst * (uint32_t)((sizeof(TraceInst) + 4u) / 4u) + 3u) & ~3u));
-        for (uint32_t k = threadIdx.x; k < 4u * S.sbNodeN; k += blockDim.x) sN[k] = S.nodes[4u * S.sbNode0 + k];
+        for (uint32_t k = threadIdx.x; k < 4u * S.sbRecN; k += blockDim.x) sN[k] = S.sbRec[k];
+        float4* const sT = sN + 4u * S.sbRecN;
+        for (uint32_t k = threadIdx.x; k < 3u * S.sbTriN; k += blockDim.x) sT[k] = S.tris[3u * S.sbTri0 + k];
     }
     const TraceTables Tt = traceTables<LDS>(S, lds, stackWordsUsed);
     const uint32_t stride = blockDim.x;
@@ -2350,7 +2463,7 @@ __global__ __launch_bounds__(kBlock, STG ? 5 : SURF_TRACE_WAVES) void k_connect(
         const uint32_t i0 = base + threadIdx.x;
         bool unocc = false;
         if (i0 < n) {
-            const uint32_t i = order ? order[i0] : i0;
+            const uint32_t i = shadowSlot(Q, sPre, i0);
             const float4 o = ldS(&Q.od[2u * i]), d = ldS(&Q.od[2u * i + 1u]);
             float depth = o.w, u = 0.0f, v = 0.0f;
             uint32_t inst = kUnset, prim = kUnset;
@@ -2420,6 +2533,7 @@ __global__ __launch_bounds__(kBlock) void k_regen(DevCamera cam, Pool nxt, float
         C->nIn[nx] = cont + nnew;
         C->issued[nx] = iss + nnew;
         C->app[nx] = 0ull;             /* next phase's append cursors */
+        for (uint32_t b = 0; b <= kShBins; ++b) C->shCur[nx][b][0] = 0u;
         C->ev[0] += cont + nnew;     /* extension rays of the next phase */
         C->ev[8] += cont + nnew;     /* ... traced by k_extend unless the drain takes the pool */
     }

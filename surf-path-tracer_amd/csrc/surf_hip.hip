@@ -101,7 +101,10 @@ struct surf_ctx {
     /* k_connect stages the emitters' BLAS node records in LDS when they are
      * few and every BLAS node index fits 16 bits (SURF_LDS_LIGHTBLAS=0: never) */
     bool ldsLightBlas = true;
-    std::map<uint32_t, std::array<uint32_t, 2>> blasNodeRange;   /* BLAS node offset -> [first, last] reachable node */
+    /* small BLASes in the compact form k_connect stages (blasAnyStaged): BLAS
+     * node offset -> interior records on the device, their count, index offset, triangle slots */
+    struct StagedBlas { const float4* rec; uint32_t recN, tri0, triN; };
+    std::map<uint32_t, StagedBlas> stagedBlas;
     uint32_t permA = 0, permFrames = 0;
     std::vector<uint32_t> heavyInst;
     /* pool ray-order key (SURF_KEY): 2 heavy-instance mask x quadrant, most
@@ -167,8 +170,6 @@ struct surf_ctx {
     bool overlap = true;
     hipStream_t side = nullptr;
     hipEvent_t capEv[2 * kPhasesPerGraph] = {};
-    uint32_t* orderQ = nullptr;
-    uint32_t* binHistQ = nullptr;
     uint32_t tailLanes = 0;
     uint32_t segMaxBase = 0;       /* longest path of finished streams */
     uint64_t tailFirstRays = 0;    /* first extension rays of drained paths: counted by regen, traced by the tail */
@@ -344,9 +345,7 @@ int allocWavefront(surf_ctx* c) {
     }
     if ((rc = devAlloc(c, c->wfAllocs, &c->order, cap))) return rc;
     if ((rc = devAlloc(c, c->wfAllocs, &c->binHist, (size_t)kBins * kSortBlocks))) return rc;
-    if ((rc = devAlloc(c, c->wfAllocs, &c->orderQ, cap))) return rc;
     if ((rc = devAlloc(c, c->wfAllocs, &c->dPerm, c->npx))) return rc;
-    if ((rc = devAlloc(c, c->wfAllocs, &c->binHistQ, (size_t)kBins * kSortBlocks))) return rc;
     /* grid: 8 workgroups of 256 per CU saturate the 256-CU chip; grid-stride beyond */
     int cus = 256;
     hipDeviceProp_t prop;
@@ -359,9 +358,14 @@ int allocWavefront(surf_ctx* c) {
     }
     if ((rc = devAlloc(c, c->wfAllocs, &c->hitTUV, cap))) return rc;
     if ((rc = devAlloc(c, c->wfAllocs, &c->hitInst, cap))) return rc;
-    if ((rc = devAlloc(c, c->wfAllocs, &c->Q.od, 2 * cap))) return rc;
-    if ((rc = devAlloc(c, c->wfAllocs, &c->Q.c, cap))) return rc;
-    if ((rc = devAlloc(c, c->wfAllocs, &c->Q.key, cap))) return rc;
+    /* shadow queue: kShBins bin regions of a quarter pool each (a phase queues
+     * at most one shadow ray per path; C3 puts <= 30 % of them in one bin), then
+     * an overflow region of a whole pool */
+    c->Q.region = (uint32_t)((cap / 4 + 255) / 256 * 256);
+    c->Q.bins = (c->sortRays && c->sortShadow) ? kShBins : 1u;
+    const size_t qslots = (size_t)kShBins * c->Q.region + cap;
+    if ((rc = devAlloc(c, c->wfAllocs, &c->Q.od, 2 * qslots))) return rc;
+    if ((rc = devAlloc(c, c->wfAllocs, &c->Q.c, qslots))) return rc;
     if ((rc = devAlloc(c, c->wfAllocs, &c->ctr, 1))) return rc;
     if ((rc = devAlloc(c, c->wfAllocs, &c->dOutRGBA, c->npx))) return rc;
     if (hipHostMalloc((void**)&c->hctr, sizeof(Counters), hipHostMallocDefault) != hipSuccess)
@@ -409,7 +413,7 @@ int allocWavefront(surf_ctx* c) {
  * later, longer stream grows the ring; a window set by surf_set_frame_batch
  * is kept as given. */
 constexpr uint64_t kWindowFloor = 256, kLoopFloor = 1024;
-constexpr uint64_t kLdsLightBlas = 20480;     /* k_connect's staged emitter BLAS node records, bytes at most */
+constexpr uint64_t kLdsLightBlas = 20480;     /* k_connect's staged emitter BLAS (compact records + triangles), bytes at most */
 int ensureWindow(surf_ctx* c, uint64_t frames, uint32_t spp) {
     const uint64_t passes = frames * spp;
     const uint64_t floor = frames == 1 ? kLoopFloor : kWindowFloor;
@@ -504,25 +508,22 @@ void launchPhase(surf_ctx* c, int ph, hipEvent_t* ev) {
         (void)hipEventRecord(c->capEv[2 * ph], s0);
         (void)hipStreamWaitEvent(s1, c->capEv[2 * ph], 0);
     }
-    /* shadow rays toward the same light together */
-    const uint32_t* qorder = nullptr;
-    if (c->sortRays && c->sortShadow) {
-        launchSort(c, c->Q.key, par, 1, s1, ovl ? c->binHistQ : c->binHist, ovl ? c->orderQ : c->order);
-        qorder = ovl ? c->orderQ : c->order;
-    }
+    /* (the shadow rays are already in bin order: k_shade appends each to its
+     * bin's region of the queue -- no sort pass) */
     if (ev) (void)hipEventRecord(ev[4], s0);
     const bool ldsC = c->ldsTables && !c->connectGlobal;   /* else global tables: LDS holds only the traversal stack */
-    /* the emitters' BLAS in LDS (S.sbNodeN > 0): after the stack and the tables, 16-B aligned */
+    /* the emitters' BLAS in LDS (S.sbRecN > 0): after the stack and the tables, 16-B aligned */
     const size_t stgLds = ((((size_t)sw * sizeof(uint16_t) + (size_t)c->nInstances * (sizeof(TraceInst) + sizeof(uint32_t))) + 15) & ~(size_t)15) +
-                          (size_t)c->S.sbNodeN * 64;
-    /* staged only where the copy still leaves 5 workgroups of 256 per CU (k_connect's residency) */
-    const bool stg = ldsC && !c->S.laneW && c->S.sbNodeN > 0u && stgLds * 5 <= 163840;
+                          (size_t)c->S.sbRecN * 64 + (size_t)c->S.sbTriN * 48;
+    /* staged only where the copy still leaves 5 workgroups of 256 per CU
+     * (k_connect's residency; 144 B of static LDS each) */
+    const bool stg = ldsC && !c->S.laneW && c->S.sbRecN > 0u && (stgLds + 256) * 5 <= 163840;
     auto connectK = c->S.laneW ? (ldsC ? k_connect<true, true> : k_connect<false, true>)
                                : (ldsC ? (stg ? k_connect<true, false, true> : k_connect<true, false>) : k_connect<false, false>);
     /* staged: 16-bit stack entries (half the stack's LDS) leave room for the
      * copy beside 5 workgroups of 256 per CU, the residency k_connect runs at */
     const size_t connectLds = (!ldsC ? (size_t)sw * sizeof(uint32_t) : stg ? stgLds : traversalLds(c, kBlock)) + c->conLdsPad;
-    hipLaunchKernelGGL(connectK, dim3(c->gridConnect), dim3(kBlock), connectLds, s1, c->S, c->Q, c->rad, c->ctr, par, sw, qorder);
+    hipLaunchKernelGGL(connectK, dim3(c->gridConnect), dim3(kBlock), connectLds, s1, c->S, c->Q, c->rad, c->ctr, par, sw);
     if (ovl) (void)hipEventRecord(c->capEv[2 * ph + 1], s1);
     if (ev) (void)hipEventRecord(ev[5], s0);
     hipLaunchKernelGGL(k_regen, dim3(c->gridRegen), dim3(kBlock), 0, s0, c->cam, c->pool[par ^ 1], c->rad, c->ctr, par,
@@ -1253,19 +1254,20 @@ void setKeys(surf_ctx* c, DevScene& S, const InstanceTables& T) {
     S.keyMode = T.nHeavy ? c->keyMode : 0u;
     /* the emitters' BLAS, when every light instance uses one BLAS and its
      * node records fit kLdsLightBlas bytes: k_connect stages them */
-    S.sbNode0 = S.sbNodeN = 0u;
+    S.sbNode0 = S.sbRecN = S.sbTri0 = S.sbTriN = 0u;
+    S.sbRec = nullptr;
     if (c->ldsLightBlas && !T.lights.empty()) {
         bool one = true;
         const DevInstance* L0 = T.lights[0].x < T.inst.size() ? &T.inst[T.lights[0].x] : nullptr;
         for (const uint2& L : T.lights)
             one = one && L0 && L.x < T.inst.size() && T.inst[L.x].nodeOffset == L0->nodeOffset &&
                   T.inst[L.x].idxOffset == L0->idxOffset && T.inst[L.x].triOffset == L0->triOffset;
-        const auto nr = one ? c->blasNodeRange.find(L0->nodeOffset) : c->blasNodeRange.end();
+        const auto sb = one ? c->stagedBlas.find(L0->nodeOffset) : c->stagedBlas.end();
         /* 16-bit stack entries: every BLAS and TLAS node index below 65536 */
         const bool small = c->nBlasNodes < 65536u && T.tnodes.size() / 4 < 65536u;
-        if (small && nr != c->blasNodeRange.end() && nr->second[0] == L0->nodeOffset) {
-            const uint64_t nN = (uint64_t)nr->second[1] - nr->second[0] + 1;
-            if (nN * 64 <= kLdsLightBlas) { S.sbNode0 = nr->second[0]; S.sbNodeN = (uint32_t)nN; }
+        if (small && sb != c->stagedBlas.end() && sb->second.tri0 == L0->idxOffset) {
+            S.sbNode0 = sb->first; S.sbRec = sb->second.rec; S.sbRecN = sb->second.recN;
+            S.sbTri0 = sb->second.tri0; S.sbTriN = sb->second.triN;
         }
     }
 }
@@ -1439,12 +1441,44 @@ int surf_upload_scene(surf_ctx* c, const surf_scene_desc* d) {
         }
     }
     c->nBlasNodes = d->blas_node_count;
-    c->blasNodeRange.clear();
-    for (uint32_t k = 0; k < d->blas_node_count; ++k)
-        if (owner[k] != kUnset) {
-            auto it = c->blasNodeRange.emplace(owner[k], std::array<uint32_t, 2>{k, k}).first;
-            it->second[0] = std::min(it->second[0], k); it->second[1] = std::max(it->second[1], k);
+    /* the compact form of every small BLAS (k_connect stages the emitters' one,
+     * blasAnyStaged): its interior records in DFS order from the root (record 0),
+     * each child an interior record index or a leaf's kLeafTagC | count << 16 |
+     * leftFirst; and the span of its triangle slots */
+    std::map<uint32_t, std::vector<float4>> compact;
+    std::map<uint32_t, std::array<uint32_t, 2>> compactTris;   /* node offset -> (index offset, slots) */
+    for (uint32_t i = 0; i < d->instance_count; ++i) {
+        const uint32_t root = d->instances[i].bvh_node_offset;
+        if (compact.count(root) || d->blas_nodes[root].count != 0) continue;
+        std::vector<float4> recs;
+        std::vector<uint32_t> order{root};                     /* interior nodes by record index */
+        uint32_t slots = 0;
+        bool ok = true;
+        for (size_t k = 0; k < order.size() && ok; ++k) {
+            const uint32_t g = order[k];
+            const float4* r = &nodes[4 * (size_t)g];
+            uint32_t ref[2];
+            for (int ch = 0; ch < 2; ++ch) {
+                const uint32_t cg = root + f2u(r[0].w) + (uint32_t)ch;
+                const surf_bvh_node& q = d->blas_nodes[cg];
+                if (q.count != 0) {
+                    ok = ok && q.count < 32768u && q.left_first < 65536u;
+                    ref[ch] = kLeafTagC | (q.count << 16) | (q.left_first & 0xffffu);
+                    slots = std::max(slots, q.left_first + q.count);
+                } else {
+                    ok = ok && order.size() < 32768u;
+                    ref[ch] = (uint32_t)order.size();
+                    order.push_back(cg);
+                }
+            }
+            recs.push_back(make_float4(r[0].x, r[0].y, r[0].z, u2f(ref[0])));
+            recs.push_back(make_float4(r[1].x, r[1].y, r[1].z, u2f(ref[1])));
+            recs.push_back(make_float4(r[2].x, r[2].y, r[2].z, 0.0f));
+            recs.push_back(make_float4(r[3].x, r[3].y, r[3].z, 0.0f));
+            ok = ok && (recs.size() / 4) * 64 + (uint64_t)slots * 48 <= kLdsLightBlas;
         }
+        if (ok) { compact[root] = std::move(recs); compactTris[root] = {d->instances[i].bvh_idx_offset, slots}; }
+    }
     c->blasRoots.clear();
     for (uint32_t i = 0; i < d->instance_count; ++i) {
         const surf_gpu_instance& g = d->instances[i];
@@ -1582,6 +1616,13 @@ int surf_upload_scene(surf_ctx* c, const surf_scene_desc* d) {
     for (const float4& q : nodes)
         if (!(std::fabs(q.x) <= FLT_MAX && std::fabs(q.y) <= FLT_MAX && std::fabs(q.z) <= FLT_MAX)) { S.finiteBoxes = 0u; break; }
     S.tlasLeafCount = IT.tlasLeafCount;
+    c->stagedBlas.clear();
+    for (const auto& kv : compact) {
+        const float4* dR = nullptr;
+        if ((rc = upload(c, kv.second, &dR))) return rc;
+        c->stagedBlas[kv.first] = surf_ctx::StagedBlas{dR, (uint32_t)(kv.second.size() / 4), compactTris[kv.first][0],
+                                                        compactTris[kv.first][1]};
+    }
     setKeys(c, S, IT);
     const surf_background& bg = *d->background;
     S.bgType = bg.type;
