@@ -137,14 +137,40 @@ struct Sink { Pool q; uint32_t* n; uint32_t cap; };
  * for a bin that outgrows its region), so k_connect reads the rays in bin
  * order sequentially: no sort pass and no gather through an order array. */
 constexpr uint32_t kShBins = 16;     /* shadow-ray order bins: light slot (mod 2) x octant cell */
-struct ShadowQ { float4* od; float4* c; uint32_t region; uint32_t bins; };
+/* Each bin's cursor and region are split by XCD (SURF_SH_XCDS parts, the
+ * appending workgroup's HW_REG_XCC_ID) and the cursors lie SURF_SH_STRIDE words
+ * apart: every workgroup iteration of k_shade reserves once per non-empty bin,
+ * and same-address device atomics serialize. */
+#ifndef SURF_SH_XCDS
+#define SURF_SH_XCDS 1
+#endif
+#ifndef SURF_SH_STRIDE
+#define SURF_SH_STRIDE 32
+#endif
+constexpr uint32_t kShXcds = SURF_SH_XCDS, kShStride = SURF_SH_STRIDE;
+constexpr uint32_t kShSegs = kShBins * kShXcds + 1u;      /* queue segments: (bin, XCD) regions, then the overflow */
+struct ShadowQ {
+    float4* od; float4* c;
+    uint32_t* cur;        /* [2 parities][kShSegs] cursors, kShStride words apart (may count past a region's end) */
+    uint32_t region;      /* slots per (bin, XCD) region */
+    uint32_t bins;        /* kShBins, or 1: no shadow order (SURF_SORT=0/2) */
+};
+__device__ __forceinline__ uint32_t* shCursor(const ShadowQ& Q, int par, uint32_t seg) {
+    return Q.cur + ((size_t)par * kShSegs + seg) * kShStride;
+}
+__device__ __forceinline__ uint32_t xccId() {
+    if constexpr (kShXcds == 1u) return 0u;
+    uint32_t x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
+    return x % kShXcds;
+}
 
 /* Device counters of the sample stream.  Double-buffered by phase parity so no
  * kernel writes a word another block of the same launch still reads. */
 struct Counters {
     uint32_t nIn[2];                 /* paths in pool[p] when a phase reads it */
-    unsigned long long app[2];       /* phase parity p: low 32 = paths appended to pool[p^1],
-                                        high 32 = shadow rays queued (one packed atomic per block) */
+    uint32_t app[2];                 /* phase parity p: paths appended to pool[p^1] (the shadow
+                                        queue's cursors are ShadowQ::cur) */
     uint32_t maxSeg;                 /* 0 = unbounded */
     uint32_t zeroCutoff;             /* end paths whose throughput is exactly 0 (radiance-neutral) */
     uint32_t segMax;                 /* longest finished path (extension rays), diagnostics */
@@ -170,10 +196,6 @@ struct Counters {
      * atomics (~12 ns each, measured); totals = ev + sum over stripes */
     unsigned long long evS[32][16];
     unsigned long long dbg[8];       /* SURF_SEG_TIMING builds: k_tail_coop cycles (extend, shade, connect, segments) */
-    /* shadow-queue cursors by phase parity: bins 0..kShBins-1 (may count past
-     * their region: the excess went to the overflow region), then the overflow
-     * region's; one 128-B line each (same-line atomics serialize) */
-    uint32_t shCur[2][kShBins + 1][32];
 };
 constexpr uint32_t kStripes = 32;    /* frameDone and event-count stripes */
 constexpr int kEvents = 9;           /* event kinds counted (ev / evS index) */
@@ -1836,7 +1858,7 @@ __device__ __forceinline__ uint8_t shadowKey(const DevScene& S, uint32_t light, 
 
 /* Rays to order: which = 0 the pool read by phase par, 1 its shadow queue. */
 __device__ __forceinline__ uint32_t sortCount(const Counters* C, int par, int which) {
-    return which ? (uint32_t)(C->app[par] >> 32) : C->nIn[par];
+    return which ? 0u : C->nIn[par];   /* (the shadow queue needs no sort: k_shade appends it in bin order) */
 }
 __device__ __forceinline__ void sortChunk(uint32_t n, uint32_t& a, uint32_t& b) {
     const uint32_t c = (n + gridDim.x - 1u) / gridDim.x;
@@ -2326,8 +2348,8 @@ __global__ __launch_bounds__(kBlock, SURF_SHADE_WAVES) void k_shade(DevScene S, 
     }
     /* block-level compaction: per iteration one packed 64-bit atomic reserves the
      * block's continuation and shadow slots (LDS double-buffered by iteration) */
-    __shared__ uint32_t sWave[2][kBlock / 64][2];
-    __shared__ uint32_t sBase[2][2];
+    __shared__ uint32_t sWave[2][kBlock / 64];
+    __shared__ uint32_t sBase[2];
     /* shadow rays per bin of the iteration (a lane's LDS atomic returns its rank
      * in its bin) and each bin's reservation: region base, the part that fits
      * the region, the overflow base of the rest */
@@ -2362,36 +2384,43 @@ __global__ __launch_bounds__(kBlock, SURF_SHADE_WAVES) void k_shade(DevScene S, 
                 rad[sid + npx] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             }
         }
-        const unsigned long long mCont = __ballot(r.cont || r.next), mSh = __ballot(r.shadow);
-        if (laneId() == 0) { sWave[it][wv][0] = (uint32_t)__popcll(mCont); sWave[it][wv][1] = (uint32_t)__popcll(mSh); }
+        const unsigned long long mCont = __ballot(r.cont || r.next);
+        if (laneId() == 0) sWave[it][wv] = (uint32_t)__popcll(mCont);
         /* the shadow ray's bin -- toward the same light from the same octant of
          * the scene -- and its rank among the iteration's rays of that bin */
         const uint32_t kb = r.shadow ? (Q.bins > 1u ? shadowKey(S, r.light, r.so) : 0u) : kShBins;
         uint32_t rk = 0;
         if (r.shadow) rk = atomicAdd(&sShCnt[it][kb], 1u);
         __syncthreads();
-        if (threadIdx.x == 0) {
-            unsigned long long tc = 0, ts = 0;
-            for (uint32_t k = 0; k < nw; ++k) { tc += sWave[it][k][0]; ts += sWave[it][k][1]; }
-            const unsigned long long old = (tc | ts) ? atomicAdd(&C->app[par], (ts << 32) | tc) : 0ull;
-            sBase[it][0] = (uint32_t)old; sBase[it][1] = (uint32_t)(old >> 32);
-        }
-        if (threadIdx.x < kShBins) {
-            /* one reservation per (iteration, non-empty bin); what does not fit
-             * the bin's region goes to the overflow region */
-            const uint32_t tot = sShCnt[it][threadIdx.x];
-            sShCnt[it ^ 1u][threadIdx.x] = 0u;     /* the next iteration's counts (last read an iteration ago) */
-            uint32_t b0 = 0, ok = 0, ov = 0;
-            if (tot) {
-                b0 = atomicAdd(&C->shCur[par][threadIdx.x][0], tot);
-                ok = b0 >= Q.region ? 0u : min(tot, Q.region - b0);
-                if (ok < tot) ov = atomicAdd(&C->shCur[par][kShBins][0], tot - ok);
+        if (threadIdx.x <= kShBins) {
+            /* the iteration's reservations in ONE atomic instruction of wave 0
+             * (a round trip each would serialize): lanes 0..kShBins-1 the
+             * non-empty shadow bins (this XCD's part of each), lane kShBins the
+             * continuations; shadow rays that do not fit their bin's region go
+             * to the overflow region */
+            const uint32_t t = threadIdx.x;
+            const uint32_t seg = t * kShXcds + xccId();
+            uint32_t tot = 0;
+            uint32_t* cur = reinterpret_cast<uint32_t*>(&C->app[par]);
+            if (t < kShBins) {
+                tot = sShCnt[it][t];
+                sShCnt[it ^ 1u][t] = 0u;           /* the next iteration's counts (last read an iteration ago) */
+                cur = shCursor(Q, par, seg);
+            } else {
+                for (uint32_t k = 0; k < nw; ++k) tot += sWave[it][k];
             }
-            sShBase[it][threadIdx.x] = b0; sShOk[it][threadIdx.x] = ok; sShOv[it][threadIdx.x] = ov;
+            const uint32_t b0 = tot ? atomicAdd(cur, tot) : 0u;
+            if (t == kShBins) {
+                sBase[it] = b0;
+            } else {
+                const uint32_t ok = b0 >= Q.region ? 0u : min(tot, Q.region - b0);
+                const uint32_t ov = ok < tot ? atomicAdd(shCursor(Q, par, kShSegs - 1u), tot - ok) : 0u;
+                sShBase[it][t] = seg * Q.region + b0; sShOk[it][t] = ok; sShOv[it][t] = ov;
+            }
         }
         __syncthreads();
-        uint32_t jc = sBase[it][0];
-        for (uint32_t k = 0; k < wv; ++k) jc += sWave[it][k][0];
+        uint32_t jc = sBase[it];
+        for (uint32_t k = 0; k < wv; ++k) jc += sWave[it][k];
         jc += rankBelow(mCont);
         if (r.cont || r.next) {
             stS(&nxt.od[2u * (jc)], r.o); stS(&nxt.od[2u * (jc) + 1u], r.d); stS(&nxt.T[jc], r.T);
@@ -2400,7 +2429,7 @@ __global__ __launch_bounds__(kBlock, SURF_SHADE_WAVES) void k_shade(DevScene S, 
         }
         if (r.shadow) {
             const uint32_t ok = sShOk[it][kb];
-            const uint32_t js = rk < ok ? kb * Q.region + sShBase[it][kb] + rk : kShBins * Q.region + sShOv[it][kb] + (rk - ok);
+            const uint32_t js = rk < ok ? sShBase[it][kb] + rk : (kShSegs - 1u) * Q.region + sShOv[it][kb] + (rk - ok);
             stS(&Q.od[2u * js], r.so); stS(&Q.od[2u * js + 1u], r.sd); stS(&Q.c[js], r.sc);
         }
         /* a path that ends here may still have this phase's shadow ray pending:
@@ -2417,31 +2446,42 @@ __global__ __launch_bounds__(kBlock, SURF_SHADE_WAVES) void k_shade(DevScene S, 
     blockCount<5>(C, {1, 2, 3, 4, 7}, {cHit, cCont, cSh, cAcc, cCap});
 }
 
-/* Where shadow ray i of the bin order lives: the bins' regions in bin order,
- * then the overflow region (pre: the first ray index of each, kShBins + 2
- * entries, the last = the count). */
+/* Where shadow ray i of the bin order lives: the (bin, XCD) regions in bin
+ * order, then the overflow region (pre: the first ray index of each segment,
+ * kShSegs + 1 entries, the last = the count). */
 __device__ __forceinline__ uint32_t shadowSlot(const ShadowQ& Q, const uint32_t* pre, uint32_t i) {
-    uint32_t b = 0;
-    while (b < kShBins && i >= pre[b + 1]) ++b;
-    return b * Q.region + (i - pre[b]);
+    uint32_t lo = 0, hi = kShSegs;            /* pre[lo] <= i < pre[hi] */
+    while (hi - lo > 1u) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (i >= pre[mid]) lo = mid; else hi = mid;
+    }
+    return lo * Q.region + (i - pre[lo]);
 }
 
 template <bool LDS, bool LW = false, bool STG = false>
 __global__ __launch_bounds__(kBlock, STG ? 5 : SURF_TRACE_WAVES) void k_connect(DevScene S, ShadowQ Q, float4* __restrict__ rad, Counters* C, int par,
                                                     uint32_t stackWords) {
     extern __shared__ uint32_t lds[];
-    const uint32_t n = (uint32_t)(C->app[par] >> 32);
-    if (blockIdx.x * blockDim.x >= n) return;               /* no shadow rays for this block */
-    __shared__ uint32_t sPre[kShBins + 2];
-    if (threadIdx.x == 0) {
-        uint32_t run = 0;
-        for (uint32_t b = 0; b <= kShBins; ++b) {
-            sPre[b] = run;
-            run += min(C->shCur[par][b][0], b < kShBins ? Q.region : 0xffffffffu);
+    __shared__ uint32_t sPre[kShSegs + 1];
+    if (threadIdx.x < 64u) {
+        /* first ray index of every queue segment: a wave scan of the cursors */
+        uint32_t carry = 0;
+        if (threadIdx.x == 0) sPre[0] = 0u;
+        for (uint32_t b0 = 0; b0 < kShSegs; b0 += 64u) {
+            const uint32_t b = b0 + threadIdx.x;
+            uint32_t v = b < kShSegs ? min(*shCursor(Q, par, b), b + 1u < kShSegs ? Q.region : 0xffffffffu) : 0u;
+#pragma unroll
+            for (uint32_t off = 1; off < 64u; off <<= 1) {
+                const uint32_t t = __shfl_up(v, off);
+                if (threadIdx.x >= off) v += t;
+            }
+            if (b < kShSegs) sPre[b + 1] = carry + v;
+            carry += (uint32_t)__shfl((int)v, 63);
         }
-        sPre[kShBins + 1] = run;     /* == n */
     }
     __syncthreads();
+    const uint32_t n = sPre[kShSegs];
+    if (blockIdx.x * blockDim.x >= n) return;               /* no shadow rays for this block */
     /* STG: the emitters' BLAS node records (every unoccluded shadow ray walks
      * that BLAS down to its sampled triangle) staged after a stack of 16-bit
      * entries (every node index < 65536) and the trace tables; stageTrace's
@@ -2485,9 +2525,9 @@ __global__ __launch_bounds__(kBlock, STG ? 5 : SURF_TRACE_WAVES) void k_connect(
  * initSeed(p + 1799 * (baseFrame + f * spp)) (renderer.cpp:169; baseFrame =
  * the sample count before the stream). */
 __global__ __launch_bounds__(kBlock) void k_regen(DevCamera cam, Pool nxt, float4* __restrict__ rad, Counters* C, int par,
-                                                  uint32_t capacity, StreamGeom G) {
+                                                  uint32_t capacity, StreamGeom G, ShadowQ Q) {
     const int nx = par ^ 1;
-    const uint32_t cont = (uint32_t)C->app[par];
+    const uint32_t cont = C->app[par];
     const unsigned long long iss = C->issued[par];
     const unsigned long long lim = C->limit;
     const unsigned long long base = C->baseFrame;
@@ -2496,6 +2536,7 @@ __global__ __launch_bounds__(kBlock) void k_regen(DevCamera cam, Pool nxt, float
     const unsigned long long left = lim > iss ? lim - iss : 0ull;
     const uint32_t nnew = (unsigned long long)room < left ? room : (uint32_t)left;
     const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid < kShSegs) *shCursor(Q, nx, gid) = 0u;      /* the next phase's shadow-queue cursors */
     /* frame / pixel of the first new chain, then step without 64-bit divisions */
     const unsigned long long f0 = iss / G.npx;
     const uint32_t lp0 = (uint32_t)(iss - f0 * G.npx);
@@ -2532,8 +2573,7 @@ __global__ __launch_bounds__(kBlock) void k_regen(DevCamera cam, Pool nxt, float
     if (gid == 0) {
         C->nIn[nx] = cont + nnew;
         C->issued[nx] = iss + nnew;
-        C->app[nx] = 0ull;             /* next phase's append cursors */
-        for (uint32_t b = 0; b <= kShBins; ++b) C->shCur[nx][b][0] = 0u;
+        C->app[nx] = 0u;               /* next phase's append cursor */
         C->ev[0] += cont + nnew;     /* extension rays of the next phase */
         C->ev[8] += cont + nnew;     /* ... traced by k_extend unless the drain takes the pool */
     }
@@ -2795,6 +2835,10 @@ __device__ __forceinline__ void pairPath(const DevScene& S, const TraceTables& T
     uint32_t slot = f2u(o4.w) / npx;
     bool pend = false;                     /* a posted shadow ray awaits its answer */
     V3 E = loadRadiance(rad, __builtin_amdgcn_readfirstlane(f2u(o4.w)));   /* the running sample's radiance */
+#if SURF_DRAIN_TRACE
+    const unsigned long long tStart = wall_clock64();
+    const uint32_t state0 = drainState(d4, T4), ext0 = pc.ext;
+#endif
     for (;;) {
         float depth = kFarAway, u = 0.0f, v = 0.0f;
         uint32_t inst = kUnset, prim = kUnset;
@@ -2854,6 +2898,9 @@ __device__ __forceinline__ void pairPath(const DevScene& S, const TraceTables& T
         ++pc.cont;
         o4 = r.o; d4 = r.d; T4 = r.T;
     }
+#if SURF_DRAIN_TRACE
+    if (lead) drainTraceEnd(tStart, pc.ext - ext0, state0);
+#endif
     ++pc.paths;
 }
 

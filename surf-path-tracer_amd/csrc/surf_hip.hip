@@ -361,11 +361,12 @@ int allocWavefront(surf_ctx* c) {
     /* shadow queue: kShBins bin regions of a quarter pool each (a phase queues
      * at most one shadow ray per path; C3 puts <= 30 % of them in one bin), then
      * an overflow region of a whole pool */
-    c->Q.region = (uint32_t)((cap / 4 + 255) / 256 * 256);
+    c->Q.region = (uint32_t)((cap / (4 * kShXcds) + 255) / 256 * 256);
     c->Q.bins = (c->sortRays && c->sortShadow) ? kShBins : 1u;
-    const size_t qslots = (size_t)kShBins * c->Q.region + cap;
+    const size_t qslots = (size_t)(kShSegs - 1) * c->Q.region + cap;
     if ((rc = devAlloc(c, c->wfAllocs, &c->Q.od, 2 * qslots))) return rc;
     if ((rc = devAlloc(c, c->wfAllocs, &c->Q.c, qslots))) return rc;
+    if ((rc = devAlloc(c, c->wfAllocs, &c->Q.cur, (size_t)2 * kShSegs * kShStride))) return rc;
     if ((rc = devAlloc(c, c->wfAllocs, &c->ctr, 1))) return rc;
     if ((rc = devAlloc(c, c->wfAllocs, &c->dOutRGBA, c->npx))) return rc;
     if (hipHostMalloc((void**)&c->hctr, sizeof(Counters), hipHostMallocDefault) != hipSuccess)
@@ -527,7 +528,7 @@ void launchPhase(surf_ctx* c, int ph, hipEvent_t* ev) {
     if (ovl) (void)hipEventRecord(c->capEv[2 * ph + 1], s1);
     if (ev) (void)hipEventRecord(ev[5], s0);
     hipLaunchKernelGGL(k_regen, dim3(c->gridRegen), dim3(kBlock), 0, s0, c->cam, c->pool[par ^ 1], c->rad, c->ctr, par,
-                       c->capacity, geom(c));
+                       c->capacity, geom(c), c->Q);
 }
 
 int buildGraph(surf_ctx* c) {
@@ -624,6 +625,7 @@ int startStream(surf_ctx* c, uint64_t baseFrame, uint32_t maxSeg, uint32_t frame
     *c->hctr = h;
     SURF_CHECK(c, hipMemcpyAsync(c->ctr, c->hctr, sizeof(Counters), hipMemcpyHostToDevice, c->stream));
     SURF_CHECK(c, hipMemsetAsync(c->frameDone, 0, (size_t)kStripes * c->window * sizeof(uint32_t), c->stream));
+    SURF_CHECK(c, hipMemsetAsync(c->Q.cur, 0, (size_t)2 * kShSegs * kShStride * sizeof(uint32_t), c->stream));
     c->streamActive = true;
     c->baseFrame = baseFrame;
     c->targetFrames = 0;
