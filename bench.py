@@ -60,7 +60,8 @@ B_EVENT = {"n_ext": 52, "n_hit": 68, "n_cont": 48, "n_shadow": 88, "n_acc": 24}
 # rocprofv3 summary of this bench command per workload (tools/profile_round.sh + tools/summarize_profile.py):
 # k_extend's average duration (--kernel-trace --stats) and HBM bytes per launch (FETCH_SIZE x2 +
 # WRITE_SIZE, separate PMC passes, MI355X_MICROARCH.md HBM/rocprofv3 section).
-PMC_SUMMARY = os.path.join(REPO, "profiles", "r4_{}", "summary.json")
+PMC_SUMMARY = os.path.join(REPO, "profiles", "r{}_{}", "summary.json")
+PMC_ROUNDS = (5, 4)   # the newest committed rocprof summary of the workload (tools/round.sh profiles)
 
 WORKLOADS = {
     "C3": dict(scene="indoor", width=1280, height=720, spp=256, max_segments=0, cpu_row_step=5),
@@ -221,8 +222,8 @@ def cpu_baseline(args, wl, first_frame, gpu_acc):
 
 def rocprof_summary(workload):
     """k_extend's rocprofv3 average and PMC traffic from the committed summary of this command."""
-    path = PMC_SUMMARY.format(workload.lower())
-    if not os.path.exists(path):
+    path = next((p for p in (PMC_SUMMARY.format(r, workload.lower()) for r in PMC_ROUNDS) if os.path.exists(p)), None)
+    if path is None:
         return None
     s = json.load(open(path))
     if s.get("workload", "C3") != workload:
