@@ -153,6 +153,8 @@ struct surf_ctx {
     uint32_t coopMax = 0;          /* survivors handled by the cooperative tail (one path per wave) */
     uint32_t coopAll = 150000;     /* drain paths left to the cooperative tail (surf_set_tail_coop); C3 drain 176-184 ms at 60000, 172-178 at 150000 */
     int drainReplays = 1;          /* graph replays per host poll while draining (SURF_DRAIN_REPLAYS) */
+    bool drainShort = false;       /* 2-phase replays once nothing is left to issue (SURF_DRAIN_SHORT=1; measured slower, MEASUREMENTS round 5) */
+    bool regenFirst = false;       /* k_regen before the connect fork (SURF_REGEN_FIRST=1; measured equal, MEASUREMENTS round 5) */
     bool coopEligible = false;     /* single-leaf TLAS of <= 64 instances, LDS tables (the four-rows engine) */
     int traceMode = 0;             /* surf_trace_closest/_any: 0 one ray per lane, 1 one ray per wave, 2 one ray per 16-lane row */
     bool tailRows = false;         /* drain on k_tail_rows (four paths per wave; SURF_TAIL_ROWS=1) instead of k_tail_coop */
@@ -505,6 +507,11 @@ void launchPhase(surf_ctx* c, int ph, hipEvent_t* ev) {
                            c->hitTUV, (const uint32_t*)c->hitInst, c->Q, c->rad, c->frameDone, c->npx, c->window, c->ctr, par, order,
                            c->cam, geom(c));
     if (ev) (void)hipEventRecord(ev[3], s0);
+    /* k_regen before the fork (SURF_REGEN_FIRST): alone it takes ~17 us, beside
+     * k_connect it waits for CU slots on the next phase's critical path */
+    if (c->regenFirst)
+        hipLaunchKernelGGL(k_regen, dim3(c->gridRegen), dim3(kBlock), 0, s0, c->cam, c->pool[par ^ 1], c->rad, c->ctr, par,
+                           c->capacity, geom(c), c->Q);
     if (ovl) {
         (void)hipEventRecord(c->capEv[2 * ph], s0);
         (void)hipStreamWaitEvent(s1, c->capEv[2 * ph], 0);
@@ -527,8 +534,9 @@ void launchPhase(surf_ctx* c, int ph, hipEvent_t* ev) {
     hipLaunchKernelGGL(connectK, dim3(c->gridConnect), dim3(kBlock), connectLds, s1, c->S, c->Q, c->rad, c->ctr, par, sw);
     if (ovl) (void)hipEventRecord(c->capEv[2 * ph + 1], s1);
     if (ev) (void)hipEventRecord(ev[5], s0);
-    hipLaunchKernelGGL(k_regen, dim3(c->gridRegen), dim3(kBlock), 0, s0, c->cam, c->pool[par ^ 1], c->rad, c->ctr, par,
-                       c->capacity, geom(c), c->Q);
+    if (!c->regenFirst)
+        hipLaunchKernelGGL(k_regen, dim3(c->gridRegen), dim3(kBlock), 0, s0, c->cam, c->pool[par ^ 1], c->rad, c->ctr, par,
+                           c->capacity, geom(c), c->Q);
 }
 
 int buildGraph(surf_ctx* c) {
@@ -724,8 +732,9 @@ int advance(surf_ctx* c, bool shortRun = false) {
             float t[kPhaseEvents];
             for (int k = 0; k < kPhaseEvents; ++k)
                 (void)hipEventElapsedTime(&t[k], c->pev[kPhaseEvents * ph + k], c->pev[kPhaseEvents * ph + k + 1]);
-            c->stats.ms_sort += t[0] + t[3];
-            c->stats.ms_extend += t[1]; c->stats.ms_shade += t[2]; c->stats.ms_connect += t[4]; c->stats.ms_regen += t[5];
+            /* (t[3]: k_regen when it runs before the fork, else nothing) */
+            c->stats.ms_sort += t[0];
+            c->stats.ms_extend += t[1]; c->stats.ms_shade += t[2]; c->stats.ms_connect += t[4]; c->stats.ms_regen += t[3] + t[5];
             c->stats.launches_extend++;
         }
     } else {
@@ -938,8 +947,10 @@ int pump(surf_ctx* c, bool drain, uint64_t lag) {
              * the per-replay poll, not the kernels, is what a small pool pays */
             const int reps = starved ? c->drainReplays : 1;
             /* a per-frame render call (lagged, or at most one frame left to
-             * issue): short replays */
-            const bool shortRun = !drain && (lag > 0 || target - issued <= c->npx);
+             * issue): short replays (SURF_DRAIN_SHORT=1: also once nothing is
+             * left to issue, so the drain takes over within 2 phases instead
+             * of up to 8 -- measured slower) */
+            const bool shortRun = (!drain && (lag > 0 || target - issued <= c->npx)) || (starved && c->drainShort);
             for (int k = 0; k < reps; ++k)
                 if ((rc = advance(c, shortRun))) return rc;
         }
@@ -1030,6 +1041,8 @@ int createCtx(int dev, uint32_t w, uint32_t h, std::vector<uint32_t> rows, surf_
     if (const char* e = std::getenv("SURF_REORDER")) c->reorder = e[0] != '0';
     if (const char* e = std::getenv("SURF_TAIL_ROWS")) c->tailRows = e[0] == '1';
     if (const char* e = std::getenv("SURF_TAIL_PAIR")) c->tailPair = e[0] != '0';
+    if (const char* e = std::getenv("SURF_DRAIN_SHORT")) c->drainShort = e[0] == '1';
+    if (const char* e = std::getenv("SURF_REGEN_FIRST")) c->regenFirst = e[0] == '1';
     c->width = w;
     c->height = h;
     c->rows = std::move(rows);
