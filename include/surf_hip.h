@@ -172,11 +172,12 @@ int surf_set_pool_capacity(surf_ctx* ctx, uint32_t paths);
  * consecutive passes) whose samples may be in flight at once -- a multiple of
  * the stream's samples_per_frame.  Default: the passes the stream being
  * started requests (one render call's frames x spp, rounded to a multiple of spp),
- * at least 256 -- 1024 for a stream opened by a one-frame request (a drop-in
+ * at least 256 -- 4096 for a stream opened by a one-frame request (a drop-in
  * loop extends its stream one frame per call) -- at most
- * 4096 and at most what min(32 GiB, a quarter of the free HBM) holds; a later
+ * 4096 and at most what min(64 GiB, a quarter of the free HBM) holds; a later
  * stream that requests more frames grows the ring (C3 at 1280x720: 256 frames
- * = 3.8 GB; C4 at 1920x1080: 1024 frames = 34 GB, within the 1035 that 32 GiB hold).
+ * = 3.8 GB, a one-frame stream 4096 = 60 GB; C4 at 1920x1080: 1024 frames = 34 GB;
+ * 64 GiB hold 2070 slots at 1080p).
  * Sample radiance is held per (frame slot, pixel) until a frame completes and
  * is accumulated in frame order; long Russian-roulette paths of old frames
  * overlap the bulk of newer ones.  A stream longer than the window issues

@@ -411,11 +411,12 @@ int allocWavefront(surf_ctx* c) {
  * and at least kLoopFloor for a stream opened by a one-frame request (a
  * drop-in loop extends its stream one frame per call, so its first request
  * says nothing about its length; 4096 one-frame calls at 1280x720 run at
- * 365 / 443 / 472 Mrays/s with 256 / 1024 / 4096 slots), at most
- * 4096 and at most what min(32 GiB, a quarter of the free HBM) holds.  A
+ * 552 / 593 / 614 Mrays/s with 1024 / 2048 / 4096 slots, MEASUREMENTS round 5), at most
+ * 4096 and at most what min(64 GiB, a quarter of the free HBM) holds (HBM3E:
+ * 288 GB per GPU; 4096 slots at 1280x720 take 60 GB).  A
  * later, longer stream grows the ring; a window set by surf_set_frame_batch
  * is kept as given. */
-constexpr uint64_t kWindowFloor = 256, kLoopFloor = 1024;
+constexpr uint64_t kWindowFloor = 256, kLoopFloor = 4096;
 constexpr uint64_t kLdsLightBlas = 20480;     /* k_connect's staged emitter BLAS (compact records + triangles), bytes at most */
 int ensureWindow(surf_ctx* c, uint64_t frames, uint32_t spp) {
     const uint64_t passes = frames * spp;
@@ -425,7 +426,7 @@ int ensureWindow(surf_ctx* c, uint64_t frames, uint32_t spp) {
         return fail(c, SURF_ERR_INVALID, "frame window " + std::to_string(c->window) + " is not a multiple of samples_per_frame " +
                                              std::to_string(spp));
     if (!c->windowFixed) {
-        uint64_t budget = 32ull << 30;
+        uint64_t budget = 64ull << 30;
         size_t freeB = 0, totalB = 0;
         if (hipMemGetInfo(&freeB, &totalB) == hipSuccess && freeB > 0)
             budget = std::min<uint64_t>(budget, (freeB + (c->rad ? (size_t)c->npx * c->window * sizeof(float4) : 0)) / 4);
