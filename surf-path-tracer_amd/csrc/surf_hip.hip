@@ -183,6 +183,8 @@ struct surf_ctx {
 
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipEvent_t pev[kPhasesPerGraph * kPhaseEvents + 1] = {};   /* profiling: kPhaseEvents per phase + the end */
+    uint32_t* hPhaseN = nullptr;   /* profiling + SURF_PHASE_LOG: paths each phase extends (pinned) */
+    FILE* phaseLog = nullptr;      /* SURF_PHASE_LOG=<file>: one line per profiled phase (size, kernel ms) */
     surf_stats stats{};
     unsigned long long evBase[kEvents] = {};   /* event counts of finished streams since the last clear */
 };
@@ -374,6 +376,11 @@ int allocWavefront(surf_ctx* c) {
     if (hipHostMalloc((void**)&c->hctr, sizeof(Counters), hipHostMallocDefault) != hipSuccess)
         return fail(c, SURF_ERR_OOM, "hipHostMalloc of the counter block failed");
     for (auto& e : c->pev) SURF_CHECK(c, hipEventCreate(&e));
+    if (const char* e = std::getenv("SURF_PHASE_LOG")) {         /* diagnostics: per-phase cost vs size */
+        if (hipHostMalloc((void**)&c->hPhaseN, kPhasesPerGraph * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess)
+            return fail(c, SURF_ERR_OOM, "hipHostMalloc of the phase log failed");
+        c->phaseLog = std::fopen(e, "a");
+    }
     const uint64_t maxBlocks = (cap + kBlock - 1) / kBlock;
     uint64_t perCu = 8;                                   /* workgroups per CU of the wavefront kernels (SURF_GRID_PER_CU) */
     if (const char* e = std::getenv("SURF_GRID_PER_CU")) perCu = (uint64_t)std::max(1, std::atoi(e));
@@ -484,6 +491,8 @@ void launchPhase(surf_ctx* c, int ph, hipEvent_t* ev) {
     const uint32_t sw = stackWords(c, kBlock);
     const bool ovl = !ev && c->overlap;
     hipStream_t s0 = c->stream, s1 = ovl ? c->side : c->stream;
+    if (ev && c->phaseLog)
+        (void)hipMemcpyAsync(&c->hPhaseN[ph], &c->ctr->nIn[par], sizeof(uint32_t), hipMemcpyDeviceToHost, s0);
     if (ev) (void)hipEventRecord(ev[0], s0);
     const uint32_t* order = nullptr;
     if (c->sortRays && c->sortPool) {
@@ -737,7 +746,11 @@ int advance(surf_ctx* c, bool shortRun = false) {
             c->stats.ms_sort += t[0];
             c->stats.ms_extend += t[1]; c->stats.ms_shade += t[2]; c->stats.ms_connect += t[4]; c->stats.ms_regen += t[3] + t[5];
             c->stats.launches_extend++;
+            if (c->phaseLog)
+                std::fprintf(c->phaseLog, "phase %u sort %.4f extend %.4f shade %.4f regen %.4f connect %.4f\n", c->hPhaseN[ph], t[0], t[1],
+                             t[2], t[3] + t[5], t[4]);
         }
+        if (c->phaseLog) std::fflush(c->phaseLog);
     } else {
         SURF_CHECK(c, hipGraphLaunch(shortRun ? c->graphExecShort : c->graphExec, c->stream));
     }
@@ -1109,6 +1122,8 @@ void surf_destroy(surf_ctx* c) {
     if (c->rad) (void)hipFree(c->rad);
     if (c->frameDone) (void)hipFree(c->frameDone);
     for (auto& e : c->pev) if (e) (void)hipEventDestroy(e);
+    if (c->hPhaseN) (void)hipHostFree(c->hPhaseN);
+    if (c->phaseLog) std::fclose(c->phaseLog);
     if (c->acc) (void)hipFree(c->acc);
     if (c->dRows) (void)hipFree(c->dRows);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
