@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define SURF_ABI_VERSION 2
+#define SURF_ABI_VERSION 3
 
 typedef enum {
     SURF_OK = 0,
@@ -122,7 +122,7 @@ typedef struct {
     uint64_t tail_paths;       /* paths finished by the tail kernel */
     double   ms_total;         /* device time of render + drain calls since the last clear */
     double   ms_extend, ms_shade, ms_connect, ms_regen, ms_tail, ms_accum;  /* per-kernel (surf_set_profiling) */
-    double   ms_sort;          /* ray-order sorts (pool + shadow queue), profiling mode */
+    double   ms_sort;          /* the pool's ray-order sort (the shadow queue needs none), profiling mode */
     uint64_t launches_extend;  /* k_extend launches timed (profiling mode) */
     uint64_t n_ext_wavefront;  /* extension rays traced by k_extend (n_ext minus the drain's) */
     uint32_t stack_depth;      /* traversal stack entries reserved per ray */
@@ -130,6 +130,7 @@ typedef struct {
     float    energy;           /* sum of acc.rgb / samples over the shard ("Lumen", renderer.cpp:191-201) */
     uint32_t max_segments;     /* longest path seen (extension rays), diagnostics */
     uint64_t tail_survivors;   /* drain paths handed to the cooperative tail */
+    uint32_t frame_window;     /* radiance ring slots (passes) of the current stream (surf_set_frame_batch), 0 before the first render */
 } surf_stats;
 
 typedef struct surf_ctx surf_ctx;       /* one per HIP device */

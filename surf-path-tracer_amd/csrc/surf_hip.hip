@@ -1864,6 +1864,7 @@ int surf_get_stats(surf_ctx* c, surf_stats* out) {
     s.max_segments = std::max(c->segMaxBase, (c->streamActive && c->hctr) ? c->hctr->segMax : 0u);
     s.stack_depth = c->stackDepth;
     s.pool_capacity = c->capacity;
+    s.frame_window = c->window;
     if (c->totalSamples) {
         /* Lumen energy, renderer.cpp:191-201: per-pixel terms on the GPU
          * (k_energy_terms), then the reference's serial sum in pixel order */

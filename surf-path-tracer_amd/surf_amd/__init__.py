@@ -65,6 +65,7 @@ class Stats(C.Structure):
         ("launches_extend", C.c_uint64), ("n_ext_wavefront", C.c_uint64),
         ("stack_depth", C.c_uint32), ("pool_capacity", C.c_uint32),
         ("energy", C.c_float), ("max_segments", C.c_uint32), ("tail_survivors", C.c_uint64),
+        ("frame_window", C.c_uint32),
     ]
 
     def as_dict(self) -> dict:

@@ -423,25 +423,37 @@ def test_c2_1280x720_cap8_rows(oracle_scene, product_scene):
 
 
 def test_window_grows_with_stream_bitexact(oracle_scene, product_scene):
-    """The radiance ring follows the requested stream: a first 1-frame stream
-    sizes it at the floor (256 frames), a later 300-frame stream grows it (the
-    graph is re-captured on the new ring); both renders equal the oracle's."""
+    """The radiance ring follows the requested stream: a first 2-frame stream
+    sizes it at the floor (256 passes), a later 300-frame stream grows it (the
+    graph is re-captured on the new ring), and a stream opened by a one-frame
+    call (the drop-in loop) gets the loop floor, 4096; every render equals the
+    oracle's."""
     W, H = 16, 12
     r = surf_amd.Renderer(product_scene, W, H)
-    r.render(1, 0, 0)
+    assert r.stats()["frame_window"] == 0
+    r.render(2, 0, 0)
     g1 = r.accumulator()
+    assert r.stats()["frame_window"] == 256
     r.clear_accumulator()
     r.render(300, 0, 0)
     g2 = r.accumulator()
+    assert r.stats()["frame_window"] == 300
+    r.close()
+    r = surf_amd.Renderer(product_scene, W, H)
+    r.render(1, 0, 0)
+    assert r.stats()["frame_window"] == 4096
+    g3 = r.accumulator()
     r.close()
     oracle.set_zero_cutoff(True)
     try:
-        c1, _, _ = oracle_scene.render(W, H, 1)
+        c1, _, _ = oracle_scene.render(W, H, 2)
         c2, _, _ = oracle_scene.render(W, H, 300)
+        c3, _, _ = oracle_scene.render(W, H, 1)
     finally:
         oracle.set_zero_cutoff(False)
-    _assert_bitexact(g1, c1, "1-frame stream")
+    _assert_bitexact(g1, c1, "2-frame stream")
     _assert_bitexact(g2, c2, "300-frame stream after the ring grew")
+    _assert_bitexact(g3, c3, "one-frame stream on the 4096-slot ring")
 
 
 def test_full_resolution_rows(oracle_scene, product_scene):
