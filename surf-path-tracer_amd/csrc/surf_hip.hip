@@ -39,10 +39,16 @@ namespace {
 
 constexpr int kPhasesPerGraph = 8;          /* even: parity returns to 0 after a replay */
 /* The short graph: a render call with at most one frame left to issue (the
- * drop-in loop's 1-spp render(), main.cpp:381-446) replays 2 phases per host
+ * drop-in loop's 1-spp render(), main.cpp:381-446) replays 4 phases per host
  * poll instead of 8, so a per-frame call does not keep the pool a quarter full
- * for 8 phases per frame. */
-constexpr int kPhasesShort = 2;
+ * for 8 phases per frame.  4096 one-frame calls at 1280x720: 625 / 641 / 637
+ * Mrays/s with 2 / 4 / 8 phases (each replay's end joins its last k_connect,
+ * which then overlaps nothing; MEASUREMENTS round 5). */
+#ifndef SURF_PHASES_SHORT
+#define SURF_PHASES_SHORT 4
+#endif
+constexpr int kPhasesShort = SURF_PHASES_SHORT;
+static_assert(kPhasesShort % 2 == 0 && kPhasesShort <= kPhasesPerGraph, "even: parity returns to 0 after a replay");
 constexpr int kPhaseEvents = 6;             /* profiling events per phase: sort, extend, shade, sort, connect, regen */
 constexpr uint32_t kMaxStack = 120;          /* LDS stack entries per ray (block 256 -> 120 KiB max) */
 constexpr uint64_t kMaxIterations = 1ull << 22;  /* safety net: a path longer than this is a bug */
@@ -127,9 +133,28 @@ struct surf_ctx {
     float4* acc = nullptr;
     uint32_t* dRows = nullptr;
     Counters* ctr = nullptr;
-    Counters* hctr = nullptr;      /* pinned */
+    Counters* hctr = nullptr;      /* pinned: the counters as of the last consumed snapshot */
     uint32_t* frameDone = nullptr; /* [kStripes][window] completions per frame slot */
-    uint32_t* hFrameDone = nullptr;/* pinned */
+    /* host snapshots of the counters and of the open passes' completion
+     * stripes, each taken after a graph replay; a lagged one-frame call may
+     * return with up to kSnaps of them (and their replays) in flight, so the
+     * GPU keeps working while the application runs its loop (pump) */
+    struct Snap { Counters* h = nullptr; uint32_t* fd = nullptr; uint64_t acc = 0, open = 0; int replays = 0; hipEvent_t ev = nullptr; };
+    static constexpr int kSnaps = 2;
+    Snap snap[kSnaps];
+    int snapHead = 0, snapCount = 0;
+    uint64_t issuePerReplay = 0;   /* chains a replay issued, last seen: what the replays in flight will issue */
+    bool pipeline = true;          /* SURF_PIPELINE=0: every replay waited for before the next (and before a call returns) */
+    /* issue limits pushed to the device: a ring of pinned sources, so a later
+     * push never rewrites the bytes an earlier, still queued copy reads */
+    static constexpr uint32_t kLimitRing = 16;
+    uint64_t* hLimit = nullptr;
+    uint32_t hLimitNext = 0;
+    /* device time of calls that return with replays in flight: two event
+     * pairs used in turn, read once their end has passed */
+    hipEvent_t tev[2][2] = {};
+    bool tevPending[2] = {false, false};
+    int tevCur = 0;
     uint32_t* dOutRGBA = nullptr;
     std::vector<void*> wfAllocs;
     uint64_t totalSamples = 0;     /* frames rendered since the last clear (samples per pixel) */
@@ -153,7 +178,7 @@ struct surf_ctx {
     uint32_t coopMax = 0;          /* survivors handled by the cooperative tail (one path per wave) */
     uint32_t coopAll = 150000;     /* drain paths left to the cooperative tail (surf_set_tail_coop); C3 drain 176-184 ms at 60000, 172-178 at 150000 */
     int drainReplays = 1;          /* graph replays per host poll while draining (SURF_DRAIN_REPLAYS) */
-    bool drainShort = false;       /* 2-phase replays once nothing is left to issue (SURF_DRAIN_SHORT=1; measured slower, MEASUREMENTS round 5) */
+    bool drainShort = false;       /* short replays once nothing is left to issue (SURF_DRAIN_SHORT=1; measured slower, MEASUREMENTS round 5) */
     bool regenFirst = false;       /* k_regen before the connect fork (SURF_REGEN_FIRST=1; measured equal, MEASUREMENTS round 5) */
     bool coopEligible = false;     /* single-leaf TLAS of <= 64 instances, LDS tables (the four-rows engine) */
     int traceMode = 0;             /* surf_trace_closest/_any: 0 one ray per lane, 1 one ray per wave, 2 one ray per 16-lane row */
@@ -373,8 +398,16 @@ int allocWavefront(surf_ctx* c) {
     if ((rc = devAlloc(c, c->wfAllocs, &c->Q.cur, (size_t)2 * kShSegs * kShStride))) return rc;
     if ((rc = devAlloc(c, c->wfAllocs, &c->ctr, 1))) return rc;
     if ((rc = devAlloc(c, c->wfAllocs, &c->dOutRGBA, c->npx))) return rc;
-    if (hipHostMalloc((void**)&c->hctr, sizeof(Counters), hipHostMallocDefault) != hipSuccess)
+    if (hipHostMalloc((void**)&c->hctr, sizeof(Counters), hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void**)&c->hLimit, surf_ctx::kLimitRing * sizeof(uint64_t), hipHostMallocDefault) != hipSuccess)
         return fail(c, SURF_ERR_OOM, "hipHostMalloc of the counter block failed");
+    for (auto& sn : c->snap) {
+        if (hipHostMalloc((void**)&sn.h, sizeof(Counters), hipHostMallocDefault) != hipSuccess)
+            return fail(c, SURF_ERR_OOM, "hipHostMalloc of a counter snapshot failed");
+        SURF_CHECK(c, hipEventCreateWithFlags(&sn.ev, hipEventDisableTiming));
+    }
+    for (auto& pr : c->tev)
+        for (auto& e : pr) SURF_CHECK(c, hipEventCreate(&e));
     for (auto& e : c->pev) SURF_CHECK(c, hipEventCreate(&e));
     if (const char* e = std::getenv("SURF_PHASE_LOG")) {         /* diagnostics: per-phase cost vs size */
         if (hipHostMalloc((void**)&c->hPhaseN, kPhasesPerGraph * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess)
@@ -447,17 +480,21 @@ int ensureWindow(surf_ctx* c, uint64_t frames, uint32_t spp) {
     if (c->rad && want == c->window) return SURF_OK;
     if (c->rad) {
         SURF_CHECK(c, hipStreamSynchronize(c->stream));
-        (void)hipFree(c->rad); (void)hipFree(c->frameDone); (void)hipHostFree(c->hFrameDone);
-        c->rad = nullptr; c->frameDone = nullptr; c->hFrameDone = nullptr;
+        (void)hipFree(c->rad); (void)hipFree(c->frameDone);
+        for (auto& sn : c->snap) { (void)hipHostFree(sn.fd); sn.fd = nullptr; }
+        c->rad = nullptr; c->frameDone = nullptr;
         destroyGraph(c);                          /* the ring and the window are kernel arguments */
     }
     c->window = (uint32_t)want;
-    if (hipMalloc(&c->rad, (size_t)c->npx * c->window * sizeof(float4)) != hipSuccess ||
-        hipMalloc(&c->frameDone, (size_t)kStripes * c->window * sizeof(uint32_t)) != hipSuccess ||
-        hipHostMalloc((void**)&c->hFrameDone, (size_t)kStripes * c->window * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess) {
+    bool ok = hipMalloc(&c->rad, (size_t)c->npx * c->window * sizeof(float4)) == hipSuccess &&
+              hipMalloc(&c->frameDone, (size_t)kStripes * c->window * sizeof(uint32_t)) == hipSuccess;
+    for (auto& sn : c->snap)
+        ok = ok && hipHostMalloc((void**)&sn.fd, (size_t)kStripes * c->window * sizeof(uint32_t), hipHostMallocDefault) == hipSuccess;
+    if (!ok) {
         if (c->rad) (void)hipFree(c->rad);
         if (c->frameDone) (void)hipFree(c->frameDone);
-        c->rad = nullptr; c->frameDone = nullptr; c->hFrameDone = nullptr;
+        for (auto& sn : c->snap) { if (sn.fd) (void)hipHostFree(sn.fd); sn.fd = nullptr; }
+        c->rad = nullptr; c->frameDone = nullptr;
         return fail(c, SURF_ERR_OOM, "radiance ring of " + std::to_string(c->window) + " frames does not fit");
     }
     return SURF_OK;
@@ -664,8 +701,9 @@ uint64_t targetPasses(const surf_ctx* c) { return c->targetFrames * c->spp; }
 int pushLimit(surf_ctx* c) {
     const uint64_t lim = issueLimit(c);
     if (lim == c->pushedLimit) return SURF_OK;
-    c->hctr->limit = lim;
-    SURF_CHECK(c, hipMemcpyAsync(&c->ctr->limit, &c->hctr->limit, sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
+    uint64_t* src = &c->hLimit[c->hLimitNext++ % surf_ctx::kLimitRing];
+    *src = lim;
+    SURF_CHECK(c, hipMemcpyAsync(&c->ctr->limit, src, sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
     c->pushedLimit = lim;
     return SURF_OK;
 }
@@ -679,10 +717,10 @@ uint64_t fullyIssuedFrames(const surf_ctx* c, uint64_t iss) {
     return iss <= endA ? 0 : (iss - endA) / (c->npx - c->permA);
 }
 
-/* Finished paths of a frame slot: sum over the completion stripes. */
-uint64_t framePaths(const surf_ctx* c, uint32_t slot) {
+/* Finished paths of a frame slot in a snapshot: sum over the completion stripes. */
+uint64_t framePaths(const surf_ctx* c, const uint32_t* fd, uint32_t slot) {
     uint64_t n = 0;
-    for (uint32_t k = 0; k < kStripes; ++k) n += c->hFrameDone[(size_t)k * c->window + slot];
+    for (uint32_t k = 0; k < kStripes; ++k) n += fd[(size_t)k * c->window + slot];
     return n;
 }
 
@@ -694,31 +732,59 @@ void streamEvents(const Counters& h, unsigned long long out[kEvents]) {
     }
 }
 
-/* Reads counters + per-pass completion (one sync) and accumulates, in pass
- * order, every leading pass whose samples have all finished. */
-int syncAndAccumulate(surf_ctx* c) {
-    SURF_CHECK(c, hipMemcpyAsync(c->hctr, c->ctr, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
-    /* completion counts of the open passes only ([accPasses, targetPasses),
-     * at most a window): a strided copy of their slots in each stripe row */
+/* Queues a snapshot of the counters and of the open passes' completion
+ * stripes ([accPasses, targetPasses), at most a window: a strided copy of
+ * their slots in each stripe row), taken after `replays` graph replays. */
+int enqueueSnap(surf_ctx* c, int replays) {
+    surf_ctx::Snap& sn = c->snap[(c->snapHead + c->snapCount) % surf_ctx::kSnaps];
+    SURF_CHECK(c, hipMemcpyAsync(sn.h, c->ctr, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
     const uint64_t tp = targetPasses(c);
     const uint64_t open = std::min<uint64_t>(tp - std::min(c->accPasses, tp), c->window);
     const uint32_t s0 = (uint32_t)(c->accPasses % c->window);
     const uint32_t n0 = (uint32_t)std::min<uint64_t>(open, c->window - s0);
     const size_t pitch = (size_t)c->window * sizeof(uint32_t);
     if (n0)
-        SURF_CHECK(c, hipMemcpy2DAsync(c->hFrameDone + s0, pitch, c->frameDone + s0, pitch, n0 * sizeof(uint32_t), kStripes,
+        SURF_CHECK(c, hipMemcpy2DAsync(sn.fd + s0, pitch, c->frameDone + s0, pitch, n0 * sizeof(uint32_t), kStripes,
                                        hipMemcpyDeviceToHost, c->stream));
     if (open > n0)
-        SURF_CHECK(c, hipMemcpy2DAsync(c->hFrameDone, pitch, c->frameDone, pitch, (open - n0) * sizeof(uint32_t), kStripes,
+        SURF_CHECK(c, hipMemcpy2DAsync(sn.fd, pitch, c->frameDone, pitch, (open - n0) * sizeof(uint32_t), kStripes,
                                        hipMemcpyDeviceToHost, c->stream));
-    SURF_CHECK(c, hipStreamSynchronize(c->stream));
-    /* a pass is complete when all its samples were issued and all finished; a
-     * slot is reused only after its pass is accumulated, so passes of frames
-     * not yet fully issued must not be tested (their slot may still count an
-     * older pass) */
-    uint64_t f = c->accPasses;
+    SURF_CHECK(c, hipEventRecord(sn.ev, c->stream));
+    sn.acc = c->accPasses;
+    sn.open = open;
+    sn.replays = replays;
+    ++c->snapCount;
+    return SURF_OK;
+}
+
+/* Waits for the oldest snapshot, makes it the host's view of the counters and
+ * accumulates, in pass order, every leading pass whose samples have all
+ * finished in it.  A pass is complete when all its samples were issued and
+ * all finished; a slot is reused only after its pass is accumulated, so passes
+ * of frames not yet fully issued must not be tested (their slot may still
+ * count an older pass), nor passes past the snapshot's copied range.  Later
+ * replays already queued cannot touch the slots accumulated here: the issue
+ * limit they run under was pushed before this accumulation. */
+int consumeSnap(surf_ctx* c) {
+    surf_ctx::Snap& sn = c->snap[c->snapHead];
+    SURF_CHECK(c, hipEventSynchronize(sn.ev));
+    const uint64_t before = c->hctr->issued[0];
+    std::memcpy(c->hctr, sn.h, sizeof(Counters));
+    if (sn.replays > 0 && c->hctr->issued[0] > before) c->issuePerReplay = (c->hctr->issued[0] - before) / (uint64_t)sn.replays;
+    c->snapHead = (c->snapHead + 1) % surf_ctx::kSnaps;
+    --c->snapCount;
+    for (int k = 0; k < 2; ++k)                       /* calls whose end this snapshot has passed */
+        if (c->tevPending[k] && hipEventQuery(c->tev[k][1]) == hipSuccess) {
+            float ms = 0;
+            (void)hipEventElapsedTime(&ms, c->tev[k][0], c->tev[k][1]);
+            c->stats.ms_total += ms;
+            c->tevPending[k] = false;
+        }
+    const uint64_t tp = targetPasses(c);
     const uint64_t issuedPasses = fullyIssuedFrames(c, c->hctr->issued[0]) * c->spp;
-    while (f < tp && f < issuedPasses && framePaths(c, f % c->window) == c->npx) ++f;
+    const uint64_t hi = sn.acc + sn.open;
+    uint64_t f = c->accPasses;
+    while (f < tp && f < issuedPasses && f < hi && framePaths(c, sn.fd, (uint32_t)(f % c->window)) == c->npx) ++f;
     if (f == c->accPasses) return SURF_OK;
     const uint32_t count = (uint32_t)(f - c->accPasses);
     const uint32_t threads = std::max<uint32_t>(c->npx, count * kStripes);
@@ -727,6 +793,20 @@ int syncAndAccumulate(surf_ctx* c) {
     SURF_CHECK(c, hipGetLastError());
     c->accPasses = f;
     return pushLimit(c);
+}
+
+int consumeAll(surf_ctx* c) {
+    int rc;
+    while (c->snapCount)
+        if ((rc = consumeSnap(c))) return rc;
+    return SURF_OK;
+}
+
+/* Reads counters + per-pass completion (one sync) and accumulates. */
+int syncAndAccumulate(surf_ctx* c, int replays = 0) {
+    int rc;
+    if ((rc = consumeAll(c)) || (rc = enqueueSnap(c, replays))) return rc;
+    return consumeSnap(c);
 }
 
 /* One unit of forward progress: kPhasesPerGraph phases (graph replay, or
@@ -931,18 +1011,33 @@ uint32_t tailThreshold(const surf_ctx* c) {
 }
 
 /* Runs until every requested sample is issued (drain = false) or until every
- * requested frame is accumulated (drain = true). */
+ * requested frame is accumulated (drain = true).  A lagged one-frame call
+ * (the drop-in loop) runs pipelined: it queues the next replay before it has
+ * read the previous one's counters -- predicting what the replays in flight
+ * issue -- and may return with up to kSnaps replays in flight, so the GPU
+ * does not wait for the host between calls.  Everything else (drains, the
+ * tail, a starved stream) decides from fresh counters. */
 int pump(surf_ctx* c, bool drain, uint64_t lag) {
     int rc;
+    const bool pipe = c->pipeline && !drain && lag > 0;
+    if (!pipe && (rc = consumeAll(c))) return rc;
     if ((rc = pushLimit(c))) return rc;
     const uint64_t target = c->targetFrames * (uint64_t)c->npx;
     for (;;) {
+        if (pipe)       /* the snapshots that have landed, and the oldest when both are in flight */
+            while (c->snapCount && (c->snapCount == surf_ctx::kSnaps || hipEventQuery(c->snap[c->snapHead].ev) == hipSuccess))
+                if ((rc = consumeSnap(c))) return rc;
         const uint64_t issued = c->hctr->issued[0];
+        const uint64_t ahead = (uint64_t)c->snapCount * c->issuePerReplay;   /* what the replays in flight issue */
         /* in flight at a replay boundary: the pool the next phase extends */
         const uint32_t inflight = c->hctr->nIn[0];
-        if (!drain && issued + lag >= target) return SURF_OK;
+        if (!drain && issued + ahead + lag >= target) return SURF_OK;
         if (drain && c->accPasses >= targetPasses(c)) return SURF_OK;
         const bool starved = issued >= c->pushedLimit;     /* nothing more may be issued right now */
+        if (c->snapCount && starved) {                     /* decided from fresh counters */
+            if ((rc = consumeAll(c))) return rc;
+            continue;
+        }
         const uint64_t accBefore = c->accPasses;
         static const bool dbgDrain = std::getenv("SURF_DEBUG_DRAIN") != nullptr;   /* diagnostics: drain timeline */
         if (dbgDrain && starved) {
@@ -952,6 +1047,7 @@ int pump(surf_ctx* c, bool drain, uint64_t lag) {
                          (unsigned long long)targetPasses(c),
                          std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tS).count());
         }
+        int reps = 0;
         if (starved && inflight > 0 && inflight <= tailThreshold(c)) {
             if ((rc = runTail(c))) return rc;
         } else if (starved && inflight == 0) {
@@ -959,24 +1055,47 @@ int pump(surf_ctx* c, bool drain, uint64_t lag) {
         } else {
             /* draining (nothing left to issue): several replays per host poll --
              * the per-replay poll, not the kernels, is what a small pool pays */
-            const int reps = starved ? c->drainReplays : 1;
+            reps = starved ? c->drainReplays : 1;
             /* a per-frame render call (lagged, or at most one frame left to
              * issue): short replays (SURF_DRAIN_SHORT=1: also once nothing is
-             * left to issue, so the drain takes over within 2 phases instead
+             * left to issue, so the drain takes over within kPhasesShort phases instead
              * of up to 8 -- measured slower) */
             const bool shortRun = (!drain && (lag > 0 || target - issued <= c->npx)) || (starved && c->drainShort);
             for (int k = 0; k < reps; ++k)
                 if ((rc = advance(c, shortRun))) return rc;
+            if (pipe) {                                    /* read later: queue the next replay first */
+                if ((rc = enqueueSnap(c, reps))) return rc;
+                continue;
+            }
         }
-        if ((rc = syncAndAccumulate(c))) return rc;
+        if ((rc = syncAndAccumulate(c, reps))) return rc;
         if (starved && inflight == 0 && c->accPasses == accBefore)
             return fail(c, SURF_ERR_HIP, "sample stream stalled: pool empty but frames incomplete");
     }
 }
 
+/* Adds the device time of calls that returned with replays in flight (their
+ * ends have passed once the stream is idle). */
+void collectCallTimes(surf_ctx* c) {
+    for (int k = 0; k < 2; ++k)
+        if (c->tevPending[k]) {
+            (void)hipEventSynchronize(c->tev[k][1]);
+            float ms = 0;
+            (void)hipEventElapsedTime(&ms, c->tev[k][0], c->tev[k][1]);
+            c->stats.ms_total += ms;
+            c->tevPending[k] = false;
+        }
+}
+
 int ensureDrained(surf_ctx* c) {
-    if (!c->streamActive || c->accPasses >= targetPasses(c)) return SURF_OK;
+    if (!c->streamActive) return SURF_OK;
     SURF_CHECK(c, hipSetDevice(c->device));
+    {
+        const int rc = consumeAll(c);                 /* the host's counters as of the last replay */
+        if (rc) return rc;
+        collectCallTimes(c);
+    }
+    if (c->accPasses >= targetPasses(c)) return SURF_OK;
     if (!c->profiling) {
         int rc = buildGraph(c);
         if (rc) return rc;
@@ -1057,6 +1176,7 @@ int createCtx(int dev, uint32_t w, uint32_t h, std::vector<uint32_t> rows, surf_
     if (const char* e = std::getenv("SURF_TAIL_PAIR")) c->tailPair = e[0] != '0';
     if (const char* e = std::getenv("SURF_DRAIN_SHORT")) c->drainShort = e[0] == '1';
     if (const char* e = std::getenv("SURF_REGEN_FIRST")) c->regenFirst = e[0] == '1';
+    if (const char* e = std::getenv("SURF_PIPELINE")) c->pipeline = e[0] != '0';
     c->width = w;
     c->height = h;
     c->rows = std::move(rows);
@@ -1118,7 +1238,14 @@ void surf_destroy(surf_ctx* c) {
     freeList(c->sceneAllocs);
     freeList(c->wfAllocs);
     if (c->hctr) (void)hipHostFree(c->hctr);
-    if (c->hFrameDone) (void)hipHostFree(c->hFrameDone);
+    if (c->hLimit) (void)hipHostFree(c->hLimit);
+    for (auto& sn : c->snap) {
+        if (sn.h) (void)hipHostFree(sn.h);
+        if (sn.fd) (void)hipHostFree(sn.fd);
+        if (sn.ev) (void)hipEventDestroy(sn.ev);
+    }
+    for (auto& pr : c->tev)
+        for (auto& e : pr) if (e) (void)hipEventDestroy(e);
     if (c->rad) (void)hipFree(c->rad);
     if (c->frameDone) (void)hipFree(c->frameDone);
     for (auto& e : c->pev) if (e) (void)hipEventDestroy(e);
@@ -1762,21 +1889,37 @@ int surf_render(surf_ctx* c, uint32_t frames, uint32_t firstSample, uint32_t max
         if ((rc = startStream(c, firstSample, maxSeg, frames, spp))) return rc;
     }
     if (!c->profiling && (rc = buildGraph(c))) return rc;         /* (re)captured if the ring moved */
-    SURF_CHECK(c, hipEventRecord(c->ev0, c->stream));
+    /* this call's device time: an event pair of its own (the pair two calls
+     * back is read first, if that call returned with replays in flight) */
+    const int tp = c->tevCur;
+    if (c->tevPending[tp]) {
+        SURF_CHECK(c, hipEventSynchronize(c->tev[tp][1]));
+        float ms0 = 0;
+        (void)hipEventElapsedTime(&ms0, c->tev[tp][0], c->tev[tp][1]);
+        c->stats.ms_total += ms0;
+        c->tevPending[tp] = false;
+    }
+    SURF_CHECK(c, hipEventRecord(c->tev[tp][0], c->stream));
     c->targetFrames += frames;
     /* A one-frame call (the drop-in loop, main.cpp:381-446) may return with up
      * to a pool's worth of its stream not yet issued: the next calls, or the
      * drain a read of the accumulator starts, issue it.  Issuing each call's
-     * frame at once would run 2 phases per frame on a pool a third full
+     * frame at once would run a short replay per frame on a pool a third full
      * (DESIGN 4 "Pool sizing"); with the lag the pool stays full and the
      * calls replay only as many phases as the stream retires. */
     const uint64_t lag = frames == 1 && c->loopLag ? c->capacity : 0;
     if ((rc = pump(c, false, lag))) return rc;
-    SURF_CHECK(c, hipEventRecord(c->ev1, c->stream));
-    SURF_CHECK(c, hipEventSynchronize(c->ev1));
-    float ms = 0;
-    (void)hipEventElapsedTime(&ms, c->ev0, c->ev1);
-    c->stats.ms_total += ms;
+    SURF_CHECK(c, hipEventRecord(c->tev[tp][1], c->stream));
+    if (c->snapCount) {
+        /* replays still in flight (a pipelined one-frame call): timed when read */
+        c->tevPending[tp] = true;
+        c->tevCur ^= 1;
+    } else {
+        SURF_CHECK(c, hipEventSynchronize(c->tev[tp][1]));
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, c->tev[tp][0], c->tev[tp][1]);
+        c->stats.ms_total += ms;
+    }
     c->totalSamples += (uint64_t)frames * spp;
     c->stats.samples += (uint64_t)frames * spp * c->npx;
     return SURF_OK;

@@ -630,6 +630,36 @@ def test_dropin_loop_lag_across_reads_and_updates():
         p.close()
 
 
+@pytest.mark.parametrize("pipeline", ["1", "0"], ids=["replays-in-flight", "synchronous"])
+def test_dropin_loop_pipelined_bitexact(pipeline, monkeypatch):
+    """A long drop-in loop (one frame per call, far past the lag's pool): each
+    call queues its replays before reading the previous one's counters and may
+    return with replays in flight (SURF_PIPELINE, default on); a read in the
+    middle and at the end drains them.  The accumulators equal the oracle's
+    bit for bit, and every call's device time is counted once."""
+    monkeypatch.setenv("SURF_PIPELINE", pipeline)
+    W, H, N1, N2 = 32, 24, 17, 23
+    o = oracle.OracleScene()
+    p = surf_amd.Scene.indoor()
+    try:
+        r = surf_amd.Renderer(p, W, H)
+        r.set_zero_cutoff(False)
+        for f in range(N1):
+            r.render(1, first_frame=f)
+        c1, _, _ = o.render(W, H, N1)
+        _assert_bitexact(r.accumulator(), c1, f"{N1} one-frame calls (pipeline={pipeline})")
+        for f in range(N1, N1 + N2):
+            r.render(1, first_frame=f)
+        st = r.stats()
+        assert st["samples"] == W * H * (N1 + N2) and st["ms_total"] > 0.0
+        c2, _, _ = o.render(W, H, N1 + N2)
+        _assert_bitexact(r.accumulator(), c2, f"{N1 + N2} one-frame calls (pipeline={pipeline})")
+        r.close()
+    finally:
+        o.close()
+        p.close()
+
+
 def test_c5_deep_bvh_bitexact():
     """C5: 10.2M-triangle lattice BLAS (HBM-resident, depth 36,
     built by the parallel builder) -- hit records, a small render and three row
