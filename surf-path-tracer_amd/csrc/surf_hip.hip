@@ -1011,15 +1011,15 @@ uint32_t tailThreshold(const surf_ctx* c) {
 }
 
 /* Runs until every requested sample is issued (drain = false) or until every
- * requested frame is accumulated (drain = true).  A lagged one-frame call
- * (the drop-in loop) runs pipelined: it queues the next replay before it has
- * read the previous one's counters -- predicting what the replays in flight
- * issue -- and may return with up to kSnaps replays in flight, so the GPU
- * does not wait for the host between calls.  Everything else (drains, the
- * tail, a starved stream) decides from fresh counters. */
+ * requested frame is accumulated (drain = true).  While issuing, a call runs
+ * pipelined: it queues the next replay before it has read the previous one's
+ * counters -- predicting what the replays in flight issue -- and may return
+ * with up to kSnaps replays in flight, so the GPU does not wait for the host
+ * between polls or calls (the drop-in loop's one-frame calls).  Drains, the
+ * tail and a starved stream decide from fresh counters. */
 int pump(surf_ctx* c, bool drain, uint64_t lag) {
     int rc;
-    const bool pipe = c->pipeline && !drain && lag > 0;
+    const bool pipe = c->pipeline && !drain;
     if (!pipe && (rc = consumeAll(c))) return rc;
     if ((rc = pushLimit(c))) return rc;
     const uint64_t target = c->targetFrames * (uint64_t)c->npx;
