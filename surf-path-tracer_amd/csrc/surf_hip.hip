@@ -420,10 +420,10 @@ int allocWavefront(surf_ctx* c) {
     c->gridWork = (uint32_t)std::min<uint64_t>(maxBlocks, (uint64_t)cus * perCu);
     /* per-kernel grids (measured): k_extend gains from one ray per
      * thread (latency hiding across many short-lived blocks), k_connect peaks
-     * at 14 workgroups per CU with its LDS-staged light BLAS (5 resident: the
-     * grid-stride chunks per workgroup quantize its tail), k_shade
-     * at 8 */
-    uint64_t extPerCu = 48, conPerCu = 14;
+     * at 14-15 workgroups per CU with its LDS-staged light BLAS (5 resident:
+     * the dispatcher rebalances the grid-stride chunks; past ~15 every extra
+     * workgroup re-stages the BLAS -- MEASUREMENTS round 5), k_shade at 8 */
+    uint64_t extPerCu = 48, conPerCu = 15;
     const char* eExt = std::getenv("SURF_GRID_EXTEND");
     if (eExt) extPerCu = (uint64_t)std::max(1, std::atoi(eExt));
     if (const char* e = std::getenv("SURF_GRID_CONNECT")) conPerCu = (uint64_t)std::max(1, std::atoi(e));
