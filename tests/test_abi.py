@@ -69,3 +69,21 @@ def test_mgpu_library_exports_every_declared_symbol():
     deps = subprocess.run(["ldd", surf_amd.MGPU_LIB_PATH], capture_output=True, text=True).stdout
     assert "librccl" in deps
     assert "librccl" not in subprocess.run(["ldd", surf_amd.LIB_PATH], capture_output=True, text=True).stdout
+
+
+def test_stats_struct_layout_matches_the_header(tmp_path):
+    """surf_stats as the C compiler lays it out (include/surf_hip.h) equals the
+    ctypes mirror the Python binding passes to surf_get_stats: size and every
+    field's offset."""
+    import ctypes as C
+    fields = [f[0] for f in surf_amd.Stats._fields_]
+    src = tmp_path / "layout.c"
+    src.write_text("#include <stdio.h>\n#include <stddef.h>\n#include \"surf_hip.h\"\nint main(void) {\n"
+                   "  printf(\"size %zu\\n\", sizeof(surf_stats));\n" +
+                   "".join(f"  printf(\"{f} %zu\\n\", offsetof(surf_stats, {f}));\n" for f in fields) + "  return 0;\n}\n")
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.dirname(HEADER), str(src), "-o", str(exe)], check=True)
+    got = dict(line.split() for line in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.splitlines())
+    assert int(got["size"]) == C.sizeof(surf_amd.Stats)
+    for f in fields:
+        assert int(got[f]) == getattr(surf_amd.Stats, f).offset, f
