@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define SURF_ABI_VERSION 3
+#define SURF_ABI_VERSION 4
 
 typedef enum {
     SURF_OK = 0,
@@ -138,11 +138,6 @@ typedef struct surf_scene surf_scene;   /* host-side scene built by this library
 
 /* ---- version / device ---- */
 int surf_abi_version(void);
-/* Optional engines compiled into this library (bit mask): SURF_FEATURE_ROWS_ENGINE
- * -- the four-paths-per-wave drain and trace mode 2 (make ROWS=1; measured
- * equal to the default partner-wave drain).  No reference counterpart. */
-#define SURF_FEATURE_ROWS_ENGINE 1
-int surf_build_features(void);
 int surf_device_count(int* count);
 
 /* ---- context ----
@@ -226,9 +221,7 @@ int surf_set_tail_policy(surf_ctx* ctx, uint32_t threshold_paths, uint32_t lanes
  * instances, materials or lights the tables are read from global memory), in
  * two-wave workgroups whose idle wave traces its sibling's shadow rays once
  * the path queue is empty (SURF_TAIL_PAIR=0 in the environment: one-wave
- * workgroups); with a ROWS=1 build and SURF_TAIL_ROWS=1 at surf_create, four
- * paths per wave (one per 16-lane row, a path queue; single-leaf TLAS of <= 16
- * instances, 1-sample frames).  Identical results. */
+ * workgroups).  Identical results. */
 int surf_set_tail_coop(surf_ctx* ctx, uint32_t max_paths);
 /* Diagnostics: how many paths the segment cap ended in the current sample
  * stream, and the sample ids (frame slot * shard pixels + pixel) of up to
@@ -250,6 +243,11 @@ int surf_debug_segment_cycles(surf_ctx* ctx, const float* path12, uint32_t reps,
  * first (0: frame-major order throughout); heavy_pixels the size of that
  * heavy class (0 when permuted_frames is 0).  No reference counterpart. */
 int surf_debug_issue_order(surf_ctx* ctx, uint32_t* heavy_pixels, uint32_t* permuted_frames);
+/* Diagnostics: the emitters' BLAS staged in k_connect's LDS by the last phase
+ * launched (blasAnyStaged): its compact interior records and its triangles,
+ * both 0 when k_connect walked every BLAS from global memory.  No reference
+ * counterpart. */
+int surf_debug_connect_staging(surf_ctx* ctx, uint32_t* records, uint32_t* triangles);
 /* When enabled, per-kernel device times are measured with HIP events on the
  * render stream (slower: disables the graph replay). */
 int surf_set_profiling(surf_ctx* ctx, int enabled);
@@ -317,10 +315,9 @@ int surf_trace_closest(surf_ctx* ctx, uint32_t n, const float* o, const float* d
 int surf_trace_any(surf_ctx* ctx, uint32_t n, const float* o, const float* d, const float* tmax,
                    uint8_t* occluded);
 /* 0: one ray per lane (the wavefront kernels' traversal); 1: one ray per
- * 64-lane wave, lanes as the node record's planes (any TLAS; needs a BVH stack
- * of <= 64 entries); 2: one ray per 16-lane
- * row, four per wave (the drain's traversal; single-leaf TLAS of <= 16
- * instances, stack <= 64).  Results are identical; selects what surf_trace_* run. */
+ * 64-lane wave, lanes as the node record's planes (the drain's traversal; any
+ * TLAS; needs a BVH stack of <= 64 entries).  Results are identical; selects
+ * what surf_trace_* run. */
 int surf_set_trace_mode(surf_ctx* ctx, int mode);
 
 /* ---- host scene build (the reference's main.cpp scene, OBJ assets) ----

@@ -176,7 +176,7 @@ struct Counters {
     uint32_t segMax;                 /* longest finished path (extension rays), diagnostics */
     uint32_t survN;                  /* k_tail survivors appended (may exceed survCap) */
     uint32_t survCap;
-    uint32_t rowNext;                /* k_tail_rows work queue: next path to hand out */
+    uint32_t rowNext;                /* k_tail_pair path queue: next path to hand out */
     /* issue order of the stream's first permFrames frames: every frame's
      * samples of the permA pixels listed first in StreamGeom::perm, then each
      * frame's other pixels frame by frame (0: frame-major throughout) */
@@ -643,8 +643,9 @@ __device__ __forceinline__ bool traceScene(const DevScene& S, const TraceTables&
                 const float t1 = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
                 if (t1 < t0 || t1 < 0.0f || t0 >= depth) continue;
             }
-            /* (wave-uniform: the staged BLAS's instances walk it in LDS) */
-            const bool hitI = (STG && !LW && I.meta.x == S.sbNode0)
+            /* (wave-uniform: the staged BLAS's instances walk it in LDS; the
+             * staged triangles are those at S.sbTri0, so both offsets must match) */
+            const bool hitI = (STG && !LW && I.meta.x == S.sbNode0 && I.meta.y == S.sbTri0)
                                   ? instanceTrace<ANY, false, true, SK>(S, I, o, d, depth, hu, hv, hprim, stk, stride, 0u, sN)
                                   : instanceTrace<ANY, LW, false, SK>(S, I, o, d, depth, hu, hv, hprim, stk, stride, 0u);
             if (hitI) {

@@ -24,14 +24,6 @@
 
 #include "surf_hip.h"
 #include "device/wavefront_kernels.h"
-/* The four-paths-per-wave engine (k_tail_rows, trace mode 2) is measured equal
- * to the partner-wave drain and built only with SURF_ROWS_ENGINE=1 (make ROWS=1). */
-#ifndef SURF_ROWS_ENGINE
-#define SURF_ROWS_ENGINE 0
-#endif
-#if SURF_ROWS_ENGINE
-#include "device/rows_tail.h"
-#endif
 
 using namespace surfdev;
 
@@ -139,11 +131,11 @@ struct surf_ctx {
      * stripes, each taken after a graph replay; a lagged one-frame call may
      * return with up to kSnaps of them (and their replays) in flight, so the
      * GPU keeps working while the application runs its loop (pump) */
-    struct Snap { Counters* h = nullptr; uint32_t* fd = nullptr; uint64_t acc = 0, open = 0; int replays = 0; hipEvent_t ev = nullptr; };
+    struct Snap { Counters* h = nullptr; uint32_t* fd = nullptr; uint64_t acc = 0, open = 0; int phases = 0; hipEvent_t ev = nullptr; };
     static constexpr int kSnaps = 2;
     Snap snap[kSnaps];
     int snapHead = 0, snapCount = 0;
-    uint64_t issuePerReplay = 0;   /* chains a replay issued, last seen: what the replays in flight will issue */
+    uint64_t issuePerPhase = 0;    /* chains a phase issued in the last unstarved snapshot of this stream: what the replays in flight will issue */
     bool pipeline = true;          /* SURF_PIPELINE=0: every replay waited for before the next (and before a call returns) */
     /* issue limits pushed to the device: a ring of pinned sources, so a later
      * push never rewrites the bytes an earlier, still queued copy reads */
@@ -180,9 +172,8 @@ struct surf_ctx {
     int drainReplays = 1;          /* graph replays per host poll while draining (SURF_DRAIN_REPLAYS) */
     bool drainShort = false;       /* short replays once nothing is left to issue (SURF_DRAIN_SHORT=1; measured slower, MEASUREMENTS round 5) */
     bool regenFirst = false;       /* k_regen before the connect fork (SURF_REGEN_FIRST=1; measured equal, MEASUREMENTS round 5) */
-    bool coopEligible = false;     /* single-leaf TLAS of <= 64 instances, LDS tables (the four-rows engine) */
-    int traceMode = 0;             /* surf_trace_closest/_any: 0 one ray per lane, 1 one ray per wave, 2 one ray per 16-lane row */
-    bool tailRows = false;         /* drain on k_tail_rows (four paths per wave; SURF_TAIL_ROWS=1) instead of k_tail_coop */
+    int traceMode = 0;             /* surf_trace_closest/_any: 0 one ray per lane, 1 one ray per wave */
+    bool connectStaged = false;    /* the last k_connect launched walked the emitters' BLAS from LDS (surf_debug_connect_staging) */
     bool tailPair = true;          /* cooperative drain on k_tail_pair (partner waves trace the shadow rays; SURF_TAIL_PAIR=0: k_tail_coop) */
     uint32_t cus = 256;            /* compute units of the device */
     bool sortRays = true;          /* order each phase's rays by start instance (SURF_SORT=0: off) */
@@ -265,12 +256,6 @@ uint32_t stackWords(const surf_ctx* c, uint32_t block) { return c->stackDepth * 
 /* one-ray-per-wave traversal (traceWave): a stack of node records, 16 words per
  * entry -- 64 with two-level records (blasWalk2 pushes whole W records) */
 uint32_t recStackWords(const surf_ctx* c) { return c->stackDepth * (c->S.wnodes ? 64u : 16u); }
-/* Dynamic LDS of the four-rows kernels: four record stacks, then the trace tables. */
-#if SURF_ROWS_ENGINE
-size_t rowsLds(const surf_ctx* c) {
-    return ((size_t)4 * recStackWords(c) + kRowProWords) * sizeof(float) + (size_t)c->nInstances * (sizeof(TraceInst) + sizeof(uint32_t));
-}
-#endif
 /* Dynamic LDS of the one-ray-per-wave kernels: the record stack, the prologue
  * table (16 words per instance), then the trace tables; k_tail_coop adds the
  * shading tables (coopTailLds). */
@@ -573,6 +558,7 @@ void launchPhase(surf_ctx* c, int ph, hipEvent_t* ev) {
     /* staged only where the copy still leaves 5 workgroups of 256 per CU
      * (k_connect's residency; 144 B of static LDS each) */
     const bool stg = ldsC && !c->S.laneW && c->S.sbRecN > 0u && (stgLds + 256) * 5 <= 163840;
+    c->connectStaged = stg;
     auto connectK = c->S.laneW ? (ldsC ? k_connect<true, true> : k_connect<false, true>)
                                : (ldsC ? (stg ? k_connect<true, false, true> : k_connect<true, false>) : k_connect<false, false>);
     /* staged: 16-bit stack entries (half the stack's LDS) leave room for the
@@ -688,6 +674,7 @@ int startStream(surf_ctx* c, uint64_t baseFrame, uint32_t maxSeg, uint32_t frame
     c->spp = spp;
     c->streamMaxSeg = maxSeg;
     c->pushedLimit = 0;
+    c->issuePerPhase = 0;          /* predicted from this stream's own replays only */
     return SURF_OK;
 }
 
@@ -735,7 +722,7 @@ void streamEvents(const Counters& h, unsigned long long out[kEvents]) {
 /* Queues a snapshot of the counters and of the open passes' completion
  * stripes ([accPasses, targetPasses), at most a window: a strided copy of
  * their slots in each stripe row), taken after `replays` graph replays. */
-int enqueueSnap(surf_ctx* c, int replays) {
+int enqueueSnap(surf_ctx* c, int phases) {
     surf_ctx::Snap& sn = c->snap[(c->snapHead + c->snapCount) % surf_ctx::kSnaps];
     SURF_CHECK(c, hipMemcpyAsync(sn.h, c->ctr, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
     const uint64_t tp = targetPasses(c);
@@ -752,7 +739,7 @@ int enqueueSnap(surf_ctx* c, int replays) {
     SURF_CHECK(c, hipEventRecord(sn.ev, c->stream));
     sn.acc = c->accPasses;
     sn.open = open;
-    sn.replays = replays;
+    sn.phases = phases;
     ++c->snapCount;
     return SURF_OK;
 }
@@ -770,7 +757,10 @@ int consumeSnap(surf_ctx* c) {
     SURF_CHECK(c, hipEventSynchronize(sn.ev));
     const uint64_t before = c->hctr->issued[0];
     std::memcpy(c->hctr, sn.h, sizeof(Counters));
-    if (sn.replays > 0 && c->hctr->issued[0] > before) c->issuePerReplay = (c->hctr->issued[0] - before) / (uint64_t)sn.replays;
+    /* per phase (a replay is 8 or kPhasesShort phases), and only from a replay
+     * that issued under its limit the whole time: a starved one undercounts */
+    if (sn.phases > 0 && c->hctr->issued[0] > before && c->hctr->issued[0] < c->hctr->limit)
+        c->issuePerPhase = (c->hctr->issued[0] - before) / (uint64_t)sn.phases;
     c->snapHead = (c->snapHead + 1) % surf_ctx::kSnaps;
     --c->snapCount;
     for (int k = 0; k < 2; ++k)                       /* calls whose end this snapshot has passed */
@@ -803,9 +793,9 @@ int consumeAll(surf_ctx* c) {
 }
 
 /* Reads counters + per-pass completion (one sync) and accumulates. */
-int syncAndAccumulate(surf_ctx* c, int replays = 0) {
+int syncAndAccumulate(surf_ctx* c, int phases = 0) {
     int rc;
-    if ((rc = consumeAll(c)) || (rc = enqueueSnap(c, replays))) return rc;
+    if ((rc = consumeAll(c)) || (rc = enqueueSnap(c, phases))) return rc;
     return consumeSnap(c);
 }
 
@@ -865,14 +855,6 @@ void launchTail(surf_ctx* c, Pool in, uint32_t n, uint32_t lpw, uint32_t firstCo
 /* Any TLAS (traceWaveTlas walks one whose root splits or that holds > 64
  * instances); the TLAS stack is one VGPR (<= 64 entries). */
 bool waveEligible(const surf_ctx* c) { return c->hasScene && c->stackDepth <= 64 && coopLdsOk(c); }
-/* The four-rows traversal: a single-leaf TLAS with at most one instance per lane of a row, LDS tables. */
-#if SURF_ROWS_ENGINE
-bool rowsEligible(const surf_ctx* c) {
-    return waveEligible(c) && c->coopEligible && c->S.tlasLeafCount <= kRowInst && rowsLds(c) <= 65536;   /* four record stacks */
-}
-#else
-bool rowsEligible(const surf_ctx*) { return false; }
-#endif
 
 /* Regen counted each pool-0 path's next extension ray (firstCounted). */
 int runTail(surf_ctx* c) {
@@ -891,20 +873,6 @@ int runTail(surf_ctx* c) {
             const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
             std::fprintf(stderr, "[surf tail] stage %d: %u paths at %.2f ms\n", stage, cnt, ms);
         }
-#if SURF_ROWS_ENGINE
-        if (c->tailRows && rowsEligible(c) && c->spp == 1 && cnt <= c->coopAll) {   /* (the rows engine runs 1-sample frames) */
-            /* every remaining path through the row queue: as many four-row
-             * waves as are resident at once, each row taking the next path
-             * when its own ends */
-            const uint32_t blocks = std::min<uint32_t>((cnt + 3u) / 4u, c->cus * 4u * SURF_ROWS_WAVES);
-            SURF_CHECK(c, hipMemsetAsync(&c->ctr->rowNext, 0, sizeof(uint32_t), c->stream));
-            hipLaunchKernelGGL(k_tail_rows, dim3(blocks), dim3(64), rowsLds(c), c->stream, c->S, in, cnt, c->rad, c->frameDone,
-                               c->npx, c->window, c->ctr, recStackWords(c), firstCounted);
-            SURF_CHECK(c, hipGetLastError());
-            c->stats.tail_survivors += cnt;
-            break;
-        }
-#endif
         if (c->tailPair && waveEligible(c) && cnt <= c->coopAll) {
             /* as many two-wave workgroups as are resident at once, each wave
              * taking paths from the queue; idle waves trace their sibling's
@@ -1028,7 +996,10 @@ int pump(surf_ctx* c, bool drain, uint64_t lag) {
             while (c->snapCount && (c->snapCount == surf_ctx::kSnaps || hipEventQuery(c->snap[c->snapHead].ev) == hipSuccess))
                 if ((rc = consumeSnap(c))) return rc;
         const uint64_t issued = c->hctr->issued[0];
-        const uint64_t ahead = (uint64_t)c->snapCount * c->issuePerReplay;   /* what the replays in flight issue */
+        /* what the replays in flight issue: predicted per phase, never past the pushed limit */
+        uint64_t inflightPhases = 0;
+        for (int k = 0; k < c->snapCount; ++k) inflightPhases += (uint64_t)c->snap[(c->snapHead + k) % surf_ctx::kSnaps].phases;
+        const uint64_t ahead = std::min<uint64_t>(inflightPhases * c->issuePerPhase, c->pushedLimit - std::min(issued, c->pushedLimit));
         /* in flight at a replay boundary: the pool the next phase extends */
         const uint32_t inflight = c->hctr->nIn[0];
         if (!drain && issued + ahead + lag >= target) return SURF_OK;
@@ -1047,7 +1018,7 @@ int pump(surf_ctx* c, bool drain, uint64_t lag) {
                          (unsigned long long)targetPasses(c),
                          std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tS).count());
         }
-        int reps = 0;
+        int phases = 0;
         if (starved && inflight > 0 && inflight <= tailThreshold(c)) {
             if ((rc = runTail(c))) return rc;
         } else if (starved && inflight == 0) {
@@ -1055,7 +1026,7 @@ int pump(surf_ctx* c, bool drain, uint64_t lag) {
         } else {
             /* draining (nothing left to issue): several replays per host poll --
              * the per-replay poll, not the kernels, is what a small pool pays */
-            reps = starved ? c->drainReplays : 1;
+            const int reps = starved ? c->drainReplays : 1;
             /* a per-frame render call (lagged, or at most one frame left to
              * issue): short replays (SURF_DRAIN_SHORT=1: also once nothing is
              * left to issue, so the drain takes over within kPhasesShort phases instead
@@ -1063,12 +1034,13 @@ int pump(surf_ctx* c, bool drain, uint64_t lag) {
             const bool shortRun = (!drain && (lag > 0 || target - issued <= c->npx)) || (starved && c->drainShort);
             for (int k = 0; k < reps; ++k)
                 if ((rc = advance(c, shortRun))) return rc;
+            phases = reps * (shortRun ? kPhasesShort : kPhasesPerGraph);
             if (pipe) {                                    /* read later: queue the next replay first */
-                if ((rc = enqueueSnap(c, reps))) return rc;
+                if ((rc = enqueueSnap(c, phases))) return rc;
                 continue;
             }
         }
-        if ((rc = syncAndAccumulate(c, reps))) return rc;
+        if ((rc = syncAndAccumulate(c, phases))) return rc;
         if (starved && inflight == 0 && c->accPasses == accBefore)
             return fail(c, SURF_ERR_HIP, "sample stream stalled: pool empty but frames incomplete");
     }
@@ -1172,7 +1144,6 @@ int createCtx(int dev, uint32_t w, uint32_t h, std::vector<uint32_t> rows, surf_
     if (const char* e = std::getenv("SURF_CON_LDS_PAD")) c->conLdsPad = (size_t)std::max(0, std::atoi(e));
     if (const char* e = std::getenv("SURF_LDS_LIGHTBLAS")) c->ldsLightBlas = e[0] != '0';
     if (const char* e = std::getenv("SURF_REORDER")) c->reorder = e[0] != '0';
-    if (const char* e = std::getenv("SURF_TAIL_ROWS")) c->tailRows = e[0] == '1';
     if (const char* e = std::getenv("SURF_TAIL_PAIR")) c->tailPair = e[0] != '0';
     if (const char* e = std::getenv("SURF_DRAIN_SHORT")) c->drainShort = e[0] == '1';
     if (const char* e = std::getenv("SURF_REGEN_FIRST")) c->regenFirst = e[0] == '1';
@@ -1208,8 +1179,6 @@ int createCtx(int dev, uint32_t w, uint32_t h, std::vector<uint32_t> rows, surf_
 extern "C" {
 
 int surf_abi_version(void) { return SURF_ABI_VERSION; }
-
-int surf_build_features(void) { return SURF_ROWS_ENGINE ? SURF_FEATURE_ROWS_ENGINE : 0; }
 
 int surf_device_count(int* count) {
     if (!count) return SURF_ERR_INVALID;
@@ -1358,13 +1327,9 @@ int surf_set_tail_coop(surf_ctx* c, uint32_t max_paths) {
 
 int surf_set_trace_mode(surf_ctx* c, int mode) {
     if (!c) return fail(nullptr, SURF_ERR_INVALID, "ctx is NULL");
-    if (mode < 0 || mode > 2) return fail(c, SURF_ERR_INVALID, "trace mode must be 0, 1 or 2");
+    if (mode < 0 || mode > 1) return fail(c, SURF_ERR_INVALID, "trace mode must be 0 or 1");
     if (mode == 1 && !waveEligible(c))
         return fail(c, SURF_ERR_INVALID, "one-ray-per-wave traversal needs a BVH stack <= 64 entries");
-    if (mode == 2 && !SURF_ROWS_ENGINE)
-        return fail(c, SURF_ERR_INVALID, "one-ray-per-row traversal: this build has no rows engine (make ROWS=1)");
-    if (mode == 2 && !rowsEligible(c))
-        return fail(c, SURF_ERR_INVALID, "one-ray-per-row traversal needs a single-leaf TLAS of <= 16 instances and a BVH stack <= 64");
     c->traceMode = mode;
     return SURF_OK;
 }
@@ -1801,7 +1766,6 @@ int surf_upload_scene(surf_ctx* c, const surf_scene_desc* d) {
     c->S = S;
     c->ldsTables = d->instance_count <= kLdsInst && d->instance_count <= kLdsTraceInst && d->material_count <= kLdsMats &&
                    d->light_count <= kLdsLights;
-    c->coopEligible = c->ldsTables && S.tlasLeafCount > 0 && S.tlasLeafCount <= 64;
     c->stackDepth = depth;
     c->nInstances = d->instance_count;
     c->nLightsUp = d->light_count;
@@ -1835,7 +1799,6 @@ int surf_update_instances(surf_ctx* c, const surf_gpu_instance* instances, uint3
     if (nLights) SURF_CHECK(c, put(c->S.lights, IT.lights.data(), IT.lights.size() * sizeof(uint2)));
     c->S.tlasLeafCount = IT.tlasLeafCount;
     setKeys(c, c->S, IT);
-    c->coopEligible = c->ldsTables && c->S.tlasLeafCount > 0 && c->S.tlasLeafCount <= 64;
     c->stackDepth = std::max(c->stackDepth, depth);
     destroyGraph(c);                  /* kernel arguments carry the scene descriptor */
     return SURF_OK;
@@ -2042,7 +2005,7 @@ int surf_trace_closest(surf_ctx* c, uint32_t n, const float* o, const float* d, 
     if (!c || (n && (!o || !d || !ot || !ou || !ov || !oi || !op))) return SURF_ERR_INVALID;
     if (!c->hasScene) return fail(c, SURF_ERR_NO_SCENE, "no scene uploaded");
     if (n == 0) return SURF_OK;
-    if ((c->traceMode == 1 && !waveEligible(c)) || (c->traceMode == 2 && !rowsEligible(c)))
+    if (c->traceMode == 1 && !waveEligible(c))
         return fail(c, SURF_ERR_INVALID, "scene no longer fits the selected cooperative traversal");
     SURF_CHECK(c, hipSetDevice(c->device));
     std::vector<void*> tmp;
@@ -2052,12 +2015,6 @@ int surf_trace_closest(surf_ctx* c, uint32_t n, const float* o, const float* d, 
         (rc = devAlloc(c, tmp, &dT, n)) || (rc = devAlloc(c, tmp, &dI, n))) { freeList(tmp); return rc; }
     (void)hipMemcpyAsync(dO, o, 12 * (size_t)n, hipMemcpyHostToDevice, c->stream);
     (void)hipMemcpyAsync(dD, d, 12 * (size_t)n, hipMemcpyHostToDevice, c->stream);
-#if SURF_ROWS_ENGINE
-    if (c->traceMode == 2)
-        hipLaunchKernelGGL(k_trace_closest_rows, dim3((n + 3) / 4), dim3(64), rowsLds(c), c->stream, c->S, (const float*)dO,
-                           (const float*)dD, n, dT, dI, recStackWords(c));
-    else
-#endif
     if (c->traceMode == 1)
         hipLaunchKernelGGL(c->ldsTables ? (c->S.wnodes ? k_trace_closest_coop<true, true> : k_trace_closest_coop<true, false>)
                                         : (c->S.wnodes ? k_trace_closest_coop<false, true> : k_trace_closest_coop<false, false>),
@@ -2084,7 +2041,7 @@ int surf_trace_any(surf_ctx* c, uint32_t n, const float* o, const float* d, cons
     if (!c || (n && (!o || !d || !tm || !occ))) return SURF_ERR_INVALID;
     if (!c->hasScene) return fail(c, SURF_ERR_NO_SCENE, "no scene uploaded");
     if (n == 0) return SURF_OK;
-    if ((c->traceMode == 1 && !waveEligible(c)) || (c->traceMode == 2 && !rowsEligible(c)))
+    if (c->traceMode == 1 && !waveEligible(c))
         return fail(c, SURF_ERR_INVALID, "scene no longer fits the selected cooperative traversal");
     SURF_CHECK(c, hipSetDevice(c->device));
     std::vector<void*> tmp;
@@ -2095,12 +2052,6 @@ int surf_trace_any(surf_ctx* c, uint32_t n, const float* o, const float* d, cons
     (void)hipMemcpyAsync(dO, o, 12 * (size_t)n, hipMemcpyHostToDevice, c->stream);
     (void)hipMemcpyAsync(dD, d, 12 * (size_t)n, hipMemcpyHostToDevice, c->stream);
     (void)hipMemcpyAsync(dM, tm, 4 * (size_t)n, hipMemcpyHostToDevice, c->stream);
-#if SURF_ROWS_ENGINE
-    if (c->traceMode == 2)
-        hipLaunchKernelGGL(k_trace_any_rows, dim3((n + 3) / 4), dim3(64), rowsLds(c), c->stream, c->S, (const float*)dO,
-                           (const float*)dD, (const float*)dM, n, dR, recStackWords(c));
-    else
-#endif
     if (c->traceMode == 1)
         hipLaunchKernelGGL(c->ldsTables ? (c->S.wnodes ? k_trace_any_coop<true, true> : k_trace_any_coop<true, false>)
                                         : (c->S.wnodes ? k_trace_any_coop<false, true> : k_trace_any_coop<false, false>),
@@ -2116,6 +2067,13 @@ int surf_trace_any(surf_ctx* c, uint32_t n, const float* o, const float* d, cons
     hipError_t e = hipStreamSynchronize(c->stream);
     freeList(tmp);
     if (e != hipSuccess) return fail(c, SURF_ERR_HIP, std::string("trace_any: ") + hipGetErrorString(e));
+    return SURF_OK;
+}
+
+int surf_debug_connect_staging(surf_ctx* c, uint32_t* records, uint32_t* triangles) {
+    if (!c || !records || !triangles) return SURF_ERR_INVALID;
+    *records = c->connectStaged ? c->S.sbRecN : 0u;
+    *triangles = c->connectStaged ? c->S.sbTriN : 0u;
     return SURF_OK;
 }
 

@@ -92,7 +92,7 @@ def load() -> C.CDLL:
     lib = C.CDLL(path)
     P, U32, I32, F = C.c_void_p, C.c_uint32, C.c_int, C.c_float
     sig = {
-        "surf_abi_version": ([], I32), "surf_build_features": ([], I32), "surf_device_count": ([C.POINTER(I32)], I32),
+        "surf_abi_version": ([], I32), "surf_device_count": ([C.POINTER(I32)], I32),
         "surf_create": ([I32, U32, U32, U32, U32, C.POINTER(P)], I32),
         "surf_create_sharded": ([I32, U32, U32, U32, U32, U32, C.POINTER(P)], I32),
         "surf_destroy": ([P], None), "surf_last_error": ([P], C.c_char_p),
@@ -103,6 +103,7 @@ def load() -> C.CDLL:
         "surf_set_profiling": ([P, I32], I32), "surf_set_zero_cutoff": ([P, I32], I32), "surf_set_trace_mode": ([P, I32], I32), "surf_set_tail_policy": ([P, U32, U32, U32], I32), "surf_set_tail_coop": ([P, U32], I32),
         "surf_debug_capped": ([P, P, U32, C.POINTER(C.c_uint64)], I32),
         "surf_debug_issue_order": ([P, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)], I32),
+        "surf_debug_connect_staging": ([P, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)], I32),
         "surf_debug_segment_cycles": ([P, P, U32, P], I32),
         "surf_upload_scene": ([P, C.POINTER(SceneDesc)], I32),
         "surf_set_camera": ([P, P], I32),
@@ -213,14 +214,6 @@ def device_count() -> int:
     n = C.c_int(0)
     rc = load().surf_device_count(C.byref(n))
     return n.value if rc == SURF_OK else 0
-
-
-FEATURE_ROWS_ENGINE = 1
-
-
-def rows_engine() -> bool:
-    """Whether the library was built with the four-paths-per-wave engine (make ROWS=1)."""
-    return bool(load().surf_build_features() & FEATURE_ROWS_ENGINE)
 
 
 class Scene:
@@ -392,6 +385,13 @@ class Renderer:
         a, f = C.c_uint32(), C.c_uint32()
         _check(load().surf_debug_issue_order(self._h, C.byref(a), C.byref(f)), "surf_debug_issue_order", self._h)
         return int(a.value), int(f.value)
+
+    def debug_connect_staging(self):
+        """(records, triangles) of the emitters' BLAS the last k_connect launch
+        walked from LDS (surf_debug_connect_staging); (0, 0) when none was staged."""
+        a, t = C.c_uint32(), C.c_uint32()
+        _check(load().surf_debug_connect_staging(self._h, C.byref(a), C.byref(t)), "surf_debug_connect_staging", self._h)
+        return int(a.value), int(t.value)
 
     def debug_segment_cycles(self, origin, direction, throughput, seed: int, segment: int = 1, reps: int = 64):
         """Diagnostics: mean shader-clock cycles of one drain segment's pieces on

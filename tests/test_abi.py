@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     lib = surf_amd.load()
     missing = [f for f in declared_functions() if not hasattr(lib, f)]
     assert not missing, missing
-    assert lib.surf_abi_version() == 3
+    assert lib.surf_abi_version() == 4
 
 
 def test_exports_are_c_linkage():

@@ -30,10 +30,8 @@ def l2_report(a, b):
     return float(np.sqrt((per ** 2).mean())), float(per.max()), float((per > 1e-3).mean())
 
 
-@pytest.mark.parametrize("mode", [0, 1, 2], ids=["lane-per-ray", "wave-lanes-as-planes", "row-per-ray"])
+@pytest.mark.parametrize("mode", [0, 1], ids=["lane-per-ray", "wave-lanes-as-planes"])
 def test_closest_hit_records_bitexact(oracle_scene, product_scene, mode):
-    if mode == 2 and not surf_amd.rows_engine():
-        pytest.skip("four-rows engine not built (make ROWS=1)")
     W = H = 96
     (eo, ed), (so, sd, st) = oracle_scene.record_rays(W, H, 0, 0, W * H)
     rng = np.random.default_rng(5)
@@ -74,7 +72,7 @@ def test_boundary_rays_bitexact(oracle_scene, product_scene):
     o = np.concatenate([src, ao]).astype(np.float32)
     d = np.concatenate([dn, axis]).astype(np.float32)
     r = surf_amd.Renderer(product_scene, W, H)
-    for mode in ((0, 1, 2) if surf_amd.rows_engine() else (0, 1)):
+    for mode in (0, 1):
         r.set_trace_mode(mode)
         gpu = r.trace_closest(o, d)
         cpu = oracle_scene.trace_closest(o, d)
@@ -86,10 +84,8 @@ def test_boundary_rays_bitexact(oracle_scene, product_scene):
             assert np.array_equal(r.trace_any(o, d, tmax), oracle_scene.trace_any(o, d, tmax)), f"mode {mode}"
 
 
-@pytest.mark.parametrize("mode", [0, 1, 2], ids=["lane-per-ray", "wave-lanes-as-planes", "row-per-ray"])
+@pytest.mark.parametrize("mode", [0, 1], ids=["lane-per-ray", "wave-lanes-as-planes"])
 def test_any_hit_bitexact(oracle_scene, product_scene, mode):
-    if mode == 2 and not surf_amd.rows_engine():
-        pytest.skip("four-rows engine not built (make ROWS=1)")
     W = H = 96
     _, (so, sd, st) = oracle_scene.record_rays(W, H, 1, 0, W * H)
     r = surf_amd.Renderer(product_scene, W, H)
@@ -173,21 +169,16 @@ def test_render_64x64x4_bitexact(oracle_scene, product_scene):
     _assert_counts(stats, cnt)
 
 
-@pytest.mark.parametrize("policy,coop,engine", [((0, 0, 16), 60000, "rows"), ((0, 0, 16), 60000, "pair"),
-                                                ((0, 0, 16), 60000, "coop"), ((0, 8, 4), 0, "lanes"),
-                                                ((1 << 30, 0, 8), 1 << 30, "rows"), ((1 << 30, 0, 8), 1 << 30, "pair"),
+@pytest.mark.parametrize("policy,coop,engine", [((0, 0, 16), 60000, "pair"), ((0, 0, 16), 60000, "coop"),
+                                                ((0, 8, 4), 0, "lanes"), ((1 << 30, 0, 8), 1 << 30, "pair"),
                                                 ((1 << 30, 0, 8), 1 << 30, "coop"), ((1, 0, 0), 0, "lanes")],
-                         ids=["staged+rows", "staged+pair", "staged+coop", "8-lanes-staged", "rows-from-start",
-                              "pair-from-start", "coop-from-start", "wavefront-to-end"])
+                         ids=["staged+pair", "staged+coop", "8-lanes-staged", "pair-from-start", "coop-from-start",
+                              "wavefront-to-end"])
 def test_drain_policies_bitexact(oracle_scene, product_scene, policy, coop, engine, monkeypatch):
-    """Every drain schedule (lane stages with survivor hand-off, the four-rows
-    tail with its path queue, the partner-wave tail (k_tail_pair: idle waves
+    """Every drain schedule (lane stages with survivor hand-off, the partner-wave tail (k_tail_pair: idle waves
     trace their sibling's shadow rays), the one-path-per-wave tail, tail from
     the first phase, wavefront to the end) gives the same radiance and event
     counts."""
-    if engine == "rows" and not surf_amd.rows_engine():
-        pytest.skip("four-rows engine not built (make ROWS=1)")
-    monkeypatch.setenv("SURF_TAIL_ROWS", "1" if engine == "rows" else "0")
     monkeypatch.setenv("SURF_TAIL_PAIR", "0" if engine == "coop" else "1")
     r0 = surf_amd.Renderer(product_scene, 96, 64)
     r0.set_tail_policy(*policy)
@@ -302,7 +293,12 @@ def test_connect_light_blas_staging_bitexact(oracle_scene, product_scene, staged
     r.render(F, 0, 0)
     g = r.accumulator()
     st = r.stats()
+    recs, tris = r.debug_connect_staging()
     r.close()
+    if staged == "1":       # the staged walk must have run, on a BLAS deeper than a root leaf
+        assert recs > 8 and tris > 0, (recs, tris)
+    else:
+        assert (recs, tris) == (0, 0)
     oracle.set_zero_cutoff(True)
     try:
         c, cnt, _ = oracle_scene.render(W, H, F)
@@ -712,7 +708,7 @@ def test_general_tlas_bitexact(variant):
         W, H = 64, 48
         r = surf_amd.Renderer(p, W, H, frame_batch=16)
         with pytest.raises(surf_amd.SurfError):
-            r.set_trace_mode(2)           # the four-rows traversal needs a single-leaf TLAS
+            r.set_trace_mode(2)           # modes are 0 (lane) and 1 (wave)
         (eo, ed), (so, sd, st) = o.record_rays(W, H, 0, 0, W * H)
         rng = np.random.default_rng(7)
         ro = rng.uniform([-9, -0.9, -9], [9, 8.9, 9], size=(20000, 3)).astype(np.float32)

@@ -50,7 +50,13 @@ def test_assemble_without_mgpu_library(monkeypatch):
     W, height, shards, block = 9, 37, 3, 4
     rng = np.random.default_rng(5)
     slabs = rng.standard_normal((shards, 13, W, 4)).astype(np.float32)
-    want = surf_amd.assemble_slabs(W, height, shards, block, slabs)
+    # the expected frame from the shard row rule itself, not from assemble_slabs
+    # (which would take the fallback too if the library were missing)
+    want = np.zeros((height, W, 4), np.float32)
+    for k in range(shards):
+        rows = surf_amd.shard_rows(height, surf_amd.ShardSpec(k, shards, block))
+        want[rows] = slabs[k, : len(rows)]
+    assert np.array_equal(surf_amd.assemble_slabs(W, height, shards, block, slabs).view(np.uint32), want.view(np.uint32))
 
     def missing():
         raise OSError("libsurf_mgpu.so not built")
