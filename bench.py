@@ -61,7 +61,7 @@ B_EVENT = {"n_ext": 52, "n_hit": 68, "n_cont": 48, "n_shadow": 88, "n_acc": 24}
 # k_extend's average duration (--kernel-trace --stats) and HBM bytes per launch (FETCH_SIZE x2 +
 # WRITE_SIZE, separate PMC passes, MI355X_MICROARCH.md HBM/rocprofv3 section).
 PMC_SUMMARY = os.path.join(REPO, "profiles", "r{}_{}", "summary.json")
-PMC_ROUNDS = (5, 4)   # the newest committed rocprof summary of the workload (tools/round.sh profiles)
+PMC_ROUNDS = (6, 5, 4)   # the newest committed rocprof summary of the workload (tools/round.sh profiles)
 
 WORKLOADS = {
     "C3": dict(scene="indoor", width=1280, height=720, spp=256, max_segments=0, cpu_row_step=5),
@@ -231,7 +231,7 @@ def rocprof_summary(workload):
     k = next((v for n, v in s.get("kernels", {}).items() if n.startswith("k_extend")), None)
     pmc = s.get("k_extend_pmc", {})
     return {"source": os.path.relpath(path, REPO), "avg_launch_ms": k["avg_us"] / 1e3 if k else None,
-            "traffic": pmc.get("hbm_bytes_per_launch_corrected")}
+            "traffic": pmc.get("hbm_bytes_per_launch_corrected"), "issue": s.get("issue")}
 
 
 def main():
@@ -306,7 +306,8 @@ def main():
     dt = time.perf_counter() - t0
     last_first = (args.warmup + args.steps - 1) * SPP
     st = r.stats()                        # the last render's counts (cleared per step)
-    ev = {k: st[k] for k in ("n_ext", "n_hit", "n_cont", "n_shadow", "n_acc", "n_unocc", "iterations", "tail_paths")}
+    ev = {k: st[k] for k in ("n_ext", "n_hit", "n_cont", "n_shadow", "n_acc", "n_unocc", "iterations", "tail_paths",
+                             "n_ext_wavefront")}
     if dist_on:
         t = torch.tensor([dt], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -360,6 +361,10 @@ def main():
         rp = rocprof_summary(args.workload) if not dist_on else None
         if rp:
             roof["traffic"] = round(rp["traffic"]) if rp["traffic"] else None
+            if rp.get("issue"):
+                # the issue-side bound next to the HBM one (SQ passes of the same command):
+                # k_extend and the drain (k_tail_pair) per ray / per segment
+                roof["issue"] = rp["issue"]
             roof["rocprof"] = {"source": rp["source"], "avg_launch_ms": rp["avg_launch_ms"],
                                "frac": round(bytes_per_launch / (rp["avg_launch_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 6)
                                if rp["avg_launch_ms"] else None}
@@ -419,6 +424,11 @@ def main():
             "gpu_vs_cpu": round(value / cpu["value"], 2) if cpu and cpu.get("value") else None,
             "events_per_sample": per_sample,
             "iterations_per_render": ev["iterations"],
+            # the units of the issue-side roofline (tools/summarize_profile.py): rays k_extend traced and
+            # segments the drain ran, summed over ranks at N > 1
+            "events_per_render": {"n_ext": ev["n_ext"], "n_ext_wavefront": ev["n_ext_wavefront"],
+                                  "drain_segments": ev["n_ext"] - ev["n_ext_wavefront"], "n_shadow": ev["n_shadow"],
+                                  "iterations": ev["iterations"]},
             "tail_paths_per_render": ev["tail_paths"],
             "kernel_ms_profile_pass": kernel_ms,
             "scene_build_s": round(scene_build_s, 3),

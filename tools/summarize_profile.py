@@ -45,6 +45,60 @@ def counter_by_kernel(path, name):
     return {k: list(v.values()) for k, v in per.items()}
 
 
+# Issue-side roofline (VERDICT r5 "What's weak" #4): a traversal kernel is bound by
+# dependent loads and divergent / scalar issue, not by HBM bytes, so the bench
+# line also reports where its waves' cycles go.  Peak VALU issue: one wave64 VALU
+# instruction per 2 cycles per SIMD (SIMD-32, MI355X_MICROARCH.md cycle
+# constants), 1024 SIMDs at the 2.4 GHz peak engine clock.
+SIMDS, CLOCK_HZ = 1024, 2.4e9
+VALU_PEAK = SIMDS * CLOCK_HZ / 2.0          # wave-instructions per second
+SQ_A = ("SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_VMEM_RD", "SQ_INSTS_SMEM", "SQ_INSTS_LDS", "SQ_INSTS_BRANCH",
+        "SQ_INSTS_VALU_FLOPS_FP64")
+SQ_B = ("SQ_WAVE_CYCLES", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_VALU", "SQ_THREAD_CYCLES_VALU",
+        "SQ_BUSY_CYCLES", "SQ_ACTIVE_INST_VMEM")
+
+
+def issue_block(d, ks, bench, kernel, unit_name, units_per_launch):
+    """Per-unit instruction mix and cycle split of `kernel` from the SQ passes."""
+    import os
+    fa, fb = f"{d}/sqa/run_counter_collection.csv", f"{d}/sqb/run_counter_collection.csv"
+    if not (os.path.exists(fa) and os.path.exists(fb)) or not units_per_launch:
+        return None
+    tot = {}
+    launches = 0
+    for path, names in ((fa, SQ_A), (fb, SQ_B)):
+        for n in names:
+            v = counter(path, kernel, n)
+            if v:
+                tot[n] = sum(v)
+                launches = max(launches, len(v))
+    if not launches or "SQ_INSTS_VALU" not in tot:
+        return None
+    units = units_per_launch * launches
+    per = lambda n: round(tot[n] / units, 2) if n in tot else None
+    k = next((v for n, v in ks.items() if n.startswith(kernel)), None)
+    avg_s = k["avg_us"] * 1e-6 if k else None
+    wc = tot.get("SQ_WAVE_CYCLES")
+    blk = {"kernel": kernel, "unit": unit_name, "units_per_launch": round(units_per_launch, 1), "launches": launches,
+           "per_unit": {"valu": per("SQ_INSTS_VALU"), "salu": per("SQ_INSTS_SALU"), "vmem_rd": per("SQ_INSTS_VMEM_RD"),
+                        "smem": per("SQ_INSTS_SMEM"), "lds": per("SQ_INSTS_LDS"), "branch": per("SQ_INSTS_BRANCH"),
+                        "valu_fp64": per("SQ_INSTS_VALU_FLOPS_FP64")},
+           "wave_cycles_split": {"issuing": round(tot["SQ_ACTIVE_INST_ANY"] / wc, 4) if wc and "SQ_ACTIVE_INST_ANY" in tot else None,
+                                 "waitcnt": round(tot["SQ_WAIT_ANY"] / wc, 4) if wc and "SQ_WAIT_ANY" in tot else None,
+                                 "issue_stall": round(tot["SQ_WAIT_INST_ANY"] / wc, 4) if wc and "SQ_WAIT_INST_ANY" in tot else None},
+           "valu_lane_utilization": round(tot["SQ_THREAD_CYCLES_VALU"] / (64.0 * tot["SQ_ACTIVE_INST_VALU"]), 4)
+                                    if tot.get("SQ_ACTIVE_INST_VALU") and "SQ_THREAD_CYCLES_VALU" in tot else None}
+    if avg_s:
+        achieved = tot["SQ_INSTS_VALU"] / launches / avg_s
+        blk["valu_issue"] = {"achieved": round(achieved / 1e9, 3), "peak": round(VALU_PEAK / 1e9, 1), "unit": "G wave-instr/s",
+                             "frac": round(achieved / VALU_PEAK, 4)}
+    split = blk["wave_cycles_split"]
+    if split["waitcnt"] is not None:
+        blk["binding"] = ("memory latency (waves parked on s_waitcnt)" if split["waitcnt"] >= max(split["issuing"], split["issue_stall"])
+                          else "instruction issue" if split["issuing"] >= split["issue_stall"] else "issue dependencies / pipe stalls")
+    return blk
+
+
 def main():
     d, out = sys.argv[1], sys.argv[2]
     cmd = sys.argv[3] if len(sys.argv) > 3 else "python3 bench.py --steps 16 --warmup 1 --no-cpu"
@@ -75,6 +129,16 @@ def main():
         },
         "pmc_by_kernel": by_kernel,
     }
+    # units: bench.py's events of its last render (every render of the command has the same workload)
+    epr = bench.get("events_per_render") or {}
+    iters = epr.get("iterations") or 0
+    issue = {}
+    if iters and epr.get("n_ext_wavefront"):
+        issue["k_extend"] = issue_block(d, ks, bench, "k_extend", "extension ray traced by k_extend", epr["n_ext_wavefront"] / iters)
+    if epr.get("drain_segments"):
+        issue["k_tail_pair"] = issue_block(d, ks, bench, "k_tail_pair", "drain segment (extension ray of the drain)",
+                                           epr["drain_segments"])
+    res["issue"] = {k: v for k, v in issue.items() if v}
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
 
