@@ -50,6 +50,14 @@ constexpr int kBlock = 256;
 #ifndef SURF_TRACE_WAVES
 #define SURF_TRACE_WAVES 2
 #endif
+/* k_extend over one-level records (the L2/MALL-resident BVHs): 6 waves per
+ * SIMD -- 80 VGPRs, a few spills -- beside the 16-bit stack that lets 6 fit
+ * the LDS (C3 k_extend 117 -> 114 ms per render, MEASUREMENTS round 6); the
+ * two-level lane walk (HBM-resident BVHs) keeps SURF_TRACE_WAVES (6 would
+ * spill 96 of its registers) */
+#ifndef SURF_TRACE_WAVES_EXT
+#define SURF_TRACE_WAVES_EXT 6
+#endif
 #ifndef SURF_COOP_WAVES
 #define SURF_COOP_WAVES 4          /* k_tail_coop waves per SIMD (launch bounds; 3: 136 VGPRs, 5: spills) */
 #endif
@@ -1976,8 +1984,10 @@ __global__ __launch_bounds__(kSortThreads) void k_binscatter(const uint8_t* __re
 }
 
 /* ------------------------------------------------------------------ kernels */
-template <bool LDS, bool LW = false>
-__global__ __launch_bounds__(kBlock, SURF_TRACE_WAVES) void k_extend(DevScene S, Pool cur, float4* __restrict__ hitTUV,
+/* SK: the traversal stack's entry type -- 16-bit when every BLAS and TLAS
+ * node index fits (half the stack's LDS: more resident workgroups) */
+template <bool LDS, bool LW = false, typename SK = uint32_t>
+__global__ __launch_bounds__(kBlock, LW ? SURF_TRACE_WAVES : SURF_TRACE_WAVES_EXT) void k_extend(DevScene S, Pool cur, float4* __restrict__ hitTUV,
                                                    uint32_t* __restrict__ hitInst, const Counters* C, int par, uint32_t stackWords,
                                                    const uint32_t* __restrict__ order) {
     extern __shared__ uint32_t lds[];
@@ -1985,15 +1995,16 @@ __global__ __launch_bounds__(kBlock, SURF_TRACE_WAVES) void k_extend(DevScene S,
     /* blocks past the pool exit before staging: a small pool (the drain) costs
      * what it traces, not the fixed grid's LDS staging */
     if (blockIdx.x * blockDim.x >= n) return;
-    const TraceTables Tt = traceTables<LDS>(S, lds, stackWords);
+    /* (stackWords: 32-bit words of the stack; a 16-bit stack uses half of them) */
+    const TraceTables Tt = traceTables<LDS>(S, lds, sizeof(SK) == 2 ? (stackWords + 1u) / 2u : stackWords);
     const uint32_t stride = blockDim.x;
-    uint32_t* stk = lds + threadIdx.x;
+    SK* stk = reinterpret_cast<SK*>(lds) + threadIdx.x;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const uint32_t j = order ? order[i] : i;       /* ray order: hit records stay in order i */
         const float4 o = ldS(&cur.od[2u * (j)]), d = ldS(&cur.od[2u * (j) + 1u]);
         float depth = kFarAway, u = 0.0f, v = 0.0f;
         uint32_t inst = kUnset, prim = kUnset;
-        const bool hit = traceScene<false, LW>(S, Tt, xyz(o), xyz(d), depth, u, v, inst, prim, stk, stride);
+        const bool hit = traceScene<false, LW, false, SK>(S, Tt, xyz(o), xyz(d), depth, u, v, inst, prim, stk, stride);
         stS(&hitTUV[i], make_float4(depth, u, v, u2f(prim)));
         stSu(&hitInst[i], hit ? inst : kUnset);
     }

@@ -75,6 +75,7 @@ struct surf_ctx {
     bool hasScene = false;
     uint32_t extBlock = 128;       /* k_extend workgroup size (SURF_EXTEND_BLOCK=128|256): 128 measured 5 % faster on k_extend */
     bool connectGlobal = false;    /* k_connect reads its tables from global memory (SURF_CONNECT_GLOBAL=1, tuning) */
+    bool extStack16 = true;        /* k_extend's stack in 16-bit entries when node indices fit (SURF_EXT_STACK16=0: 32-bit) */
     bool ldsTables = false;        /* instance/material/light tables fit the per-workgroup LDS copy */
     DevScene S{};
     std::vector<void*> sceneAllocs;
@@ -524,9 +525,14 @@ void launchPhase(surf_ctx* c, int ph, hipEvent_t* ev) {
     if (ev) (void)hipEventRecord(ev[1], s0);
     const Pool cur = c->pool[par];                 /* the pool k_extend / k_shade read */
     /* LW: the two-level records in the lane traversal (HBM-resident BVHs, S.laneW) */
+    /* 16-bit stack entries when every node index fits (the lane walk over
+     * two-level records stacks 32-bit packed leaf references) */
+    const bool sk16 = c->extStack16 && !c->S.laneW && c->nBlasNodes < 65536u && c->tlasNodeCount < 65536u;
     auto extendK = c->S.laneW ? (c->ldsTables ? k_extend<true, true> : k_extend<false, true>)
-                              : (c->ldsTables ? k_extend<true, false> : k_extend<false, false>);
-    hipLaunchKernelGGL(extendK, dim3(c->gridExtend), dim3(c->extBlock), traversalLds(c, c->extBlock) + c->extLdsPad, s0, c->S,
+                              : sk16 ? (c->ldsTables ? k_extend<true, false, uint16_t> : k_extend<false, false, uint16_t>)
+                                     : (c->ldsTables ? k_extend<true, false> : k_extend<false, false>);
+    const size_t extLds = traversalLds(c, c->extBlock) - (sk16 ? (size_t)stackWords(c, c->extBlock) * 2u : 0u);
+    hipLaunchKernelGGL(extendK, dim3(c->gridExtend), dim3(c->extBlock), extLds + c->extLdsPad, s0, c->S,
                        cur, c->hitTUV, c->hitInst, (const Counters*)c->ctr, par, stackWords(c, c->extBlock), order);
     if (ev) (void)hipEventRecord(ev[2], s0);
     if (ovl && ph > 0) (void)hipStreamWaitEvent(s0, c->capEv[2 * (ph - 1) + 1], 0);   /* the previous phase's connect */
@@ -1137,6 +1143,7 @@ int createCtx(int dev, uint32_t w, uint32_t h, std::vector<uint32_t> rows, surf_
         c->sortShadow = e[0] != '2';
     }
     if (const char* e = std::getenv("SURF_CONNECT_GLOBAL")) c->connectGlobal = e[0] != '0';
+    if (const char* e = std::getenv("SURF_EXT_STACK16")) c->extStack16 = e[0] != '0';
     if (const char* e = std::getenv("SURF_KEY")) c->keyMode = e[0] == '0' ? 0u : (e[0] == '1' ? 1u : 2u);
     if (const char* e = std::getenv("SURF_OVERLAP")) c->overlap = e[0] != '0';
     if (const char* e = std::getenv("SURF_LOOP_LAG")) c->loopLag = e[0] != '0';
