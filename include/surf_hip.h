@@ -248,6 +248,10 @@ int surf_debug_issue_order(surf_ctx* ctx, uint32_t* heavy_pixels, uint32_t* perm
  * both 0 when k_connect walked every BLAS from global memory.  No reference
  * counterpart. */
 int surf_debug_connect_staging(surf_ctx* ctx, uint32_t* records, uint32_t* triangles);
+/* Diagnostics: extension rays the capped two-level lane walk left to
+ * k_extend_resume (SURF_LANE_CAP) since the last surf_clear_accumulator.  No
+ * reference counterpart. */
+int surf_debug_lane_resumed(surf_ctx* ctx, uint64_t* rays);
 /* When enabled, per-kernel device times are measured with HIP events on the
  * render stream (slower: disables the graph replay). */
 int surf_set_profiling(surf_ctx* ctx, int enabled);

@@ -197,16 +197,17 @@ struct Counters {
     unsigned long long issued[2];    /* stream chains issued (first samples of (frame, pixel)), per parity */
     unsigned long long limit;        /* host-written issue limit (frame window) */
     unsigned long long baseFrame;    /* absolute frame index of stream frame 0 */
-    unsigned long long ev[16];       /* ext, hit, cont, shadow, acc, unocc, tail paths, capped paths, wavefront ext */
+    unsigned long long ev[16];       /* ext, hit, cont, shadow, acc, unocc, tail paths, capped paths, wavefront ext, resumed rays */
     uint32_t capped[64];             /* sample ids of paths ended by the segment cap, slot blockIdx % 64 (diagnostics, ~0 = none) */
     /* event counts striped over kStripes cache lines (block b adds to stripe
      * b % kStripes): a counter shared by every block of a launch serializes its
      * atomics (~12 ns each, measured); totals = ev + sum over stripes */
     unsigned long long evS[32][16];
     unsigned long long dbg[8];       /* SURF_SEG_TIMING builds: k_tail_coop cycles (extend, shade, connect, segments) */
+    uint32_t resumeN[2];             /* capped lane walks: resume records written by k_extend of parity p (k_regen zeroes) */
 };
 constexpr uint32_t kStripes = 32;    /* frameDone and event-count stripes */
-constexpr int kEvents = 9;           /* event kinds counted (ev / evS index) */
+constexpr int kEvents = 10;          /* event kinds counted (ev / evS index; 9: rays k_extend_resume finished) */
 
 /* A path ended by the segment cap: counted in the event stripes; its sample
  * id is also stored in slot blockIdx % 64 (diagnostics: a racy overwrite, so
@@ -491,9 +492,25 @@ __device__ __forceinline__ WRow wSel(bool c, const WRow& x, const WRow& y) {
     r.a = c ? y.a : x.a; r.b = c ? y.b : x.b; r.c = c ? y.c : x.c; r.d = c ? y.d : x.d;
     return r;
 }
-template <bool ANY, bool FIN>
+/* The capped lane walk (k_extend with a cap; HBM-resident BVHs, S.laneW): a
+ * lane whose BLAS walk has taken its `left` W-record iterations reserves a
+ * resume record and stops, its state here -- the ref it was about to take --
+ * and the refs below it still on its LDS stack; k_extend writes the record and
+ * k_extend_resume finishes the ray one ray per wave from that state (blasWalk2
+ * RES, then the instances after `turn`).  Exact: the wave walk takes the
+ * reference's decisions from the same state (same boxes, order, pruning and
+ * leaf order), so the ray ends as the uncapped lane walk would end it. */
+struct LaneCap {
+    uint32_t left;        /* W-record iterations the lane may still take */
+    uint32_t* n;          /* resume records reserved this phase (Counters::resumeN[par]) */
+    uint32_t cap;         /* records available */
+    uint32_t slot, ref, depthN, turn;
+    bool capped;
+};
+template <bool ANY, bool FIN, bool CAP = false>
 __device__ __forceinline__ bool blasTraceW(const DevScene& S, const TraceInst& I, V3 o, V3 d, V3 rd, float& depth,
-                                           float& hu, float& hv, uint32_t& hprim, uint32_t* stk, uint32_t stride, uint32_t base) {
+                                           float& hu, float& hv, uint32_t& hprim, uint32_t* stk, uint32_t stride, uint32_t base,
+                                           LaneCap* lc = nullptr) {
     const uint32_t nodeOff = I.meta.x;
     const float4* tri = S.tris + 3u * I.meta.y;
     const uint32_t rlf = f2u(I.r0.w), rcnt = f2u(I.r1.w);
@@ -504,6 +521,17 @@ __device__ __forceinline__ bool blasTraceW(const DevScene& S, const TraceInst& I
     uint32_t ref = nodeOff;                 /* the root: its children are tested in its first visit */
     bool any = false;
     for (;;) {
+        if (CAP) {
+            if (lc->left == 0u) {
+                const uint32_t q = atomicAdd(lc->n, 1u);
+                if (q < lc->cap) {
+                    lc->slot = q; lc->ref = ref; lc->depthN = (uint32_t)((sp - bottom) / stride); lc->capped = true;
+                    return any;
+                }
+                lc->left = 0xFFFFFFFFu;     /* no record left: the lane walks on */
+            }
+            --lc->left;
+        }
         uint32_t lf = 0u, cnt = 0u;
         if (ref & kLeafTag) {
             lf = ref & 0xFFFFFFu; cnt = (ref >> 24) & 0x7Fu;
@@ -580,10 +608,10 @@ __device__ __forceinline__ float rowDot(float4 r, float x, float y, float z, flo
     return a + b;
 }
 
-template <bool ANY, bool LW = false, bool STG = false, typename SK = uint32_t>
+template <bool ANY, bool LW = false, bool STG = false, typename SK = uint32_t, bool CAP = false>
 __device__ __forceinline__ bool instanceTrace(const DevScene& S, const TraceInst& I, V3 o, V3 d, float& depth, float& hu,
                                               float& hv, uint32_t& hprim, SK* stk, uint32_t stride, uint32_t base,
-                                              const float4* sN = nullptr) {
+                                              const float4* sN = nullptr, LaneCap* lc = nullptr) {
     V3 oo = mk3(rowDot(I.m0, o.x, o.y, o.z, 1.0f), rowDot(I.m1, o.x, o.y, o.z, 1.0f), rowDot(I.m2, o.x, o.y, o.z, 1.0f));
     if (!I.meta.z) oo = divs(oo, rowDot(I.m3, o.x, o.y, o.z, 1.0f));
     const V3 dd = mk3(rowDot(I.m0, d.x, d.y, d.z, 0.0f), rowDot(I.m1, d.x, d.y, d.z, 0.0f), rowDot(I.m2, d.x, d.y, d.z, 0.0f));
@@ -594,7 +622,7 @@ __device__ __forceinline__ bool instanceTrace(const DevScene& S, const TraceInst
     /* S.finiteBoxes: every BLAS box is finite (checked at upload) */
     const bool fin = S.finiteBoxes && finite3(oo) && finite3(rd);
     if constexpr (LW)
-        return fin ? blasTraceW<ANY, true>(S, I, oo, dd, rd, depth, hu, hv, hprim, stk, stride, base)
+        return fin ? blasTraceW<ANY, true, CAP>(S, I, oo, dd, rd, depth, hu, hv, hprim, stk, stride, base, lc)
                    : blasTraceW<ANY, false>(S, I, oo, dd, rd, depth, hu, hv, hprim, stk, stride, base);
     if (fin) return blasTrace<ANY, true, STG, SK>(S, I, oo, dd, rd, depth, hu, hv, hprim, stk, stride, base, sN);
     return blasTrace<ANY, false, STG, SK>(S, I, oo, dd, rd, depth, hu, hv, hprim, stk, stride, base, sN);
@@ -625,9 +653,12 @@ __device__ __forceinline__ TraceTables traceTables(const DevScene& S, uint32_t* 
 }
 
 /* BvhTLAS::intersect / intersectAny (bvh.cpp:654-778). */
-template <bool ANY, bool LW = false, bool STG = false, typename SK = uint32_t>
+/* CAP (single-leaf TLAS, LW): the walk stops where the lane's cap ran out
+ * (LaneCap); lc->turn is then the instance's place in TLAS order */
+template <bool ANY, bool LW = false, bool STG = false, typename SK = uint32_t, bool CAP = false>
 __device__ __forceinline__ bool traceScene(const DevScene& S, const TraceTables& Tt, V3 o, V3 d, float& depth, float& hu, float& hv,
-                                           uint32_t& hinst, uint32_t& hprim, SK* stk, uint32_t stride, const float4* sN = nullptr) {
+                                           uint32_t& hinst, uint32_t& hprim, SK* stk, uint32_t stride, const float4* sN = nullptr,
+                                           LaneCap* lc = nullptr) {
     bool any = false;
     if (S.tlasLeafCount) {
         /* single-leaf TLAS (the bundled scene): every lane visits the same
@@ -655,12 +686,13 @@ __device__ __forceinline__ bool traceScene(const DevScene& S, const TraceTables&
              * staged triangles are those at S.sbTri0, so both offsets must match) */
             const bool hitI = (STG && !LW && I.meta.x == S.sbNode0 && I.meta.y == S.sbTri0)
                                   ? instanceTrace<ANY, false, true, SK>(S, I, o, d, depth, hu, hv, hprim, stk, stride, 0u, sN)
-                                  : instanceTrace<ANY, LW, false, SK>(S, I, o, d, depth, hu, hv, hprim, stk, stride, 0u);
+                                  : instanceTrace<ANY, LW, false, SK, CAP>(S, I, o, d, depth, hu, hv, hprim, stk, stride, 0u, nullptr, lc);
             if (hitI) {
                 if (ANY) return true;
                 any = true;
                 hinst = ii;
             }
+            if (CAP && lc->capped) { lc->turn = k; return any; }
         }
         return any;
     }
@@ -1315,7 +1347,9 @@ __device__ __forceinline__ bool blasWave(const DevScene& S, const TraceInst& I, 
     /* the 36 planes of rows 0..2: distances, the DPP min/max fold */                                  \
     "v_sub_f32 %[t], %[st], %[oA]\n\t"                                                                 \
     "v_mul_f32 %[t], %[t], %[rdA]\n\t"                                                                 \
-    "s_nop 1\n\t"                                                                                      \
+    /* (the children's counts, for level 2: the two wait states the DPP read needs) */                 \
+    "v_readlane_b32 %[cL], %[st], 29\n\t"                                                              \
+    "v_readlane_b32 %[cR], %[st], 45\n\t"                                                              \
     "v_min_f32_dpp %[t0a], %[t], %[t] quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"             \
     "v_max_f32_dpp %[t1a], %[t], %[t] quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"             \
     "s_nop 1\n\t"                                                                                      \
@@ -1336,53 +1370,48 @@ __device__ __forceinline__ bool blasWave(const DevScene& S, const TraceInst& I, 
     "v_mov_b32_dpp %[mp], %[m0] row_shr:6 row_mask:0xf bank_mask:0xf\n\t"                              \
     "v_cmp_gt_f32_e64 %[g], %[mp], %[m0]\n\t"
 
-/* level 1 (X's children, row 0): none hit -> pop; b0: both hit (far pushed); c: near child */
+/* level 1 (X's children, row 0): none hit -> pop; b0: both hit (far pushed; 256 =
+ * one stack entry, or 0; sb0 its lane mask); c: near child (non-zero: the right) */
 #define SURF_W2_L1A                                                                                    \
     "s_and_b64 %[a], %[h], %[m410]\n\t"                                                                \
     "s_cbranch_scc0 L_pop_%=\n\t"                                                                      \
     "s_cmp_eq_u64 %[a], %[m410]\n\t"                                                                   \
-    "s_cselect_b32 %[b0], 1, 0\n\t"                                                                    \
+    "s_cselect_b32 %[b0], 0x100, 0\n\t"                                                                \
+    "s_cselect_b64 %[sb0], -1, 0\n\t"                                                                  \
     "s_cmp_eq_u64 %[a], 0x400\n\t"                                                                     \
     "s_cselect_b32 %[c], 1, 0\n\t"
 /* closest hit, both hit: the nearer (swap when m0 of box 0 > m0 of box 1) */
 #define SURF_W2_L1ORDER                                                                                \
     "s_bitcmp1_b64 %[g], 10\n\t"                                                                       \
-    "s_cselect_b32 %[idx], 1, 0\n\t"                                                                   \
-    "s_and_b32 %[idx], %[idx], %[b0]\n\t"                                                              \
+    "s_cselect_b32 %[idx], %[b0], 0\n\t"                                                               \
     "s_or_b32 %[c], %[c], %[idx]\n\t"
 /* near child C in row 1 + c; a leaf: push the far child, leave for C; else level 2 (row 1 + c) */
 #define SURF_W2_L2A                                                                                    \
-    "s_lshl_b32 %[k16], %[c], 4\n\t"                                                                   \
-    "s_add_u32 %[k16], %[k16], 16\n\t"                                                                 \
-    "s_add_u32 %[idx], %[k16], 13\n\t"                                                                 \
-    "v_readlane_b32 %[cnt], %[st], %[idx]\n\t"                                                         \
     "s_cmp_lg_u32 %[c], 0\n\t"                                                                         \
     "s_cselect_b64 %[sc], -1, 0\n\t"                                                                   \
+    "s_cselect_b32 %[cnt], %[cR], %[cL]\n\t"                                                           \
+    "s_cselect_b32 %[k16], 32, 16\n\t"                                                                 \
     "s_cmp_lg_u32 %[cnt], 0\n\t"                                                                       \
     "s_cbranch_scc1 L_leafC_%=\n\t"                                                                    \
     "s_lshr_b64 %[tt], %[h], %[k16]\n\t"                                                               \
     "s_and_b64 %[a], %[tt], %[m410]\n\t"                                                               \
     "s_cbranch_scc0 L_miss2_%=\n\t"                                                                    \
     "s_cmp_eq_u64 %[a], %[m410]\n\t"                                                                   \
-    "s_cselect_b32 %[b1], 1, 0\n\t"                                                                    \
+    "s_cselect_b32 %[b1], 0x100, 0\n\t"                                                                \
     "s_cmp_eq_u64 %[a], 0x400\n\t"                                                                     \
     "s_cselect_b32 %[cc], 1, 0\n\t"
 #define SURF_W2_L2ORDER                                                                                \
     "s_lshr_b64 %[tt], %[g], %[k16]\n\t"                                                               \
     "s_bitcmp1_b64 %[tt], 10\n\t"                                                                      \
-    "s_cselect_b32 %[idx], 1, 0\n\t"                                                                   \
-    "s_and_b32 %[idx], %[idx], %[b1]\n\t"                                                              \
+    "s_cselect_b32 %[idx], %[b1], 0\n\t"                                                               \
     "s_or_b32 %[cc], %[cc], %[idx]\n\t"
 /* descend to grandchild n[2c + cc]; push the far child f[1 - c] (b0) and the far
  * grandchild n[2c + 1 - cc] (b1): slot 0 = b0 ? far child : far grandchild,
- * slot 1 = far grandchild, the stack pointer advances by b0 + b1 entries */
+ * slot 1 = far grandchild, the stack pointer advances by b0 + b1 (bytes of
+ * 256-B entries).  SCC on entry: cc != 0 (the last op of L2A / L2ORDER). */
 #define SURF_W2_TAIL                                                                                   \
-    "s_cmp_lg_u32 %[cc], 0\n\t"                                                                        \
     "s_cselect_b64 %[scc], -1, 0\n\t"                                                                  \
-    "s_cmp_lg_u32 %[b0], 0\n\t"                                                                        \
-    "s_cselect_b64 %[sb0], -1, 0\n\t"                                                                  \
     "s_add_u32 %[b1], %[b1], %[b0]\n\t"                                                                \
-    "s_lshl_b32 %[b1], %[b1], 8\n\t"                                                                   \
     "v_add_u32 %[addr], %[sp], %[stk]\n\t"                                                             \
     "s_waitcnt vmcnt(0)\n\t"                                                                           \
     "v_cndmask_b32_e64 %[ta], %[n0], %[n1], %[scc]\n\t"                                                \
@@ -1398,8 +1427,8 @@ __device__ __forceinline__ bool blasWave(const DevScene& S, const TraceInst& I, 
     "s_branch L_chk_%=\n"                                                                              \
     /* C is a leaf: push the far child (when both were hit), leave for C */                            \
     "L_leafC_%=:\n\t"                                                                                  \
-    "s_add_u32 %[idx], %[k16], 12\n\t"                                                                 \
-    "v_readlane_b32 %[lf], %[st], %[idx]\n\t"                                                          \
+    "s_cmp_lg_u32 %[c], 0\n\t"                                                                         \
+    "s_cselect_b32 %[lf], %[lfR], %[lfL]\n\t"                                                          \
     "v_add_u32 %[addr], %[sp], %[stk]\n\t"                                                             \
     "s_waitcnt vmcnt(0)\n\t"                                                                           \
     "v_cndmask_b32_e64 %[t], %[f1], %[f0], %[sc]\n\t"                                                  \
@@ -1439,7 +1468,7 @@ __device__ __forceinline__ bool blasWave(const DevScene& S, const TraceInst& I, 
       [sl0] "=&v"(sl0), [addr] "=&v"(addr), [lfL] "=&s"(lfL), [lfR] "=&s"(lfR), [o0] "=&s"(o0),          \
       [o2] "=&s"(o2), [of] "=&s"(of), [c] "=&s"(c), [cc] "=&s"(cc), [k16] "=&s"(k16), [idx] "=&s"(idx),   \
       [b0] "=&s"(b0), [b1] "=&s"(b1), [h] "=&s"(h), [tt] "=&s"(tt), [g] "=&s"(g), [a] "=&s"(a),           \
-      [sc] "=&s"(sc), [scc] "=&s"(scc), [sb0] "=&s"(sb0)                                                 \
+      [sc] "=&s"(sc), [scc] "=&s"(scc), [sb0] "=&s"(sb0), [cL] "=&s"(cL), [cR] "=&s"(cR)                \
     : [oA] "v"(oA), [rdA] "v"(rdA), [depth] "s"(depth), [rsrc] "s"(rsrc), [loff] "v"(laneOff),            \
       [stk] "v"(stkLane), [m410] "s"(m410)                                                               \
     : "memory", "scc"
@@ -1467,7 +1496,7 @@ template <bool ANY>
 __device__ __forceinline__ void walk2Fin(float& st, uint32_t& spb, uint32_t& lf, uint32_t& cnt, float oA, float rdA, float depth,
                                          surfI4 rsrc, uint32_t laneOff, uint32_t stkLane, uint32_t& nv) {
     float n0, n1, n2, n3, f0, f1, t, t0a, t1a, m0, m1, mp, ta, tb, sl0;
-    uint32_t addr, lfL, lfR, o0, o2, of, c, cc, k16, idx, b0, b1;
+    uint32_t addr, lfL, lfR, o0, o2, of, c, cc, k16, idx, b0, b1, cL, cR;
     unsigned long long h, tt, g = 0, a, sc, scc, sb0;
     const unsigned long long m410 = 0x410ull;
     if (ANY) {
@@ -1520,9 +1549,14 @@ constexpr uint32_t kLeafInW = 3;     /* triangles a two-level leaf record holds 
 /* blasWalk with two-level visits (S.wnodes): the DFS below one BLAS root from
  * W(root) -- its first visit re-tests the root's children at the current
  * depth (the caller's entry test gave the same answer) and their children. */
-template <bool ANY>
+/* RES (k_extend_resume): the walk starts from state st0 with sp0 bytes of W
+ * records already on the LDS stack instead of from W(root); a leaf record it
+ * synthesized for a packed leaf reference carries kSynLeaf in its count and
+ * takes the triangles from memory. */
+constexpr uint32_t kSynLeaf = 0x40000000u;
+template <bool ANY, bool RES = false>
 __device__ __forceinline__ bool blasWalk2(const DevScene& S, uint32_t nodeOff, const float4* tri, V3 o, V3 d, V3 rd, float& depth,
-                                          float& hu, float& hv, uint32_t& hprim, float* rs) {
+                                          float& hu, float& hv, uint32_t& hprim, float* rs, float st0 = 0.0f, uint32_t sp0 = 0u) {
     const uint32_t lane = __lane_id(), l16 = lane & 15u;
     const uint32_t ax = l16 < 12u ? (l16 % 6u) >> 1 : 0u;
     const float oA = pick3(o, ax), rdA = pick3(rd, ax);
@@ -1531,9 +1565,12 @@ __device__ __forceinline__ bool blasWalk2(const DevScene& S, uint32_t nodeOff, c
     const surfI4 rsrc = {(int)(uint32_t)nb, (int)(uint32_t)(nb >> 32), (int)((S.nWnodes - nodeOff) * 192u), 0x00020000};
     const uint32_t laneOff = 4u * lane;
     const uint32_t stkLane = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) float*)rs) + 4u * lane;
-    float st = loadEarly(wb + lane);                                     /* W(root) */
-    waitLoads(st);
-    uint32_t sp = 0u;
+    float st = st0;
+    uint32_t sp = sp0;
+    if (!RES) {
+        st = loadEarly(wb + lane);                                       /* W(root) */
+        waitLoads(st);
+    }
     bool any = false;
     uint32_t nv = 0u;
     if (SURF_WALK_PROFILE) profAdd(2, 1);
@@ -1546,7 +1583,7 @@ __device__ __forceinline__ bool blasWalk2(const DevScene& S, uint32_t nodeOff, c
         if (SURF_WALK_PROFILE) { const unsigned long long tB = profClock(); profAdd(0, tB - tA); tA = tB; }
         if (cnt == 0u) { if (SURF_WALK_PROFILE) profAdd(5, nv); return any; }
         const bool lh = cnt <= kLeafInW ? leafWaveW<ANY>(st, cnt, o, d, depth, hu, hv, hprim)
-                                         : leafWave<ANY>(tri, lf, cnt, o, d, depth, hu, hv, hprim);
+                                         : leafWave<ANY>(tri, lf, RES ? cnt & ~kSynLeaf : cnt, o, d, depth, hu, hv, hprim);
         if (SURF_WALK_PROFILE) { profAdd(1, profClock() - tA); profAdd(3, 1); profAdd(4, cnt); }
         if (lh) {
             if (ANY) { if (SURF_WALK_PROFILE) profAdd(5, nv); return true; }
@@ -1701,9 +1738,12 @@ __device__ __forceinline__ bool traceWaveTlas(const DevScene& S, const TraceTabl
  * applying the depth tests at its turn (a missed instance costs a few
  * readlanes instead of a serial transform, three divisions and a slab test).
  * Any other TLAS: traceWaveTlas. */
+/* firstTurn: instances before that place in TLAS order are skipped (a walk
+ * resumed at an earlier instance, k_extend_resume; single-leaf TLAS only) */
 template <bool ANY, bool W2 = false>
 __device__ __forceinline__ bool traceWave(const DevScene& S, const TraceTables& Tt, V3 o, V3 d, float& depth, float& hu,
-                                          float& hv, uint32_t& hinst, uint32_t& hprim, float* rs, float4* pro, SegStats* ss = nullptr) {
+                                          float& hv, uint32_t& hinst, uint32_t& hprim, float* rs, float4* pro, SegStats* ss = nullptr,
+                                          uint32_t firstTurn = 0u) {
     bool any = false;
     const uint32_t nI = S.tlasLeafCount;
     if (nI == 0u || nI > 64u) return traceWaveTlas<ANY, W2>(S, Tt, o, d, depth, hu, hv, hinst, hprim, rs, pro, ss);
@@ -1722,6 +1762,7 @@ __device__ __forceinline__ bool traceWave(const DevScene& S, const TraceTables& 
     bool keep = false;
     if (lane < nI) keep = waveProEntry(Tt.inst[Tt.order[lane]], o, d, rdw, cullOk, depth, pro + 4u * lane);
     unsigned long long cand = __ballot(keep);
+    if (firstTurn) cand &= firstTurn >= 64u ? 0ull : ~0ull << firstTurn;
     if (SURF_WALK_PROFILE) { const unsigned long long t = profClock(); profAdd(6, t - tP); tP = t; }
     while (cand) {
         const uint32_t k = (uint32_t)(__ffsll((long long)cand) - 1);
@@ -1986,10 +2027,17 @@ __global__ __launch_bounds__(kSortThreads) void k_binscatter(const uint8_t* __re
 /* ------------------------------------------------------------------ kernels */
 /* SK: the traversal stack's entry type -- 16-bit when every BLAS and TLAS
  * node index fits (half the stack's LDS: more resident workgroups) */
-template <bool LDS, bool LW = false, typename SK = uint32_t>
+constexpr uint32_t kResumeHead = 10;   /* words of a resume record before its stack refs (64 words in all) */
+/* CAP (LW, single-leaf TLAS): a lane leaves a ray after capIters W-record
+ * iterations of one BLAS walk (LaneCap) and writes its resume record (64
+ * words: slot i, pool index j, TLAS turn, next ref, stack depth, depth, u, v,
+ * prim, instance, then the stack's refs bottom first); k_extend_resume
+ * finishes those rays one per wave and writes their hit records. */
+template <bool LDS, bool LW = false, typename SK = uint32_t, bool CAP = false>
 __global__ __launch_bounds__(kBlock, LW ? SURF_TRACE_WAVES : SURF_TRACE_WAVES_EXT) void k_extend(DevScene S, Pool cur, float4* __restrict__ hitTUV,
                                                    uint32_t* __restrict__ hitInst, const Counters* C, int par, uint32_t stackWords,
-                                                   const uint32_t* __restrict__ order) {
+                                                   const uint32_t* __restrict__ order, uint32_t capIters, uint32_t* __restrict__ resumeRec,
+                                                   uint32_t resumeCap) {
     extern __shared__ uint32_t lds[];
     const uint32_t n = C->nIn[par];
     /* blocks past the pool exit before staging: a small pool (the drain) costs
@@ -1999,12 +2047,23 @@ __global__ __launch_bounds__(kBlock, LW ? SURF_TRACE_WAVES : SURF_TRACE_WAVES_EX
     const TraceTables Tt = traceTables<LDS>(S, lds, sizeof(SK) == 2 ? (stackWords + 1u) / 2u : stackWords);
     const uint32_t stride = blockDim.x;
     SK* stk = reinterpret_cast<SK*>(lds) + threadIdx.x;
+    LaneCap lc;
+    if (CAP) { lc.n = &const_cast<Counters*>(C)->resumeN[par]; lc.cap = resumeCap; }
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const uint32_t j = order ? order[i] : i;       /* ray order: hit records stay in order i */
         const float4 o = ldS(&cur.od[2u * (j)]), d = ldS(&cur.od[2u * (j) + 1u]);
         float depth = kFarAway, u = 0.0f, v = 0.0f;
         uint32_t inst = kUnset, prim = kUnset;
-        const bool hit = traceScene<false, LW, false, SK>(S, Tt, xyz(o), xyz(d), depth, u, v, inst, prim, stk, stride);
+        if (CAP) { lc.left = capIters; lc.capped = false; }
+        const bool hit = traceScene<false, LW, false, SK, CAP>(S, Tt, xyz(o), xyz(d), depth, u, v, inst, prim, stk, stride, nullptr,
+                                                               CAP ? &lc : nullptr);
+        if (CAP && lc.capped) {
+            uint32_t* r = resumeRec + 64u * (size_t)lc.slot;
+            r[0] = i; r[1] = j; r[2] = lc.turn; r[3] = lc.ref; r[4] = lc.depthN;
+            r[5] = f2u(depth); r[6] = f2u(u); r[7] = f2u(v); r[8] = prim; r[9] = inst;
+            for (uint32_t e = 0; e < lc.depthN; ++e) r[kResumeHead + e] = (uint32_t)stk[e * stride];
+            continue;
+        }
         stS(&hitTUV[i], make_float4(depth, u, v, u2f(prim)));
         stSu(&hitInst[i], hit ? inst : kUnset);
     }
@@ -2583,6 +2642,7 @@ __global__ __launch_bounds__(kBlock) void k_regen(DevCamera cam, Pool nxt, float
         rad[sid] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     }
     if (gid == 0) {
+        C->resumeN[par] = 0u;          /* this phase's k_extend_resume has run */
         C->nIn[nx] = cont + nnew;
         C->issued[nx] = iss + nnew;
         C->app[nx] = 0u;               /* next phase's append cursor */
@@ -3106,6 +3166,65 @@ __global__ __launch_bounds__(64) void k_trace_any_coop(DevScene S, const float* 
     const bool oc = traceWave<true, W2>(S, Tt, ro, rdir, depth, u, v, inst, prim, reinterpret_cast<float*>(lds),
                                     reinterpret_cast<float4*>(lds + stackWords));
     if (threadIdx.x == 0) occ[i] = oc ? 1 : 0;
+}
+
+/* One lane of the W record a capped lane walk's ref stands for: the node's
+ * two-level record, or for a packed leaf reference (kLeafTag) a leaf record
+ * of its leftFirst / count only, marked kSynLeaf (its triangles come from
+ * memory, blasWalk2 RES). */
+__device__ __forceinline__ float wRecordLane(const DevScene& S, uint32_t ref, uint32_t lane) {
+    if (ref & kLeafTag)
+        return u2f(lane == 12u ? (ref & 0xFFFFFFu) : (lane == 13u ? (((ref >> 24) & 0x7Fu) | kSynLeaf) : 0u));
+    return lane < 48u ? S.wnodes[48u * (size_t)ref + lane] : 0.0f;
+}
+
+/* The rays k_extend's capped lane walk left (LaneCap), one per wave: the rest
+ * of the BLAS walk it stopped in, from its resume record (the lane's stack as
+ * W records on the wave's stack, the next ref as the state; blasWalk2 RES),
+ * then the instances after it in TLAS order (traceWave from turn + 1), with
+ * the depth and hit the lane had reached; writes the hit record k_extend
+ * would have written.  Grid-stride over the records of parity par. */
+template <bool LDS>
+__global__ __launch_bounds__(64) void k_extend_resume(DevScene S, Pool cur, float4* __restrict__ hitTUV, uint32_t* __restrict__ hitInst,
+                                                      const Counters* C, int par, uint32_t recWords, const uint32_t* __restrict__ rec,
+                                                      uint32_t recCap) {
+    extern __shared__ uint32_t lds[];
+    const uint32_t n = min(C->resumeN[par], recCap);
+    if (blockIdx.x >= n) return;
+    const TraceTables Tt = coopTrace<LDS>(S, lds, recWords + proWords(S));
+    float* rs = reinterpret_cast<float*>(lds);
+    float4* pro = reinterpret_cast<float4*>(lds + recWords);
+    const uint32_t lane = __lane_id();
+    uint32_t done = 0u;
+    for (uint32_t q = blockIdx.x; q < n; q += gridDim.x, ++done) {
+        const int w = (int)rec[64u * (size_t)q + lane];
+        const uint32_t i = (uint32_t)__builtin_amdgcn_readlane(w, 0), j = (uint32_t)__builtin_amdgcn_readlane(w, 1);
+        const uint32_t turn = (uint32_t)__builtin_amdgcn_readlane(w, 2), ref = (uint32_t)__builtin_amdgcn_readlane(w, 3);
+        const uint32_t nS = (uint32_t)__builtin_amdgcn_readlane(w, 4);
+        float depth = __int_as_float(__builtin_amdgcn_readlane(w, 5));
+        float hu = __int_as_float(__builtin_amdgcn_readlane(w, 6)), hv = __int_as_float(__builtin_amdgcn_readlane(w, 7));
+        uint32_t hprim = (uint32_t)__builtin_amdgcn_readlane(w, 8), hinst = (uint32_t)__builtin_amdgcn_readlane(w, 9);
+        const V3 o = xyz(cur.od[2u * j]), d = xyz(cur.od[2u * j + 1u]);
+        /* the instance the lane stopped in, its object-space ray as instanceTrace forms it */
+        const uint32_t ii = Tt.order[turn];
+        const TraceInst& I = Tt.inst[ii];
+        V3 oo, dd;
+        instanceRay(I, o, d, oo, dd);
+        const V3 rd = mk3(1.0f / dd.x, 1.0f / dd.y, 1.0f / dd.z);
+        const uint32_t nodeOff = (uint32_t)__builtin_amdgcn_readfirstlane((int)I.meta.x);
+        const float4* tri = S.tris + 3u * (uint32_t)__builtin_amdgcn_readfirstlane((int)I.meta.y);
+        for (uint32_t e = 0; e < nS; ++e)
+            rs[64u * e + lane] = wRecordLane(S, (uint32_t)__builtin_amdgcn_readlane(w, (int)(kResumeHead + e)), lane);
+        const float st = wRecordLane(S, ref, lane);
+        bool any = hinst != kUnset;
+        if (blasWalk2<false, true>(S, nodeOff, tri, oo, dd, rd, depth, hu, hv, hprim, rs, st, 256u * nS)) { any = true; hinst = ii; }
+        if (traceWave<false, true>(S, Tt, o, d, depth, hu, hv, hinst, hprim, rs, pro, nullptr, turn + 1u)) any = true;
+        if (lane == 0u) {
+            stS(&hitTUV[i], make_float4(depth, hu, hv, u2f(hprim)));
+            stSu(&hitInst[i], any ? hinst : kUnset);
+        }
+    }
+    if (lane == 0u) atomicAdd(&const_cast<Counters*>(C)->evS[blockIdx.x % kStripes][9], (unsigned long long)done);
 }
 
 /* Diagnostics (surf_debug_segment_cycles): the latency of one drain segment's

@@ -76,6 +76,11 @@ struct surf_ctx {
     uint32_t extBlock = 128;       /* k_extend workgroup size (SURF_EXTEND_BLOCK=128|256): 128 measured 5 % faster on k_extend */
     bool connectGlobal = false;    /* k_connect reads its tables from global memory (SURF_CONNECT_GLOBAL=1, tuning) */
     bool extStack16 = true;        /* k_extend's stack in 16-bit entries when node indices fit (SURF_EXT_STACK16=0: 32-bit) */
+    /* the two-level lane walk (S.laneW) leaves a ray after laneCap W-record
+     * iterations of one BLAS walk to k_extend_resume (SURF_LANE_CAP; 0 = off) */
+    uint32_t laneCap = 0;
+    uint32_t* resumeRec = nullptr;  /* resume records, 64 words each (allocated with the first capped graph) */
+    uint32_t resumeCap = 0;
     bool ldsTables = false;        /* instance/material/light tables fit the per-workgroup LDS copy */
     DevScene S{};
     std::vector<void*> sceneAllocs;
@@ -488,6 +493,15 @@ int ensureWindow(surf_ctx* c, uint64_t frames, uint32_t spp) {
 
 StreamGeom geom(const surf_ctx* c) { return StreamGeom{c->dRows, c->width, c->npx, c->window, c->dPerm}; }
 
+bool waveEligible(const surf_ctx* c);
+/* The capped two-level lane walk (LaneCap): an HBM-resident scene (S.laneW)
+ * whose TLAS is one leaf of <= 64 instances, whose stack fits a resume record
+ * and whose rays k_extend_resume can walk one per wave */
+bool laneCapOn(const surf_ctx* c) {
+    return c->laneCap > 0u && c->S.laneW && c->S.wnodes && c->S.tlasLeafCount >= 1u && c->S.tlasLeafCount <= 64u &&
+           c->stackDepth <= 64u - kResumeHead && waveEligible(c);
+}
+
 /* Counting sort of the pool (which 0) or shadow queue (which 1) of phase par
  * by its 4-bit key into c->order. */
 void launchSort(surf_ctx* c, const uint8_t* key, int par, int which, hipStream_t st, uint32_t* hist, uint32_t* out) {
@@ -528,12 +542,19 @@ void launchPhase(surf_ctx* c, int ph, hipEvent_t* ev) {
     /* 16-bit stack entries when every node index fits (the lane walk over
      * two-level records stacks 32-bit packed leaf references) */
     const bool sk16 = c->extStack16 && !c->S.laneW && c->nBlasNodes < 65536u && c->tlasNodeCount < 65536u;
-    auto extendK = c->S.laneW ? (c->ldsTables ? k_extend<true, true> : k_extend<false, true>)
+    const bool capW = laneCapOn(c);
+    auto extendK = c->S.laneW ? (capW ? (c->ldsTables ? k_extend<true, true, uint32_t, true> : k_extend<false, true, uint32_t, true>)
+                                      : (c->ldsTables ? k_extend<true, true> : k_extend<false, true>))
                               : sk16 ? (c->ldsTables ? k_extend<true, false, uint16_t> : k_extend<false, false, uint16_t>)
                                      : (c->ldsTables ? k_extend<true, false> : k_extend<false, false>);
     const size_t extLds = traversalLds(c, c->extBlock) - (sk16 ? (size_t)stackWords(c, c->extBlock) * 2u : 0u);
     hipLaunchKernelGGL(extendK, dim3(c->gridExtend), dim3(c->extBlock), extLds + c->extLdsPad, s0, c->S,
-                       cur, c->hitTUV, c->hitInst, (const Counters*)c->ctr, par, stackWords(c, c->extBlock), order);
+                       cur, c->hitTUV, c->hitInst, (const Counters*)c->ctr, par, stackWords(c, c->extBlock), order,
+                       c->laneCap, c->resumeRec, c->resumeCap);
+    if (capW)   /* the rays the capped lane walk left, one per wave (LaneCap) */
+        hipLaunchKernelGGL(c->ldsTables ? k_extend_resume<true> : k_extend_resume<false>, dim3(c->cus * 16u), dim3(64), coopLds(c), s0,
+                           c->S, cur, c->hitTUV, c->hitInst, (const Counters*)c->ctr, par, recStackWords(c),
+                           (const uint32_t*)c->resumeRec, c->resumeCap);
     if (ev) (void)hipEventRecord(ev[2], s0);
     if (ovl && ph > 0) (void)hipStreamWaitEvent(s0, c->capEv[2 * (ph - 1) + 1], 0);   /* the previous phase's connect */
     if (c->ldsTables)
@@ -578,8 +599,18 @@ void launchPhase(surf_ctx* c, int ph, hipEvent_t* ev) {
                            c->capacity, geom(c), c->Q);
 }
 
+/* The resume records of the capped lane walk, before the first phase that
+ * may write them: a quarter of the pool's rays may be left to k_extend_resume
+ * per phase (a lane finding no record free walks on) */
+int ensureResume(surf_ctx* c) {
+    if (!laneCapOn(c) || c->resumeRec) return SURF_OK;
+    c->resumeCap = std::max<uint32_t>(c->capacity / 4u, 4096u);
+    return devAlloc(c, c->wfAllocs, &c->resumeRec, (size_t)c->resumeCap * 64u);
+}
+
 int buildGraph(surf_ctx* c) {
     if (c->graphExec) return SURF_OK;
+    if (int rc = ensureResume(c)) return rc;
     for (int shortG = 0; shortG < 2; ++shortG) {
         SURF_CHECK(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
         const int nph = shortG ? kPhasesShort : kPhasesPerGraph;
@@ -810,6 +841,7 @@ int syncAndAccumulate(surf_ctx* c, int phases = 0) {
 int advance(surf_ctx* c, bool shortRun = false) {
     const int phases = shortRun ? kPhasesShort : kPhasesPerGraph;
     if (c->profiling) {
+        if (int rc = ensureResume(c)) return rc;
         for (int ph = 0; ph < phases; ++ph) launchPhase(c, ph, &c->pev[kPhaseEvents * ph]);
         SURF_CHECK(c, hipEventRecord(c->pev[kPhaseEvents * phases], c->stream));
         SURF_CHECK(c, hipGetLastError());
@@ -1144,6 +1176,7 @@ int createCtx(int dev, uint32_t w, uint32_t h, std::vector<uint32_t> rows, surf_
     }
     if (const char* e = std::getenv("SURF_CONNECT_GLOBAL")) c->connectGlobal = e[0] != '0';
     if (const char* e = std::getenv("SURF_EXT_STACK16")) c->extStack16 = e[0] != '0';
+    if (const char* e = std::getenv("SURF_LANE_CAP")) c->laneCap = (uint32_t)std::max(0, std::atoi(e));
     if (const char* e = std::getenv("SURF_KEY")) c->keyMode = e[0] == '0' ? 0u : (e[0] == '1' ? 1u : 2u);
     if (const char* e = std::getenv("SURF_OVERLAP")) c->overlap = e[0] != '0';
     if (const char* e = std::getenv("SURF_LOOP_LAG")) c->loopLag = e[0] != '0';
@@ -2074,6 +2107,16 @@ int surf_trace_any(surf_ctx* c, uint32_t n, const float* o, const float* d, cons
     hipError_t e = hipStreamSynchronize(c->stream);
     freeList(tmp);
     if (e != hipSuccess) return fail(c, SURF_ERR_HIP, std::string("trace_any: ") + hipGetErrorString(e));
+    return SURF_OK;
+}
+
+int surf_debug_lane_resumed(surf_ctx* c, uint64_t* rays) {
+    if (!c || !rays) return SURF_ERR_INVALID;
+    int rc = ensureDrained(c);
+    if (rc) return rc;
+    unsigned long long cur[kEvents] = {};
+    if (c->streamActive && c->hctr) streamEvents(*c->hctr, cur);
+    *rays = c->evBase[9] + cur[9];
     return SURF_OK;
 }
 

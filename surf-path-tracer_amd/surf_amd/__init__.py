@@ -104,6 +104,7 @@ def load() -> C.CDLL:
         "surf_debug_capped": ([P, P, U32, C.POINTER(C.c_uint64)], I32),
         "surf_debug_issue_order": ([P, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)], I32),
         "surf_debug_connect_staging": ([P, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)], I32),
+        "surf_debug_lane_resumed": ([P, C.POINTER(C.c_uint64)], I32),
         "surf_debug_segment_cycles": ([P, P, U32, P], I32),
         "surf_upload_scene": ([P, C.POINTER(SceneDesc)], I32),
         "surf_set_camera": ([P, P], I32),
@@ -129,7 +130,14 @@ def load() -> C.CDLL:
         "surf_ref_sinf": ([F], F), "surf_ref_cosf": ([F], F), "surf_ref_expf": ([F], F),
     }
     for name, (args, res) in sig.items():
-        fn = getattr(lib, name)
+        try:
+            fn = getattr(lib, name)
+        except AttributeError:
+            # a library variant built before a diagnostics entry point existed
+            # (tools/ab.sh SURF_HIP_LIB=...); tests/test_abi.py checks the product exports all
+            if name.startswith("surf_debug_") and os.environ.get("SURF_HIP_LIB"):
+                continue
+            raise
         fn.argtypes = args
         fn.restype = res
     _lib = lib
@@ -385,6 +393,13 @@ class Renderer:
         a, f = C.c_uint32(), C.c_uint32()
         _check(load().surf_debug_issue_order(self._h, C.byref(a), C.byref(f)), "surf_debug_issue_order", self._h)
         return int(a.value), int(f.value)
+
+    def debug_lane_resumed(self):
+        """Extension rays the capped two-level lane walk left to k_extend_resume
+        (SURF_LANE_CAP) since the accumulator was last cleared (surf_debug_lane_resumed)."""
+        n = C.c_uint64()
+        _check(load().surf_debug_lane_resumed(self._h, C.byref(n)), "surf_debug_lane_resumed", self._h)
+        return int(n.value)
 
     def debug_connect_staging(self):
         """(records, triangles) of the emitters' BLAS the last k_connect launch

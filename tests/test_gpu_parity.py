@@ -132,6 +132,37 @@ def test_lane_two_level_walk_bitexact(oracle_scene, monkeypatch):
         p.close()
 
 
+@pytest.mark.parametrize("cap", ["2", "12"])
+def test_lane_walk_cap_resume_bitexact(oracle_scene, monkeypatch, cap):
+    """The capped two-level lane walk (SURF_LANE_CAP): a ray whose BLAS walk
+    takes more than `cap` W-record iterations is finished one ray per wave by
+    k_extend_resume from the lane's state (its next node, its stack, depth and
+    hit so far, then the instances after it).  Forced on the bundled scene
+    (SURF_LANEW=1) with caps small enough that most rays hand over: a render
+    and its event counts equal the oracle's, and rays were resumed."""
+    monkeypatch.setenv("SURF_LANEW", "1")
+    monkeypatch.setenv("SURF_LANE_CAP", cap)
+    p = surf_amd.Scene.indoor()
+    try:
+        W = H = 96
+        r = surf_amd.Renderer(p, W, H)
+        r.render(4, 0, 0)
+        g = r.accumulator()
+        stats = r.stats()
+        resumed = r.debug_lane_resumed()
+        r.close()
+        oracle.set_zero_cutoff(True)
+        try:
+            c, cnt, _ = oracle_scene.render(W, H, 4)
+        finally:
+            oracle.set_zero_cutoff(False)
+        _assert_bitexact(g, c, f"capped lane walk (cap {cap}) 96x96x4")
+        _assert_counts(stats, cnt)
+        assert resumed > 1000, resumed
+    finally:
+        p.close()
+
+
 def _render_both(oracle_scene, product_scene, W, H, frames, first=0, max_seg=0, **kw):
     """GPU render (zero-throughput cutoff on, the product default) against the
     oracle in reference semantics (no cutoff) for radiance, and against the
