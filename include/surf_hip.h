@@ -178,7 +178,11 @@ int surf_set_pool_capacity(surf_ctx* ctx, uint32_t paths);
  * is accumulated in frame order; long Russian-roulette paths of old frames
  * overlap the bulk of newer ones.  A stream longer than the window issues
  * frame f only once frame f - window is accumulated.  Setting it fixes it
- * (must be called before the first render). */
+ * (must be called before the first render).  Several contexts on one device:
+ * each sizes its default ring from the HBM free when its stream starts, so a
+ * context started after another gets a smaller window (and, for a drop-in
+ * loop, a lower throughput) -- fix the window here on each context for
+ * predictable memory and throughput (memory: W * H * 16 B per slot). */
 int surf_set_frame_batch(surf_ctx* ctx, uint32_t frames);
 /* Throughput cutoff (enabled 1 / 0; -1 = automatic, the default: on for
  * streams of 1-sample frames, off for multi-sample frames, whose next sample
@@ -248,9 +252,9 @@ int surf_debug_issue_order(surf_ctx* ctx, uint32_t* heavy_pixels, uint32_t* perm
  * both 0 when k_connect walked every BLAS from global memory.  No reference
  * counterpart. */
 int surf_debug_connect_staging(surf_ctx* ctx, uint32_t* records, uint32_t* triangles);
-/* Diagnostics: extension rays the capped two-level lane walk left to
- * k_extend_resume (SURF_LANE_CAP) since the last surf_clear_accumulator.  No
- * reference counterpart. */
+/* Diagnostics: extension rays the capped lane walk left to k_extend_cont
+ * (SURF_LANE_CAP) since the last surf_clear_accumulator.  No reference
+ * counterpart. */
 int surf_debug_lane_resumed(surf_ctx* ctx, uint64_t* rays);
 /* When enabled, per-kernel device times are measured with HIP events on the
  * render stream (slower: disables the graph replay). */

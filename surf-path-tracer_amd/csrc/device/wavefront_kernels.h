@@ -207,7 +207,7 @@ struct Counters {
     uint32_t resumeN[2];             /* capped lane walks: resume records written by k_extend of parity p (k_regen zeroes) */
 };
 constexpr uint32_t kStripes = 32;    /* frameDone and event-count stripes */
-constexpr int kEvents = 10;          /* event kinds counted (ev / evS index; 9: rays k_extend_resume finished) */
+constexpr int kEvents = 10;          /* event kinds counted (ev / evS index; 9: rays k_extend_cont finished) */
 
 /* A path ended by the segment cap: counted in the event stripes; its sample
  * id is also stored in slot blockIdx % 64 (diagnostics: a racy overwrite, so
@@ -387,15 +387,30 @@ __device__ __forceinline__ bool blasAnyStaged(uint32_t recN, const float4* sR, V
     }
 }
 
+/* The capped lane walk (k_extend with a cap): a lane whose BLAS walk has
+ * taken its `left` iterations (node visits; W-record visits in the two-level
+ * walk) reserves a resume record and stops, its state here -- the node (ref)
+ * it was about to visit -- and the entries below it still on its LDS stack;
+ * k_extend writes the record and k_extend_cont continues the walk from that
+ * state, 64 such rays to a wave.  Exact: the continuation takes the
+ * reference's decisions from the same state (same boxes, order, pruning and
+ * leaf order), so the ray ends as the uncapped walk would end it. */
+struct LaneCap {
+    uint32_t left;        /* iterations the lane may still take */
+    uint32_t ref, depthN, turn;
+    bool capped;
+};
+
 /* FIN: o, rd and every box finite (slabFinite is exact); else the reference's
  * ternary slab with its NaN behaviour. */
 /* STG: the BLAS is the emitters' one staged in LDS (S.sbNode0, sN; any-hit
  * only: blasAnyStaged).  SK: the stack entry type (16-bit when every node
  * index fits). */
-template <bool ANY, bool FIN, bool STG = false, typename SK = uint32_t>
+template <bool ANY, bool FIN, bool STG = false, typename SK = uint32_t, bool CAP = false, bool RES = false>
 __device__ __forceinline__ bool blasTrace(const DevScene& S, const TraceInst& I, V3 o, V3 d, V3 rd, float& depth,
                                           float& hu, float& hv, uint32_t& hprim,
-                                          SK* stk, uint32_t stride, uint32_t base, const float4* sN = nullptr) {
+                                          SK* stk, uint32_t stride, uint32_t base, const float4* sN = nullptr,
+                                          LaneCap* lc = nullptr, uint32_t ref0 = 0u, uint32_t n0 = 0u) {
     const uint32_t nodeOff = I.meta.x;
     const float4* tri = S.tris + 3u * I.meta.y;
     /* root: never box-tested (bvh.cpp:131), only its children are */
@@ -408,7 +423,10 @@ __device__ __forceinline__ bool blasTrace(const DevScene& S, const TraceInst& I,
     SK* sp = bottom;
     uint32_t node;
     bool any = false;
-    {
+    if (RES) {
+        node = ref0;
+        sp = bottom + n0 * stride;
+    } else {
         const float4 r2 = I.r2, r3 = I.r3;
         float dn = boxDist<FIN>(r0, r1, o, rd, depth);
         float df = boxDist<FIN>(r2, r3, o, rd, depth);
@@ -427,6 +445,13 @@ __device__ __forceinline__ bool blasTrace(const DevScene& S, const TraceInst& I,
         }
     }
     for (;;) {
+        if (CAP) {
+            if (lc->left == 0u) {
+                lc->ref = node; lc->depthN = (uint32_t)((sp - bottom) / stride); lc->capped = true;
+                return any;
+            }
+            --lc->left;
+        }
         const float4* nd = S.nodes + 4u * node;
         float4 q0 = nd[0], q1 = nd[1], q2 = nd[2], q3 = nd[3];
         pin(q0); pin(q1); pin(q2); pin(q3);
@@ -492,43 +517,26 @@ __device__ __forceinline__ WRow wSel(bool c, const WRow& x, const WRow& y) {
     r.a = c ? y.a : x.a; r.b = c ? y.b : x.b; r.c = c ? y.c : x.c; r.d = c ? y.d : x.d;
     return r;
 }
-/* The capped lane walk (k_extend with a cap; HBM-resident BVHs, S.laneW): a
- * lane whose BLAS walk has taken its `left` W-record iterations reserves a
- * resume record and stops, its state here -- the ref it was about to take --
- * and the refs below it still on its LDS stack; k_extend writes the record and
- * k_extend_resume finishes the ray one ray per wave from that state (blasWalk2
- * RES, then the instances after `turn`).  Exact: the wave walk takes the
- * reference's decisions from the same state (same boxes, order, pruning and
- * leaf order), so the ray ends as the uncapped lane walk would end it. */
-struct LaneCap {
-    uint32_t left;        /* W-record iterations the lane may still take */
-    uint32_t* n;          /* resume records reserved this phase (Counters::resumeN[par]) */
-    uint32_t cap;         /* records available */
-    uint32_t slot, ref, depthN, turn;
-    bool capped;
-};
-template <bool ANY, bool FIN, bool CAP = false>
+/* RES (k_extend_cont): the walk continues from a capped lane's state -- ref0
+ * next, n0 refs already on the stack -- instead of from the root. */
+template <bool ANY, bool FIN, bool CAP = false, bool RES = false>
 __device__ __forceinline__ bool blasTraceW(const DevScene& S, const TraceInst& I, V3 o, V3 d, V3 rd, float& depth,
                                            float& hu, float& hv, uint32_t& hprim, uint32_t* stk, uint32_t stride, uint32_t base,
-                                           LaneCap* lc = nullptr) {
+                                           LaneCap* lc = nullptr, uint32_t ref0 = 0u, uint32_t n0 = 0u) {
     const uint32_t nodeOff = I.meta.x;
     const float4* tri = S.tris + 3u * I.meta.y;
     const uint32_t rlf = f2u(I.r0.w), rcnt = f2u(I.r1.w);
     if (rcnt != 0u) return leafTestUniform<ANY>(tri, rlf, rcnt, o, d, depth, hu, hv, hprim);
     const float4* W = reinterpret_cast<const float4*>(S.wnodes);
     uint32_t* const bottom = stk + base * stride;
-    uint32_t* sp = bottom;
-    uint32_t ref = nodeOff;                 /* the root: its children are tested in its first visit */
+    uint32_t* sp = RES ? bottom + n0 * stride : bottom;
+    uint32_t ref = RES ? ref0 : nodeOff;    /* the root: its children are tested in its first visit */
     bool any = false;
     for (;;) {
         if (CAP) {
             if (lc->left == 0u) {
-                const uint32_t q = atomicAdd(lc->n, 1u);
-                if (q < lc->cap) {
-                    lc->slot = q; lc->ref = ref; lc->depthN = (uint32_t)((sp - bottom) / stride); lc->capped = true;
-                    return any;
-                }
-                lc->left = 0xFFFFFFFFu;     /* no record left: the lane walks on */
+                lc->ref = ref; lc->depthN = (uint32_t)((sp - bottom) / stride); lc->capped = true;
+                return any;
             }
             --lc->left;
         }
@@ -611,7 +619,26 @@ __device__ __forceinline__ float rowDot(float4 r, float x, float y, float z, flo
 template <bool ANY, bool LW = false, bool STG = false, typename SK = uint32_t, bool CAP = false>
 __device__ __forceinline__ bool instanceTrace(const DevScene& S, const TraceInst& I, V3 o, V3 d, float& depth, float& hu,
                                               float& hv, uint32_t& hprim, SK* stk, uint32_t stride, uint32_t base,
-                                              const float4* sN = nullptr, LaneCap* lc = nullptr) {
+                                              const float4* sN = nullptr, LaneCap* lc = nullptr);
+/* The rest of a capped lane walk's BLAS walk (k_extend_cont): the instance's
+ * object-space ray formed as instanceTrace forms it, then blasTraceW from the
+ * saved ref with the saved refs on the stack (a capped walk was a finite one) */
+template <bool LW, typename SK>
+__device__ __forceinline__ bool instanceResume(const DevScene& S, const TraceInst& I, V3 o, V3 d, float& depth, float& hu, float& hv,
+                                               uint32_t& hprim, SK* stk, uint32_t stride, uint32_t ref0, uint32_t n0) {
+    V3 oo = mk3(rowDot(I.m0, o.x, o.y, o.z, 1.0f), rowDot(I.m1, o.x, o.y, o.z, 1.0f), rowDot(I.m2, o.x, o.y, o.z, 1.0f));
+    if (!I.meta.z) oo = divs(oo, rowDot(I.m3, o.x, o.y, o.z, 1.0f));
+    const V3 dd = mk3(rowDot(I.m0, d.x, d.y, d.z, 0.0f), rowDot(I.m1, d.x, d.y, d.z, 0.0f), rowDot(I.m2, d.x, d.y, d.z, 0.0f));
+    const V3 rd = mk3(1.0f / dd.x, 1.0f / dd.y, 1.0f / dd.z);
+    if constexpr (LW)
+        return blasTraceW<false, true, false, true>(S, I, oo, dd, rd, depth, hu, hv, hprim, stk, stride, 0u, nullptr, ref0, n0);
+    return blasTrace<false, true, false, SK, false, true>(S, I, oo, dd, rd, depth, hu, hv, hprim, stk, stride, 0u, nullptr, nullptr,
+                                                         ref0, n0);
+}
+template <bool ANY, bool LW, bool STG, typename SK, bool CAP>
+__device__ __forceinline__ bool instanceTrace(const DevScene& S, const TraceInst& I, V3 o, V3 d, float& depth, float& hu,
+                                              float& hv, uint32_t& hprim, SK* stk, uint32_t stride, uint32_t base,
+                                              const float4* sN, LaneCap* lc) {
     V3 oo = mk3(rowDot(I.m0, o.x, o.y, o.z, 1.0f), rowDot(I.m1, o.x, o.y, o.z, 1.0f), rowDot(I.m2, o.x, o.y, o.z, 1.0f));
     if (!I.meta.z) oo = divs(oo, rowDot(I.m3, o.x, o.y, o.z, 1.0f));
     const V3 dd = mk3(rowDot(I.m0, d.x, d.y, d.z, 0.0f), rowDot(I.m1, d.x, d.y, d.z, 0.0f), rowDot(I.m2, d.x, d.y, d.z, 0.0f));
@@ -624,7 +651,7 @@ __device__ __forceinline__ bool instanceTrace(const DevScene& S, const TraceInst
     if constexpr (LW)
         return fin ? blasTraceW<ANY, true, CAP>(S, I, oo, dd, rd, depth, hu, hv, hprim, stk, stride, base, lc)
                    : blasTraceW<ANY, false>(S, I, oo, dd, rd, depth, hu, hv, hprim, stk, stride, base);
-    if (fin) return blasTrace<ANY, true, STG, SK>(S, I, oo, dd, rd, depth, hu, hv, hprim, stk, stride, base, sN);
+    if (fin) return blasTrace<ANY, true, STG, SK, CAP>(S, I, oo, dd, rd, depth, hu, hv, hprim, stk, stride, base, sN, lc);
     return blasTrace<ANY, false, STG, SK>(S, I, oo, dd, rd, depth, hu, hv, hprim, stk, stride, base, sN);
 }
 
@@ -655,11 +682,21 @@ __device__ __forceinline__ TraceTables traceTables(const DevScene& S, uint32_t* 
 /* BvhTLAS::intersect / intersectAny (bvh.cpp:654-778). */
 /* CAP (single-leaf TLAS, LW): the walk stops where the lane's cap ran out
  * (LaneCap); lc->turn is then the instance's place in TLAS order */
-template <bool ANY, bool LW = false, bool STG = false, typename SK = uint32_t, bool CAP = false>
+/* RES (closest hit, LW): continue a capped lane's walk -- the instance at
+ * TLAS place lc->turn from lc->ref / lc->depthN (instanceResume), then the
+ * instances after it; any / hinst come in as the lane left them */
+template <bool ANY, bool LW = false, bool STG = false, typename SK = uint32_t, bool CAP = false, bool RES = false>
 __device__ __forceinline__ bool traceScene(const DevScene& S, const TraceTables& Tt, V3 o, V3 d, float& depth, float& hu, float& hv,
                                            uint32_t& hinst, uint32_t& hprim, SK* stk, uint32_t stride, const float4* sN = nullptr,
-                                           LaneCap* lc = nullptr) {
-    bool any = false;
+                                           LaneCap* lc = nullptr, bool any0 = false) {
+    bool any = any0;
+    if (RES) {
+        const uint32_t ii = Tt.order[lc->turn];
+        if (instanceResume<LW, SK>(S, Tt.inst[ii], o, d, depth, hu, hv, hprim, stk, stride, lc->ref, lc->depthN)) {
+            any = true;
+            hinst = ii;
+        }
+    }
     if (S.tlasLeafCount) {
         /* single-leaf TLAS (the bundled scene): every lane visits the same
          * instances in the same order -> wave-uniform loop over LDS records.
@@ -671,7 +708,7 @@ __device__ __forceinline__ bool traceScene(const DevScene& S, const TraceTables&
          * shadow queue is ordered by light and origin cell). */
         const V3 rdw = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
         const bool cullOk = finite3(o) && finite3(rdw);
-        for (uint32_t k = 0; k < S.tlasLeafCount; ++k) {
+        for (uint32_t k = RES ? lc->turn + 1u : 0u; k < S.tlasLeafCount; ++k) {
             const uint32_t ii = Tt.order[k];
             const TraceInst& I = Tt.inst[ii];
             if (cullOk && I.wlo.w != 0.0f) {
@@ -1549,14 +1586,9 @@ constexpr uint32_t kLeafInW = 3;     /* triangles a two-level leaf record holds 
 /* blasWalk with two-level visits (S.wnodes): the DFS below one BLAS root from
  * W(root) -- its first visit re-tests the root's children at the current
  * depth (the caller's entry test gave the same answer) and their children. */
-/* RES (k_extend_resume): the walk starts from state st0 with sp0 bytes of W
- * records already on the LDS stack instead of from W(root); a leaf record it
- * synthesized for a packed leaf reference carries kSynLeaf in its count and
- * takes the triangles from memory. */
-constexpr uint32_t kSynLeaf = 0x40000000u;
-template <bool ANY, bool RES = false>
+template <bool ANY>
 __device__ __forceinline__ bool blasWalk2(const DevScene& S, uint32_t nodeOff, const float4* tri, V3 o, V3 d, V3 rd, float& depth,
-                                          float& hu, float& hv, uint32_t& hprim, float* rs, float st0 = 0.0f, uint32_t sp0 = 0u) {
+                                          float& hu, float& hv, uint32_t& hprim, float* rs) {
     const uint32_t lane = __lane_id(), l16 = lane & 15u;
     const uint32_t ax = l16 < 12u ? (l16 % 6u) >> 1 : 0u;
     const float oA = pick3(o, ax), rdA = pick3(rd, ax);
@@ -1565,12 +1597,9 @@ __device__ __forceinline__ bool blasWalk2(const DevScene& S, uint32_t nodeOff, c
     const surfI4 rsrc = {(int)(uint32_t)nb, (int)(uint32_t)(nb >> 32), (int)((S.nWnodes - nodeOff) * 192u), 0x00020000};
     const uint32_t laneOff = 4u * lane;
     const uint32_t stkLane = (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) float*)rs) + 4u * lane;
-    float st = st0;
-    uint32_t sp = sp0;
-    if (!RES) {
-        st = loadEarly(wb + lane);                                       /* W(root) */
-        waitLoads(st);
-    }
+    float st = loadEarly(wb + lane);                                     /* W(root) */
+    waitLoads(st);
+    uint32_t sp = 0u;
     bool any = false;
     uint32_t nv = 0u;
     if (SURF_WALK_PROFILE) profAdd(2, 1);
@@ -1583,7 +1612,7 @@ __device__ __forceinline__ bool blasWalk2(const DevScene& S, uint32_t nodeOff, c
         if (SURF_WALK_PROFILE) { const unsigned long long tB = profClock(); profAdd(0, tB - tA); tA = tB; }
         if (cnt == 0u) { if (SURF_WALK_PROFILE) profAdd(5, nv); return any; }
         const bool lh = cnt <= kLeafInW ? leafWaveW<ANY>(st, cnt, o, d, depth, hu, hv, hprim)
-                                         : leafWave<ANY>(tri, lf, RES ? cnt & ~kSynLeaf : cnt, o, d, depth, hu, hv, hprim);
+                                         : leafWave<ANY>(tri, lf, cnt, o, d, depth, hu, hv, hprim);
         if (SURF_WALK_PROFILE) { profAdd(1, profClock() - tA); profAdd(3, 1); profAdd(4, cnt); }
         if (lh) {
             if (ANY) { if (SURF_WALK_PROFILE) profAdd(5, nv); return true; }
@@ -1738,12 +1767,9 @@ __device__ __forceinline__ bool traceWaveTlas(const DevScene& S, const TraceTabl
  * applying the depth tests at its turn (a missed instance costs a few
  * readlanes instead of a serial transform, three divisions and a slab test).
  * Any other TLAS: traceWaveTlas. */
-/* firstTurn: instances before that place in TLAS order are skipped (a walk
- * resumed at an earlier instance, k_extend_resume; single-leaf TLAS only) */
 template <bool ANY, bool W2 = false>
 __device__ __forceinline__ bool traceWave(const DevScene& S, const TraceTables& Tt, V3 o, V3 d, float& depth, float& hu,
-                                          float& hv, uint32_t& hinst, uint32_t& hprim, float* rs, float4* pro, SegStats* ss = nullptr,
-                                          uint32_t firstTurn = 0u) {
+                                          float& hv, uint32_t& hinst, uint32_t& hprim, float* rs, float4* pro, SegStats* ss = nullptr) {
     bool any = false;
     const uint32_t nI = S.tlasLeafCount;
     if (nI == 0u || nI > 64u) return traceWaveTlas<ANY, W2>(S, Tt, o, d, depth, hu, hv, hinst, hprim, rs, pro, ss);
@@ -1762,7 +1788,6 @@ __device__ __forceinline__ bool traceWave(const DevScene& S, const TraceTables& 
     bool keep = false;
     if (lane < nI) keep = waveProEntry(Tt.inst[Tt.order[lane]], o, d, rdw, cullOk, depth, pro + 4u * lane);
     unsigned long long cand = __ballot(keep);
-    if (firstTurn) cand &= firstTurn >= 64u ? 0ull : ~0ull << firstTurn;
     if (SURF_WALK_PROFILE) { const unsigned long long t = profClock(); profAdd(6, t - tP); tP = t; }
     while (cand) {
         const uint32_t k = (uint32_t)(__ffsll((long long)cand) - 1);
@@ -2028,13 +2053,16 @@ __global__ __launch_bounds__(kSortThreads) void k_binscatter(const uint8_t* __re
 /* SK: the traversal stack's entry type -- 16-bit when every BLAS and TLAS
  * node index fits (half the stack's LDS: more resident workgroups) */
 constexpr uint32_t kResumeHead = 10;   /* words of a resume record before its stack refs (64 words in all) */
-/* CAP (LW, single-leaf TLAS): a lane leaves a ray after capIters W-record
- * iterations of one BLAS walk (LaneCap) and writes its resume record (64
- * words: slot i, pool index j, TLAS turn, next ref, stack depth, depth, u, v,
- * prim, instance, then the stack's refs bottom first); k_extend_resume
- * finishes those rays one per wave and writes their hit records. */
+/* CAP (single-leaf TLAS): a lane leaves a ray after capIters node visits of
+ * one BLAS walk (W-record visits in the two-level walk; LaneCap) and writes
+ * its resume record (64 words: slot i, pool index j, TLAS turn, next node,
+ * stack depth, depth, u, v, prim, instance, then the stack's entries bottom
+ * first); k_extend_cont finishes those rays and writes their hit records. */
+#ifndef SURF_TRACE_WAVES_CAP
+#define SURF_TRACE_WAVES_CAP SURF_TRACE_WAVES_EXT
+#endif
 template <bool LDS, bool LW = false, typename SK = uint32_t, bool CAP = false>
-__global__ __launch_bounds__(kBlock, LW ? SURF_TRACE_WAVES : SURF_TRACE_WAVES_EXT) void k_extend(DevScene S, Pool cur, float4* __restrict__ hitTUV,
+__global__ __launch_bounds__(kBlock, LW ? SURF_TRACE_WAVES : (CAP ? SURF_TRACE_WAVES_CAP : SURF_TRACE_WAVES_EXT)) void k_extend(DevScene S, Pool cur, float4* __restrict__ hitTUV,
                                                    uint32_t* __restrict__ hitInst, const Counters* C, int par, uint32_t stackWords,
                                                    const uint32_t* __restrict__ order, uint32_t capIters, uint32_t* __restrict__ resumeRec,
                                                    uint32_t resumeCap) {
@@ -2048,7 +2076,6 @@ __global__ __launch_bounds__(kBlock, LW ? SURF_TRACE_WAVES : SURF_TRACE_WAVES_EX
     const uint32_t stride = blockDim.x;
     SK* stk = reinterpret_cast<SK*>(lds) + threadIdx.x;
     LaneCap lc;
-    if (CAP) { lc.n = &const_cast<Counters*>(C)->resumeN[par]; lc.cap = resumeCap; }
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const uint32_t j = order ? order[i] : i;       /* ray order: hit records stay in order i */
         const float4 o = ldS(&cur.od[2u * (j)]), d = ldS(&cur.od[2u * (j) + 1u]);
@@ -2057,8 +2084,17 @@ __global__ __launch_bounds__(kBlock, LW ? SURF_TRACE_WAVES : SURF_TRACE_WAVES_EX
         if (CAP) { lc.left = capIters; lc.capped = false; }
         const bool hit = traceScene<false, LW, false, SK, CAP>(S, Tt, xyz(o), xyz(d), depth, u, v, inst, prim, stk, stride, nullptr,
                                                                CAP ? &lc : nullptr);
+        /* (the records hold a whole pool: every lane that stops has one) */
+        uint32_t slot = 0u;
+        if (CAP) {   /* one atomic per wave, by its first active lane (lanes past the pool have left the loop) */
+            const unsigned long long m = __ballot(lc.capped);
+            const int lead = __ffsll((long long)__ballot(true)) - 1;
+            uint32_t base = 0u;
+            if ((int)__lane_id() == lead && m) base = atomicAdd(&const_cast<Counters*>(C)->resumeN[par], (uint32_t)__popcll(m));
+            slot = (uint32_t)__shfl((int)base, lead) + rankBelow(m);
+        }
         if (CAP && lc.capped) {
-            uint32_t* r = resumeRec + 64u * (size_t)lc.slot;
+            uint32_t* r = resumeRec + 64u * (size_t)slot;
             r[0] = i; r[1] = j; r[2] = lc.turn; r[3] = lc.ref; r[4] = lc.depthN;
             r[5] = f2u(depth); r[6] = f2u(u); r[7] = f2u(v); r[8] = prim; r[9] = inst;
             for (uint32_t e = 0; e < lc.depthN; ++e) r[kResumeHead + e] = (uint32_t)stk[e * stride];
@@ -2067,6 +2103,40 @@ __global__ __launch_bounds__(kBlock, LW ? SURF_TRACE_WAVES : SURF_TRACE_WAVES_EX
         stS(&hitTUV[i], make_float4(depth, u, v, u2f(prim)));
         stSu(&hitInst[i], hit ? inst : kUnset);
     }
+}
+
+/* The second pass of the capped lane walk (LaneCap): each lane takes one
+ * resume record of this phase, puts the capped lane's stack into its own LDS
+ * column and continues that walk (traceScene RES) -- the rays that outlived
+ * the cap, 64 to a wave again -- then writes the hit record k_extend would
+ * have written.  Same traversal code and decisions: exact. */
+template <bool LDS, bool LW, typename SK>
+__global__ __launch_bounds__(kBlock, SURF_TRACE_WAVES) void k_extend_cont(DevScene S, Pool cur, float4* __restrict__ hitTUV,
+                                                                         uint32_t* __restrict__ hitInst, const Counters* C, int par,
+                                                                         uint32_t stackWords, const uint32_t* __restrict__ rec,
+                                                                         uint32_t recCap) {
+    extern __shared__ uint32_t lds[];
+    const uint32_t n = min(C->resumeN[par], recCap);
+    if (blockIdx.x * blockDim.x >= n) return;
+    const TraceTables Tt = traceTables<LDS>(S, lds, sizeof(SK) == 2 ? (stackWords + 1u) / 2u : stackWords);
+    const uint32_t stride = blockDim.x;
+    SK* stk = reinterpret_cast<SK*>(lds) + threadIdx.x;
+    uint32_t done = 0u;
+    for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x, ++done) {
+        const uint32_t* r = rec + 64u * (size_t)q;
+        const uint32_t i = r[0], j = r[1];
+        LaneCap lc;
+        lc.turn = r[2]; lc.ref = r[3]; lc.depthN = r[4];
+        float depth = u2f(r[5]), u = u2f(r[6]), v = u2f(r[7]);
+        uint32_t prim = r[8], inst = r[9];
+        for (uint32_t e = 0; e < lc.depthN; ++e) stk[e * stride] = (SK)r[kResumeHead + e];
+        const float4 o = ldS(&cur.od[2u * j]), d = ldS(&cur.od[2u * j + 1u]);
+        const bool hit = traceScene<false, LW, false, SK, false, true>(S, Tt, xyz(o), xyz(d), depth, u, v, inst, prim, stk, stride,
+                                                                    nullptr, &lc, inst != kUnset);
+        stS(&hitTUV[i], make_float4(depth, u, v, u2f(prim)));
+        stSu(&hitInst[i], hit ? inst : kUnset);
+    }
+    if (done) atomicAdd(&const_cast<Counters*>(C)->evS[blockIdx.x % kStripes][9], (unsigned long long)done);
 }
 
 /* randomOnHemisphereCosineWeighted, surf_math.cpp:116-134 (retry loop for R.N == 0) */
@@ -2642,7 +2712,7 @@ __global__ __launch_bounds__(kBlock) void k_regen(DevCamera cam, Pool nxt, float
         rad[sid] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     }
     if (gid == 0) {
-        C->resumeN[par] = 0u;          /* this phase's k_extend_resume has run */
+        C->resumeN[par] = 0u;          /* this phase's k_extend_cont has run */
         C->nIn[nx] = cont + nnew;
         C->issued[nx] = iss + nnew;
         C->app[nx] = 0u;               /* next phase's append cursor */
@@ -3166,65 +3236,6 @@ __global__ __launch_bounds__(64) void k_trace_any_coop(DevScene S, const float* 
     const bool oc = traceWave<true, W2>(S, Tt, ro, rdir, depth, u, v, inst, prim, reinterpret_cast<float*>(lds),
                                     reinterpret_cast<float4*>(lds + stackWords));
     if (threadIdx.x == 0) occ[i] = oc ? 1 : 0;
-}
-
-/* One lane of the W record a capped lane walk's ref stands for: the node's
- * two-level record, or for a packed leaf reference (kLeafTag) a leaf record
- * of its leftFirst / count only, marked kSynLeaf (its triangles come from
- * memory, blasWalk2 RES). */
-__device__ __forceinline__ float wRecordLane(const DevScene& S, uint32_t ref, uint32_t lane) {
-    if (ref & kLeafTag)
-        return u2f(lane == 12u ? (ref & 0xFFFFFFu) : (lane == 13u ? (((ref >> 24) & 0x7Fu) | kSynLeaf) : 0u));
-    return lane < 48u ? S.wnodes[48u * (size_t)ref + lane] : 0.0f;
-}
-
-/* The rays k_extend's capped lane walk left (LaneCap), one per wave: the rest
- * of the BLAS walk it stopped in, from its resume record (the lane's stack as
- * W records on the wave's stack, the next ref as the state; blasWalk2 RES),
- * then the instances after it in TLAS order (traceWave from turn + 1), with
- * the depth and hit the lane had reached; writes the hit record k_extend
- * would have written.  Grid-stride over the records of parity par. */
-template <bool LDS>
-__global__ __launch_bounds__(64) void k_extend_resume(DevScene S, Pool cur, float4* __restrict__ hitTUV, uint32_t* __restrict__ hitInst,
-                                                      const Counters* C, int par, uint32_t recWords, const uint32_t* __restrict__ rec,
-                                                      uint32_t recCap) {
-    extern __shared__ uint32_t lds[];
-    const uint32_t n = min(C->resumeN[par], recCap);
-    if (blockIdx.x >= n) return;
-    const TraceTables Tt = coopTrace<LDS>(S, lds, recWords + proWords(S));
-    float* rs = reinterpret_cast<float*>(lds);
-    float4* pro = reinterpret_cast<float4*>(lds + recWords);
-    const uint32_t lane = __lane_id();
-    uint32_t done = 0u;
-    for (uint32_t q = blockIdx.x; q < n; q += gridDim.x, ++done) {
-        const int w = (int)rec[64u * (size_t)q + lane];
-        const uint32_t i = (uint32_t)__builtin_amdgcn_readlane(w, 0), j = (uint32_t)__builtin_amdgcn_readlane(w, 1);
-        const uint32_t turn = (uint32_t)__builtin_amdgcn_readlane(w, 2), ref = (uint32_t)__builtin_amdgcn_readlane(w, 3);
-        const uint32_t nS = (uint32_t)__builtin_amdgcn_readlane(w, 4);
-        float depth = __int_as_float(__builtin_amdgcn_readlane(w, 5));
-        float hu = __int_as_float(__builtin_amdgcn_readlane(w, 6)), hv = __int_as_float(__builtin_amdgcn_readlane(w, 7));
-        uint32_t hprim = (uint32_t)__builtin_amdgcn_readlane(w, 8), hinst = (uint32_t)__builtin_amdgcn_readlane(w, 9);
-        const V3 o = xyz(cur.od[2u * j]), d = xyz(cur.od[2u * j + 1u]);
-        /* the instance the lane stopped in, its object-space ray as instanceTrace forms it */
-        const uint32_t ii = Tt.order[turn];
-        const TraceInst& I = Tt.inst[ii];
-        V3 oo, dd;
-        instanceRay(I, o, d, oo, dd);
-        const V3 rd = mk3(1.0f / dd.x, 1.0f / dd.y, 1.0f / dd.z);
-        const uint32_t nodeOff = (uint32_t)__builtin_amdgcn_readfirstlane((int)I.meta.x);
-        const float4* tri = S.tris + 3u * (uint32_t)__builtin_amdgcn_readfirstlane((int)I.meta.y);
-        for (uint32_t e = 0; e < nS; ++e)
-            rs[64u * e + lane] = wRecordLane(S, (uint32_t)__builtin_amdgcn_readlane(w, (int)(kResumeHead + e)), lane);
-        const float st = wRecordLane(S, ref, lane);
-        bool any = hinst != kUnset;
-        if (blasWalk2<false, true>(S, nodeOff, tri, oo, dd, rd, depth, hu, hv, hprim, rs, st, 256u * nS)) { any = true; hinst = ii; }
-        if (traceWave<false, true>(S, Tt, o, d, depth, hu, hv, hinst, hprim, rs, pro, nullptr, turn + 1u)) any = true;
-        if (lane == 0u) {
-            stS(&hitTUV[i], make_float4(depth, hu, hv, u2f(hprim)));
-            stSu(&hitInst[i], any ? hinst : kUnset);
-        }
-    }
-    if (lane == 0u) atomicAdd(&const_cast<Counters*>(C)->evS[blockIdx.x % kStripes][9], (unsigned long long)done);
 }
 
 /* Diagnostics (surf_debug_segment_cycles): the latency of one drain segment's

@@ -76,8 +76,8 @@ struct surf_ctx {
     uint32_t extBlock = 128;       /* k_extend workgroup size (SURF_EXTEND_BLOCK=128|256): 128 measured 5 % faster on k_extend */
     bool connectGlobal = false;    /* k_connect reads its tables from global memory (SURF_CONNECT_GLOBAL=1, tuning) */
     bool extStack16 = true;        /* k_extend's stack in 16-bit entries when node indices fit (SURF_EXT_STACK16=0: 32-bit) */
-    /* the two-level lane walk (S.laneW) leaves a ray after laneCap W-record
-     * iterations of one BLAS walk to k_extend_resume (SURF_LANE_CAP; 0 = off) */
+    /* the lane walk leaves a ray after laneCap node visits of one BLAS walk
+     * to k_extend_cont (SURF_LANE_CAP; 0 = off, the default: measured slower) */
     uint32_t laneCap = 0;
     uint32_t* resumeRec = nullptr;  /* resume records, 64 words each (allocated with the first capped graph) */
     uint32_t resumeCap = 0;
@@ -493,13 +493,10 @@ int ensureWindow(surf_ctx* c, uint64_t frames, uint32_t spp) {
 
 StreamGeom geom(const surf_ctx* c) { return StreamGeom{c->dRows, c->width, c->npx, c->window, c->dPerm}; }
 
-bool waveEligible(const surf_ctx* c);
-/* The capped two-level lane walk (LaneCap): an HBM-resident scene (S.laneW)
- * whose TLAS is one leaf of <= 64 instances, whose stack fits a resume record
- * and whose rays k_extend_resume can walk one per wave */
+/* The capped lane walk (LaneCap): a TLAS of one leaf of <= 64 instances and
+ * a stack that fits a resume record */
 bool laneCapOn(const surf_ctx* c) {
-    return c->laneCap > 0u && c->S.laneW && c->S.wnodes && c->S.tlasLeafCount >= 1u && c->S.tlasLeafCount <= 64u &&
-           c->stackDepth <= 64u - kResumeHead && waveEligible(c);
+    return c->laneCap > 0u && c->S.tlasLeafCount >= 1u && c->S.tlasLeafCount <= 64u && c->stackDepth <= 64u - kResumeHead;
 }
 
 /* Counting sort of the pool (which 0) or shadow queue (which 1) of phase par
@@ -545,16 +542,23 @@ void launchPhase(surf_ctx* c, int ph, hipEvent_t* ev) {
     const bool capW = laneCapOn(c);
     auto extendK = c->S.laneW ? (capW ? (c->ldsTables ? k_extend<true, true, uint32_t, true> : k_extend<false, true, uint32_t, true>)
                                       : (c->ldsTables ? k_extend<true, true> : k_extend<false, true>))
-                              : sk16 ? (c->ldsTables ? k_extend<true, false, uint16_t> : k_extend<false, false, uint16_t>)
-                                     : (c->ldsTables ? k_extend<true, false> : k_extend<false, false>);
+                   : capW ? (sk16 ? (c->ldsTables ? k_extend<true, false, uint16_t, true> : k_extend<false, false, uint16_t, true>)
+                                  : (c->ldsTables ? k_extend<true, false, uint32_t, true> : k_extend<false, false, uint32_t, true>))
+                          : sk16 ? (c->ldsTables ? k_extend<true, false, uint16_t> : k_extend<false, false, uint16_t>)
+                                 : (c->ldsTables ? k_extend<true, false> : k_extend<false, false>);
     const size_t extLds = traversalLds(c, c->extBlock) - (sk16 ? (size_t)stackWords(c, c->extBlock) * 2u : 0u);
     hipLaunchKernelGGL(extendK, dim3(c->gridExtend), dim3(c->extBlock), extLds + c->extLdsPad, s0, c->S,
                        cur, c->hitTUV, c->hitInst, (const Counters*)c->ctr, par, stackWords(c, c->extBlock), order,
                        c->laneCap, c->resumeRec, c->resumeCap);
-    if (capW)   /* the rays the capped lane walk left, one per wave (LaneCap) */
-        hipLaunchKernelGGL(c->ldsTables ? k_extend_resume<true> : k_extend_resume<false>, dim3(c->cus * 16u), dim3(64), coopLds(c), s0,
-                           c->S, cur, c->hitTUV, c->hitInst, (const Counters*)c->ctr, par, recStackWords(c),
-                           (const uint32_t*)c->resumeRec, c->resumeCap);
+    if (capW) {   /* the rays the capped lane walk left, 64 to a wave again (LaneCap) */
+        auto contK = c->S.laneW ? (c->ldsTables ? k_extend_cont<true, true, uint32_t> : k_extend_cont<false, true, uint32_t>)
+                     : sk16 ? (c->ldsTables ? k_extend_cont<true, false, uint16_t> : k_extend_cont<false, false, uint16_t>)
+                            : (c->ldsTables ? k_extend_cont<true, false, uint32_t> : k_extend_cont<false, false, uint32_t>);
+        hipLaunchKernelGGL(contK, dim3(std::min<uint32_t>((c->resumeCap + kBlock - 1) / kBlock, c->cus * 8u)), dim3(kBlock),
+                           traversalLds(c, kBlock) - (sk16 ? (size_t)stackWords(c, kBlock) * 2u : 0u), s0, c->S, cur, c->hitTUV,
+                           c->hitInst, (const Counters*)c->ctr, par, stackWords(c, kBlock), (const uint32_t*)c->resumeRec,
+                           c->resumeCap);
+    }
     if (ev) (void)hipEventRecord(ev[2], s0);
     if (ovl && ph > 0) (void)hipStreamWaitEvent(s0, c->capEv[2 * (ph - 1) + 1], 0);   /* the previous phase's connect */
     if (c->ldsTables)
@@ -600,11 +604,10 @@ void launchPhase(surf_ctx* c, int ph, hipEvent_t* ev) {
 }
 
 /* The resume records of the capped lane walk, before the first phase that
- * may write them: a quarter of the pool's rays may be left to k_extend_resume
- * per phase (a lane finding no record free walks on) */
+ * may write them: one per pool slot (every ray of a phase may stop once) */
 int ensureResume(surf_ctx* c) {
     if (!laneCapOn(c) || c->resumeRec) return SURF_OK;
-    c->resumeCap = std::max<uint32_t>(c->capacity / 4u, 4096u);
+    c->resumeCap = c->capacity;
     return devAlloc(c, c->wfAllocs, &c->resumeRec, (size_t)c->resumeCap * 64u);
 }
 

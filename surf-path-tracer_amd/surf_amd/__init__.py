@@ -395,8 +395,8 @@ class Renderer:
         return int(a.value), int(f.value)
 
     def debug_lane_resumed(self):
-        """Extension rays the capped two-level lane walk left to k_extend_resume
-        (SURF_LANE_CAP) since the accumulator was last cleared (surf_debug_lane_resumed)."""
+        """Extension rays the capped lane walk left to k_extend_cont (SURF_LANE_CAP)
+        since the accumulator was last cleared (surf_debug_lane_resumed)."""
         n = C.c_uint64()
         _check(load().surf_debug_lane_resumed(self._h, C.byref(n)), "surf_debug_lane_resumed", self._h)
         return int(n.value)

@@ -132,15 +132,16 @@ def test_lane_two_level_walk_bitexact(oracle_scene, monkeypatch):
         p.close()
 
 
-@pytest.mark.parametrize("cap", ["2", "12"])
-def test_lane_walk_cap_resume_bitexact(oracle_scene, monkeypatch, cap):
-    """The capped two-level lane walk (SURF_LANE_CAP): a ray whose BLAS walk
-    takes more than `cap` W-record iterations is finished one ray per wave by
-    k_extend_resume from the lane's state (its next node, its stack, depth and
-    hit so far, then the instances after it).  Forced on the bundled scene
-    (SURF_LANEW=1) with caps small enough that most rays hand over: a render
-    and its event counts equal the oracle's, and rays were resumed."""
-    monkeypatch.setenv("SURF_LANEW", "1")
+@pytest.mark.parametrize("walk,cap", [("one-level", "4"), ("one-level", "24"), ("two-level", "2"), ("two-level", "12")])
+def test_lane_walk_cap_resume_bitexact(oracle_scene, monkeypatch, walk, cap):
+    """The capped lane walk (SURF_LANE_CAP): a ray whose BLAS walk takes more
+    than `cap` node visits (W-record visits in the two-level walk, forced on
+    the bundled scene by SURF_LANEW=1) is finished from the lane's state (its
+    next node, its stack, depth and hit so far, then the instances after it)
+    by k_extend_cont, the lane walk again with 64 such rays to a wave.  With
+    caps small enough that many rays hand over: a render and its event counts
+    equal the oracle's, and rays were resumed."""
+    monkeypatch.setenv("SURF_LANEW", "1" if walk == "two-level" else "0")
     monkeypatch.setenv("SURF_LANE_CAP", cap)
     p = surf_amd.Scene.indoor()
     try:

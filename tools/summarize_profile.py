@@ -135,6 +135,12 @@ def main():
     issue = {}
     if iters and epr.get("n_ext_wavefront"):
         issue["k_extend"] = issue_block(d, ks, bench, "k_extend", "extension ray traced by k_extend", epr["n_ext_wavefront"] / iters)
+    if iters and epr.get("n_ext_wavefront"):
+        issue["k_shade"] = issue_block(d, ks, bench, "k_shade", "pool path shaded by k_shade", epr["n_ext_wavefront"] / iters)
+    if iters and epr.get("n_shadow") and epr.get("n_ext"):
+        # the wavefront phases' shadow rays, estimated as the wavefront share of the extension rays
+        issue["k_connect"] = issue_block(d, ks, bench, "k_connect", "shadow ray traced by k_connect (wavefront share, estimated)",
+                                         epr["n_shadow"] * epr["n_ext_wavefront"] / epr["n_ext"] / iters)
     if epr.get("drain_segments"):
         issue["k_tail_pair"] = issue_block(d, ks, bench, "k_tail_pair", "drain segment (extension ray of the drain)",
                                            epr["drain_segments"])
