@@ -5,7 +5,8 @@
 #           slots, MI355X_MICROARCH.md "rocprofv3 PMC slots")
 #   sqa/ sqb/  two SQ passes: instruction mix; issuing / waiting / stalled wave
 #           cycles and VALU lane utilization (the issue-side roofline)
-# then tools/summarize_profile.py writes OUTDIR/summary.json.
+# then tools/summarize_profile.py writes OUTDIR/summary.json, the kernel stats
+# are kept as OUTDIR/kernel_stats.csv and the raw pass directories removed.
 # usage: tools/profile_round.sh OUTDIR [WORKLOAD [STEPS]]
 set -e
 OUT=${1:-gpurun_out/prof}
@@ -27,4 +28,7 @@ timeout -k 10 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_
 timeout -k 10 400 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_BUSY_CYCLES SQ_ACTIVE_INST_VMEM \
     --output-format csv -d "$OUT/sqb" -o run -- python3 $CMD > "$OUT/bench_sqb.json" 2> "$OUT/sqb.err"
 python3 tools/summarize_profile.py "$OUT" "$OUT/summary.json" "python3 $CMD" "$WL" > /dev/null
+# keep the reductions only: the raw per-dispatch CSVs of five passes exceed what a gpurun call brings back
+cp "$OUT/trace/run_kernel_stats.csv" "$OUT/kernel_stats.csv"
+rm -rf "$OUT/trace" "$OUT/fetch" "$OUT/write" "$OUT/sqa" "$OUT/sqb"
 echo done

@@ -145,6 +145,17 @@ def main():
         issue["k_tail_pair"] = issue_block(d, ks, bench, "k_tail_pair", "drain segment (extension ray of the drain)",
                                            epr["drain_segments"])
     res["issue"] = {k: v for k, v in issue.items() if v}
+    # every kernel's SQ counter totals over the command (the raw passes are not committed)
+    import os
+    sq = {}
+    for path, names in ((f"{d}/sqa/run_counter_collection.csv", SQ_A), (f"{d}/sqb/run_counter_collection.csv", SQ_B)):
+        if not os.path.exists(path):
+            continue
+        for n in names:
+            for k, v in counter_by_kernel(path, n).items():
+                sq.setdefault(k, {"launches": len(v)})[n] = sum(v)
+    if sq:
+        res["sq_totals_by_kernel"] = sq
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
 
