@@ -1865,7 +1865,13 @@ __device__ __forceinline__ void blockCount(Counters* C, const int (&idx)[N], con
 constexpr uint32_t kBins = 64;
 constexpr uint32_t kSortBlocks = 256;
 constexpr uint32_t kSortUnroll = 16;   /* keys per thread in flight in k_bincount / k_binscatter */
-constexpr uint32_t kSortThreads = 1024; /* threads per k_bincount / k_binscatter block (4 waves per SIMD) */
+/* threads per k_bincount / k_binscatter / k_regen_count block: 256 -- four
+ * waves, which find room beside the concurrent k_connect where a 1024-thread
+ * workgroup (16 waves on one CU) waits for a CU to empty (MEASUREMENTS r6) */
+#ifndef SURF_SORT_THREADS
+#define SURF_SORT_THREADS 256
+#endif
+constexpr uint32_t kSortThreads = SURF_SORT_THREADS;
 #ifndef SURF_SORT_FUSED_SCAN
 #define SURF_SORT_FUSED_SCAN 1          /* k_binscatter scans the counts itself (no k_binscan launch) */
 #endif
@@ -2660,6 +2666,71 @@ __global__ __launch_bounds__(kBlock, STG ? 5 : SURF_TRACE_WAVES) void k_connect(
     blockCount<2>(C, {5, 4}, {cUn, cUn});
 }
 
+/* What k_regen issues in phase par: chains [iss, iss + nnew) into pool slots
+ * [cont, cont + nnew) of pool[par^1], and where the stream's permuted head ends. */
+struct RegenPlan {
+    uint32_t cont, nnew, lp0, nA, nB;
+    unsigned long long iss, base, f0, endA, endP;
+    uint32_t spp;
+};
+__device__ __forceinline__ RegenPlan regenPlan(const Counters* C, int par, uint32_t capacity, const StreamGeom& G) {
+    RegenPlan R;
+    R.cont = C->app[par];
+    R.iss = C->issued[par];
+    const unsigned long long lim = C->limit;
+    R.base = C->baseFrame;
+    R.spp = C->spp;
+    const uint32_t room = capacity - R.cont;
+    const unsigned long long left = lim > R.iss ? lim - R.iss : 0ull;
+    R.nnew = (unsigned long long)room < left ? room : (uint32_t)left;
+    /* frame / pixel of the first new chain, then step without 64-bit divisions */
+    R.f0 = R.iss / G.npx;
+    R.lp0 = (uint32_t)(R.iss - R.f0 * G.npx);
+    /* the permuted head of the stream (surf_hip.hip classifyPixels) */
+    R.nA = C->permA; R.nB = G.npx - C->permA;
+    R.endA = (unsigned long long)R.nA * C->permFrames; R.endP = (unsigned long long)G.npx * C->permFrames;
+    return R;
+}
+/* The k-th new chain's first sample into pool slot cont + k. */
+__device__ __forceinline__ void regenSample(const DevCamera& cam, const Pool& nxt, float4* __restrict__ rad, const StreamGeom& G,
+                                            const RegenPlan& R, uint32_t k) {
+    uint32_t lp;
+    unsigned long long f;
+    if (R.iss + k < R.endP) {
+        const unsigned long long s = R.iss + k;
+        if (s < R.endA) { f = s / R.nA; lp = G.perm[(uint32_t)(s - f * R.nA)]; }
+        else { const unsigned long long j = s - R.endA; f = j / R.nB; lp = G.perm[R.nA + (uint32_t)(j - f * R.nB)]; }
+    } else {
+        lp = R.lp0 + k;
+        const uint32_t df = lp / G.npx;
+        lp -= df * G.npx;
+        f = R.f0 + df;
+    }
+    const unsigned long long pass = f * R.spp;
+    const uint32_t slot = (uint32_t)(pass % G.window);
+    const uint32_t rowi = lp / G.width;
+    const uint32_t p = (lp - rowi * G.width) + G.rows[rowi] * G.width;
+    const uint32_t sid = slot * G.npx + lp;
+    float4 o4, d4, T4;
+    cameraSample(cam, G, lp, sid, initSeed(p + (uint32_t)(R.base + pass) * 1799u), o4, d4, T4);
+    const uint32_t slotIdx = R.cont + k;
+    stS(&nxt.od[2u * (slotIdx)], o4);
+    stS(&nxt.od[2u * (slotIdx) + 1u], d4);
+    stS(&nxt.T[slotIdx], T4);
+    nxt.key[slotIdx] = (uint8_t)(kBins - 1u);                      /* camera rays */
+    rad[sid] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+}
+/* The counters of the phase after par (one thread). */
+__device__ __forceinline__ void regenCounters(Counters* C, int par, const RegenPlan& R) {
+    const int nx = par ^ 1;
+    C->resumeN[par] = 0u;          /* this phase's k_extend_cont has run */
+    C->nIn[nx] = R.cont + R.nnew;
+    C->issued[nx] = R.iss + R.nnew;
+    C->app[nx] = 0u;               /* next phase's append cursor */
+    C->ev[0] += R.cont + R.nnew;   /* extension rays of the next phase */
+    C->ev[8] += R.cont + R.nnew;   /* ... traced by k_extend unless the drain takes the pool */
+}
+
 /* Fills pool[par^1] after the continuing paths, up to capacity and the issue
  * limit, with the first sample of the next (frame, pixel) chains in issue
  * order: frame f's first sample is stream pass f * spp, seeded
@@ -2667,58 +2738,39 @@ __global__ __launch_bounds__(kBlock, STG ? 5 : SURF_TRACE_WAVES) void k_connect(
  * the sample count before the stream). */
 __global__ __launch_bounds__(kBlock) void k_regen(DevCamera cam, Pool nxt, float4* __restrict__ rad, Counters* C, int par,
                                                   uint32_t capacity, StreamGeom G, ShadowQ Q) {
-    const int nx = par ^ 1;
-    const uint32_t cont = C->app[par];
-    const unsigned long long iss = C->issued[par];
-    const unsigned long long lim = C->limit;
-    const unsigned long long base = C->baseFrame;
-    const uint32_t spp = C->spp;
-    const uint32_t room = capacity - cont;
-    const unsigned long long left = lim > iss ? lim - iss : 0ull;
-    const uint32_t nnew = (unsigned long long)room < left ? room : (uint32_t)left;
+    const RegenPlan R = regenPlan(C, par, capacity, G);
     const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
-    if (gid < kShSegs) *shCursor(Q, nx, gid) = 0u;      /* the next phase's shadow-queue cursors */
-    /* frame / pixel of the first new chain, then step without 64-bit divisions */
-    const unsigned long long f0 = iss / G.npx;
-    const uint32_t lp0 = (uint32_t)(iss - f0 * G.npx);
-    /* the permuted head of the stream (surf_hip.hip classifyPixels) */
-    const uint32_t nA = C->permA, nB = G.npx - C->permA;
-    const unsigned long long endA = (unsigned long long)nA * C->permFrames, endP = (unsigned long long)G.npx * C->permFrames;
-    for (uint32_t k = gid; k < nnew; k += gridDim.x * blockDim.x) {
-        uint32_t lp;
-        unsigned long long f;
-        if (iss + k < endP) {
-            const unsigned long long s = iss + k;
-            if (s < endA) { f = s / nA; lp = G.perm[(uint32_t)(s - f * nA)]; }
-            else { const unsigned long long j = s - endA; f = j / nB; lp = G.perm[nA + (uint32_t)(j - f * nB)]; }
-        } else {
-            lp = lp0 + k;
-            const uint32_t df = lp / G.npx;
-            lp -= df * G.npx;
-            f = f0 + df;
-        }
-        const unsigned long long pass = f * spp;
-        const uint32_t slot = (uint32_t)(pass % G.window);
-        const uint32_t rowi = lp / G.width;
-        const uint32_t p = (lp - rowi * G.width) + G.rows[rowi] * G.width;
-        const uint32_t sid = slot * G.npx + lp;
-        float4 o4, d4, T4;
-        cameraSample(cam, G, lp, sid, initSeed(p + (uint32_t)(base + pass) * 1799u), o4, d4, T4);
-        const uint32_t slotIdx = cont + k;
-        stS(&nxt.od[2u * (slotIdx)], o4);
-        stS(&nxt.od[2u * (slotIdx) + 1u], d4);
-        stS(&nxt.T[slotIdx], T4);
-        nxt.key[slotIdx] = (uint8_t)(kBins - 1u);                      /* camera rays */
-        rad[sid] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (gid < kShSegs) *shCursor(Q, par ^ 1, gid) = 0u;      /* the next phase's shadow-queue cursors */
+    for (uint32_t k = gid; k < R.nnew; k += gridDim.x * blockDim.x) regenSample(cam, nxt, rad, G, R, k);
+    if (gid == 0) regenCounters(C, par, R);
+}
+
+/* k_regen fused with the next phase's pool count (the default; SURF_REGEN_COUNT=0:
+ * k_regen + k_bincount): one workgroup per sort chunk (k_binscatter's
+ * sortChunk over the next pool's cont + nnew paths), which counts the
+ * continuations' keys of its chunk and generates the chunk's new camera
+ * samples (key kBins - 1), then writes the chunk's bin counts where k_bincount
+ * would -- so the next phase's sort is k_binscatter alone, and one kernel
+ * instead of two waits for CU slots beside k_connect. */
+__global__ __launch_bounds__(kSortThreads) void k_regen_count(DevCamera cam, Pool nxt, float4* __restrict__ rad, Counters* C, int par,
+                                                             uint32_t capacity, StreamGeom G, ShadowQ Q, uint32_t* __restrict__ hist) {
+    __shared__ uint32_t h[kBins];
+    if (threadIdx.x < kBins) h[threadIdx.x] = 0u;
+    const RegenPlan R = regenPlan(C, par, capacity, G);
+    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid < kShSegs) *shCursor(Q, par ^ 1, gid) = 0u;      /* the next phase's shadow-queue cursors */
+    __syncthreads();
+    uint32_t a, b;
+    sortChunk(R.cont + R.nnew, a, b);
+    uint32_t cam0 = 0u;
+    for (uint32_t i = a + threadIdx.x; i < b; i += blockDim.x) {
+        if (i < R.cont) atomicAdd(&h[nxt.key[i]], 1u);
+        else { regenSample(cam, nxt, rad, G, R, i - R.cont); ++cam0; }
     }
-    if (gid == 0) {
-        C->resumeN[par] = 0u;          /* this phase's k_extend_cont has run */
-        C->nIn[nx] = cont + nnew;
-        C->issued[nx] = iss + nnew;
-        C->app[nx] = 0u;               /* next phase's append cursor */
-        C->ev[0] += cont + nnew;     /* extension rays of the next phase */
-        C->ev[8] += cont + nnew;     /* ... traced by k_extend unless the drain takes the pool */
-    }
+    if (cam0) atomicAdd(&h[kBins - 1u], cam0);
+    __syncthreads();
+    if (threadIdx.x < kBins) hist[threadIdx.x * gridDim.x + blockIdx.x] = h[threadIdx.x];
+    if (gid == 0) regenCounters(C, par, R);
 }
 
 /* Finishes the last paths of the stream: one kernel, each active lane runs its

@@ -76,6 +76,7 @@ struct surf_ctx {
     uint32_t extBlock = 128;       /* k_extend workgroup size (SURF_EXTEND_BLOCK=128|256): 128 measured 5 % faster on k_extend */
     bool connectGlobal = false;    /* k_connect reads its tables from global memory (SURF_CONNECT_GLOBAL=1, tuning) */
     bool extStack16 = true;        /* k_extend's stack in 16-bit entries when node indices fit (SURF_EXT_STACK16=0: 32-bit) */
+    bool regenCount = true;        /* k_regen_count fills the next pool and counts it for its sort (SURF_REGEN_COUNT=0: k_regen + k_bincount) */
     /* the lane walk leaves a ray after laneCap node visits of one BLAS walk
      * to k_extend_cont (SURF_LANE_CAP; 0 = off, the default: measured slower) */
     uint32_t laneCap = 0;
@@ -501,8 +502,9 @@ bool laneCapOn(const surf_ctx* c) {
 
 /* Counting sort of the pool (which 0) or shadow queue (which 1) of phase par
  * by its 4-bit key into c->order. */
-void launchSort(surf_ctx* c, const uint8_t* key, int par, int which, hipStream_t st, uint32_t* hist, uint32_t* out) {
-    hipLaunchKernelGGL(k_bincount, dim3(kSortBlocks), dim3(kSortThreads), 0, st, key, (const Counters*)c->ctr, par, which, hist);
+void launchSort(surf_ctx* c, const uint8_t* key, int par, int which, hipStream_t st, uint32_t* hist, uint32_t* out, bool count = true) {
+    if (count)   /* (else k_regen_count left the counts) */
+        hipLaunchKernelGGL(k_bincount, dim3(kSortBlocks), dim3(kSortThreads), 0, st, key, (const Counters*)c->ctr, par, which, hist);
 #if !SURF_SORT_FUSED_SCAN
     hipLaunchKernelGGL(k_binscan, dim3(1), dim3(1024), 0, st, hist, kBins * kSortBlocks);
 #endif
@@ -529,10 +531,20 @@ void launchPhase(surf_ctx* c, int ph, hipEvent_t* ev) {
         (void)hipMemcpyAsync(&c->hPhaseN[ph], &c->ctr->nIn[par], sizeof(uint32_t), hipMemcpyDeviceToHost, s0);
     if (ev) (void)hipEventRecord(ev[0], s0);
     const uint32_t* order = nullptr;
-    if (c->sortRays && c->sortPool) {
-        launchSort(c, c->pool[par].key, par, 0, s0, c->binHist, c->order);
+    const bool sortOn = c->sortRays && c->sortPool;
+    const bool fused = sortOn && c->regenCount;    /* k_regen_count counts the next pool for its sort */
+    if (sortOn) {
+        launchSort(c, c->pool[par].key, par, 0, s0, c->binHist, c->order, !fused);
         order = c->order;
     }
+    auto regen = [&]() {
+        if (fused)
+            hipLaunchKernelGGL(k_regen_count, dim3(kSortBlocks), dim3(kSortThreads), 0, s0, c->cam, c->pool[par ^ 1], c->rad, c->ctr,
+                               par, c->capacity, geom(c), c->Q, c->binHist);
+        else
+            hipLaunchKernelGGL(k_regen, dim3(c->gridRegen), dim3(kBlock), 0, s0, c->cam, c->pool[par ^ 1], c->rad, c->ctr, par,
+                               c->capacity, geom(c), c->Q);
+    };
     if (ev) (void)hipEventRecord(ev[1], s0);
     const Pool cur = c->pool[par];                 /* the pool k_extend / k_shade read */
     /* LW: the two-level records in the lane traversal (HBM-resident BVHs, S.laneW) */
@@ -572,9 +584,7 @@ void launchPhase(surf_ctx* c, int ph, hipEvent_t* ev) {
     if (ev) (void)hipEventRecord(ev[3], s0);
     /* k_regen before the fork (SURF_REGEN_FIRST): alone it takes ~17 us, beside
      * k_connect it waits for CU slots on the next phase's critical path */
-    if (c->regenFirst)
-        hipLaunchKernelGGL(k_regen, dim3(c->gridRegen), dim3(kBlock), 0, s0, c->cam, c->pool[par ^ 1], c->rad, c->ctr, par,
-                           c->capacity, geom(c), c->Q);
+    if (c->regenFirst) regen();
     if (ovl) {
         (void)hipEventRecord(c->capEv[2 * ph], s0);
         (void)hipStreamWaitEvent(s1, c->capEv[2 * ph], 0);
@@ -598,9 +608,7 @@ void launchPhase(surf_ctx* c, int ph, hipEvent_t* ev) {
     hipLaunchKernelGGL(connectK, dim3(c->gridConnect), dim3(kBlock), connectLds, s1, c->S, c->Q, c->rad, c->ctr, par, sw);
     if (ovl) (void)hipEventRecord(c->capEv[2 * ph + 1], s1);
     if (ev) (void)hipEventRecord(ev[5], s0);
-    if (!c->regenFirst)
-        hipLaunchKernelGGL(k_regen, dim3(c->gridRegen), dim3(kBlock), 0, s0, c->cam, c->pool[par ^ 1], c->rad, c->ctr, par,
-                           c->capacity, geom(c), c->Q);
+    if (!c->regenFirst) regen();
 }
 
 /* The resume records of the capped lane walk, before the first phase that
@@ -1179,6 +1187,7 @@ int createCtx(int dev, uint32_t w, uint32_t h, std::vector<uint32_t> rows, surf_
     }
     if (const char* e = std::getenv("SURF_CONNECT_GLOBAL")) c->connectGlobal = e[0] != '0';
     if (const char* e = std::getenv("SURF_EXT_STACK16")) c->extStack16 = e[0] != '0';
+    if (const char* e = std::getenv("SURF_REGEN_COUNT")) c->regenCount = e[0] != '0';
     if (const char* e = std::getenv("SURF_LANE_CAP")) c->laneCap = (uint32_t)std::max(0, std::atoi(e));
     if (const char* e = std::getenv("SURF_KEY")) c->keyMode = e[0] == '0' ? 0u : (e[0] == '1' ? 1u : 2u);
     if (const char* e = std::getenv("SURF_OVERLAP")) c->overlap = e[0] != '0';
