@@ -186,7 +186,7 @@ struct surf_ctx {
     bool sortRays = true;          /* order each phase's rays by start instance (SURF_SORT=0: off) */
     bool sortPool = true;
     bool sortShadow = true;        /* ... and the shadow queue by light (SURF_SORT=2: pool only, 3: shadow queue only) */
-    /* ray order (k_bincount / k_binscan / k_binscatter each phase) */
+    /* ray order: counts from k_regen_count (or k_bincount), then k_binscatter each phase */
     uint32_t* order = nullptr;
     uint32_t* binHist = nullptr;
     /* connect overlapped with the next phase's regen / pool sort / extend
