@@ -29,7 +29,14 @@ using namespace surfdev;
 
 namespace {
 
-constexpr int kPhasesPerGraph = 8;          /* even: parity returns to 0 after a replay */
+/* phases per full replay: 16 (C3 515.2 / 513.9 → 520.7 / 520.0 Mrays/s against
+ * 8 on one box, C4, the drop-in loop and the 8-shard projection unchanged;
+ * MEASUREMENTS r6) */
+#ifndef SURF_PHASES_GRAPH
+#define SURF_PHASES_GRAPH 16
+#endif
+constexpr int kPhasesPerGraph = SURF_PHASES_GRAPH;   /* even: parity returns to 0 after a replay */
+static_assert(kPhasesPerGraph % 2 == 0, "even: parity returns to 0 after a replay");
 /* The short graph: a render call with at most one frame left to issue (the
  * drop-in loop's 1-spp render(), main.cpp:381-446) replays 4 phases per host
  * poll instead of 8, so a per-frame call does not keep the pool a quarter full
@@ -805,7 +812,7 @@ int consumeSnap(surf_ctx* c) {
     SURF_CHECK(c, hipEventSynchronize(sn.ev));
     const uint64_t before = c->hctr->issued[0];
     std::memcpy(c->hctr, sn.h, sizeof(Counters));
-    /* per phase (a replay is 8 or kPhasesShort phases), and only from a replay
+    /* per phase (a replay is kPhasesPerGraph or kPhasesShort phases), and only from a replay
      * that issued under its limit the whole time: a starved one undercounts */
     if (sn.phases > 0 && c->hctr->issued[0] > before && c->hctr->issued[0] < c->hctr->limit)
         c->issuePerPhase = (c->hctr->issued[0] - before) / (uint64_t)sn.phases;
